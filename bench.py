@@ -1,0 +1,221 @@
+#!/usr/bin/env python3
+"""Benchmark: stereo pairs/s (+ Mpix·disp/s) on the BASELINE.json headline
+workload — KITTI 1242×375, D=128, Census 9×7 + 8-path SGM, WTA + uniqueness
++ sub-pixel + left/right check + 3×3 median — on 1..8 MI355X, one process per
+GPU (launched by torch.distributed.run for N > 1).
+
+A step = every rank runs the hot path over its batch of ``--pairs-per-gpu``
+synthetic pairs already resident in HBM, then (N > 1) the int16 disparity
+maps are gathered to rank 0 over RCCL/xGMI (BASELINE config 4).  Weak
+scaling: per-GPU work is fixed as N grows.  Timed region: barrier +
+device sync on both sides, K steps, max over ranks.
+
+Prints ONE JSON line on rank 0 (see DESIGN.md §6 for every field).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="kitti", choices=["kitti", "middlebury", "tsukuba", "mccnn"])
+    ap.add_argument("--mode", default="census8", choices=["census8", "sgbm5"])
+    ap.add_argument("--pairs-per-gpu", type=int, default=8)
+    ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--cpu-baseline-pairs", type=int, default=8,
+                    help="KITTI pairs timed on the host C port (rank 0, N=1 only); 0 = skip")
+    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from stereo_match_amd import _lib, synthetic
+    from stereo_match_amd.batch import gather_to_root
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+
+    H, W, D = synthetic.CONFIGS[args.config]
+    p = synthetic.headline_params(D) if args.mode == "census8" else synthetic.parity_params(D)
+    prm = synthetic.to_sm_params(p)
+    P = args.pairs_per_gpu
+    gpairs = P * world
+
+    # synthetic inputs for this rank's pairs, resident in HBM before timing
+    lefts, rights = [], []
+    for i in range(rank * P, rank * P + P):
+        l, r, _ = synthetic.random_dot_pair(H, W, D, seed=1000 + i)
+        lefts.append(l)
+        rights.append(r)
+    dL = torch.tensor(np.stack(lefts), device=dev)
+    dR = torch.tensor(np.stack(rights), device=dev)
+    dOut = torch.empty((P, H, W), dtype=torch.int16, device=dev)
+
+    eng = _lib.Engine(local_rank)
+    stream = torch.cuda.current_stream(dev)
+    eng.set_stream(stream.cuda_stream)
+
+    def step():
+        eng.compute_batch_device(dL.data_ptr(), dR.data_ptr(), P, H * W, H, W, W, prm, dOut.data_ptr())
+        if world > 1 and not args.no_gather:
+            gather_to_root(dOut, gpairs)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    eng.set_timing(True)
+    eng.reset_timing()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    stages = eng.timing()
+    eng.set_timing(False)
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # correctness spot check of the last step (cheap, outside the timed region)
+    out0 = dOut[0].cpu().numpy()
+    valid_frac = float((out0 >= 0).mean())
+
+    if rank == 0:
+        K = args.steps
+        pairs_total = gpairs * K
+        value = pairs_total / elapsed
+        cells = H * W * D
+        width1 = W - D
+        vol = H * width1 * D
+        P_dirs = 8 if args.mode == "census8" else 5
+        eb = 1 if args.mode == "census8" else 2  # bytes per cost / path element
+        paths_ms, paths_n = stages["paths"]
+        paths_avg_s = paths_ms / 1e3 / max(paths_n, 1)
+        # dominant kernel = SGM path aggregation: reads the cost volume once per
+        # direction and writes one path volume per direction
+        alg_bytes_paths = P_dirs * vol * eb * 2
+        achieved = alg_bytes_paths / paths_avg_s / 1e9 if paths_avg_s > 0 else None
+        traffic = None
+        if os.path.exists(args.traffic_file):
+            try:
+                with open(args.traffic_file) as f:
+                    tr = json.load(f)
+                if tr.get("config") == args.config and tr.get("mode") == args.mode:
+                    traffic = tr.get("paths_hbm_bytes_per_launch")
+            except (OSError, ValueError):
+                traffic = None
+        # SURVEY.md §8(d) whole-pipeline model: H·W·D·(1+P+4) + 2HW + 4HW per pair
+        survey_bytes = cells * (1 + P_dirs + 4) + 2 * H * W + 4 * H * W
+        tot_ms, tot_n = stages["total"]
+        pair_s = tot_ms / 1e3 / max(tot_n, 1)
+        line = {
+            "metric": "stereo pairs/sec + Mpix·disp/sec, KITTI 1242×375 D=128 SGM, 1/2/4/8 GPU",
+            "value": value,
+            "unit": "pairs/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / K * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8" if args.mode == "census8" else "i16",
+            "data": "synthetic random-dot pairs (no dataset in the image)",
+            "config": {
+                "workload": f"{args.config} {W}x{H} D={D} "
+                            + ("census9x7 + 8-path SGM" if args.mode == "census8" else "OpenCV-SGBM 5-path"),
+                "pairs_per_gpu": P, "global_batch": gpairs, "H": H, "W": W, "D": D,
+                "gather": world > 1 and not args.no_gather, "parallelism": f"pairs/dp{world}",
+            },
+            "mpix_disp_per_s": value * cells / 1e6,
+            "roofline": {
+                "kernel": "k_sgm_paths (all directions, one launch)",
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+                "traffic": traffic,
+                "alg_bytes_per_launch": alg_bytes_paths,
+                "avg_launch_us": paths_avg_s * 1e6,
+            },
+            "pipeline_roofline": {
+                "model": "SURVEY §8d H·W·D·(1+P+4)+I/O per pair",
+                "bytes_per_pair": survey_bytes,
+                "device_us_per_pair": pair_s * 1e6,
+                "achieved_GBs": survey_bytes / pair_s / 1e9 if pair_s > 0 else None,
+                "frac": survey_bytes / pair_s / 1e9 / HBM_PEAK_GBS if pair_s > 0 else None,
+            },
+            "stage_us_per_pair": {k: v[0] * 1e3 / max(v[1], 1) for k, v in stages.items()},
+            "valid_frac_pair0": valid_frac,
+        }
+        if world == 1 and args.cpu_baseline_pairs > 0:
+            line["cpu_baseline"] = cpu_baseline(args, H, W, D, p, lefts, rights, out0)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args, H, W, D, p, lefts, rights, out0):
+    """The C restatement (oracle/sgm_ref.c, -O3, one thread) on a bounded
+    sample of the same workload; also re-checks pair 0 bit for bit."""
+    from oracle import ref_c
+
+    n = args.cpu_baseline_pairs
+    t0 = time.perf_counter()
+    first = None
+    for i in range(n):
+        o = ref_c.compute(lefts[i % len(lefts)], rights[i % len(rights)], p)
+        if i == 0:
+            first = o
+    dt = time.perf_counter() - t0
+    return {
+        "value": n / dt,
+        "unit": "pairs/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"{n} {W}x{H} D={D} pairs, oracle/sgm_ref.c single-threaded, {dt:.1f} s",
+        "mpix_disp_per_s": n * H * W * D / dt / 1e6,
+        "host_cpus_visible": os.cpu_count(),
+        "gpu_matches_port_pair0": bool(np.array_equal(first, out0)),
+    }
+
+
+if __name__ == "__main__":
+    main()

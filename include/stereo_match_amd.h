@@ -1,0 +1,122 @@
+/*
+ * stereo_match_amd.h — C-ABI of the MI355X stereo disparity engine.
+ *
+ * Drop-in boundary for the reference hot path
+ *   stereo_vision/stereo_vision.py:132  compute_disparity(gray_l, gray_r, disparity_settings, method="SGBM")
+ * whose arithmetic the reference reaches through
+ *   stereo_vision/stereo_vision.py:153  cv2.StereoSGBM_create(minDisparity=..., ..., preFilterCap=...)
+ *   stereo_vision/stereo_vision.py:178  left_matcher.compute(gray_l, gray_r)   -> int16 disparity x16
+ *   stereo_vision/stereo_vision.py:179  right_matcher.compute(gray_r, gray_l)  (createRightMatcher, :171)
+ * Python binds this header with ctypes (stereo_match_amd/_lib.py); see
+ * INTEGRATION.md for the binding a maintainer adds on the reference side.
+ *
+ * Conventions: plain pointers + sizes, no torch types.  Every function
+ * returns 0 on success or a negative SM_E* code; sm_last_error() gives the
+ * text.  One context per device, not shared by concurrent threads.
+ * Host-pointer entry points are synchronous on return; *_device entry
+ * points are asynchronous on the context's stream (sm_set_stream).
+ */
+#ifndef STEREO_MATCH_AMD_H
+#define STEREO_MATCH_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SM_OK 0
+#define SM_E_ARG (-1)         /* bad argument: mirrors OpenCV's CV_Assert failures */
+#define SM_E_HIP (-2)         /* HIP runtime / launch error */
+#define SM_E_UNSUPPORTED (-4) /* valid for OpenCV but not implemented / outside exact range */
+
+#define SM_COST_SGBM 0   /* OpenCV StereoSGBM cost: BT(Sobel-x clip) + BT(raw)>>2, blockSize^2 box */
+#define SM_COST_CENSUS 1 /* north-star cost: 9x7 census + Hamming (no reference counterpart) */
+
+#define SM_MODE_SGBM 5 /* cv2.STEREO_SGBM_MODE_SGBM: 5 paths (reference default) */
+#define SM_MODE_HH 8   /* cv2.STEREO_SGBM_MODE_HH: 8 paths */
+
+/* Field meaning follows cv2.StereoSGBM_create kwargs (reference:
+ * stereo_vision/stereo_vision.py:153-163); unnormalised values are accepted
+ * and normalised exactly as OpenCV does (P1<=0 -> 2, ...). */
+typedef struct sm_params {
+    int min_disparity;
+    int num_disparities; /* > 0, multiple of 16 (OpenCV asserts this) */
+    int block_size;      /* SADWindowSize; <= 0 -> 5 */
+    int P1, P2;
+    int disp12_max_diff;
+    int uniqueness_ratio;
+    int pre_filter_cap;
+    int speckle_window_size; /* must be 0 on the GPU path for now (SM_E_UNSUPPORTED) */
+    int speckle_range;
+    int cost_kind; /* SM_COST_* */
+    int mode;      /* SM_MODE_SGBM | SM_MODE_HH */
+} sm_params;
+
+typedef struct sm_ctx sm_ctx;
+
+/* Create a context bound to HIP device `device` (its own non-blocking stream). */
+int sm_create(int device, sm_ctx** out);
+void sm_destroy(sm_ctx* ctx);
+
+/* Use an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream);
+ * NULL restores the context's own stream. */
+int sm_set_stream(sm_ctx* ctx, void* hip_stream);
+
+/* StereoSGBM::compute(left, right) on host buffers (uint8, row stride in
+ * bytes >= W).  disp_out: int16[H*W], disparity x16, invalid = (minD-1)*16.
+ * Replaces stereo_vision/stereo_vision.py:178 (and :179 with the right
+ * matcher's params, see sm_right_matcher_params). */
+int sm_compute(sm_ctx* ctx, const uint8_t* left, const uint8_t* right, int H, int W, int stride,
+               const sm_params* p, int16_t* disp_out);
+
+/* Same on device pointers already resident in HBM; enqueued on the context
+ * stream, returns before completion. */
+int sm_compute_device(sm_ctx* ctx, const uint8_t* d_left, const uint8_t* d_right, int H, int W,
+                      int stride, const sm_params* p, int16_t* d_disp_out);
+
+/* Batch of npairs same-size pairs on device pointers: pair i reads
+ * d_left + i*pair_stride_bytes (same for right) and writes
+ * d_disp_out + i*H*W.  Asynchronous on the context stream. */
+int sm_compute_batch_device(sm_ctx* ctx, const uint8_t* d_left, const uint8_t* d_right, int npairs,
+                            size_t pair_stride_bytes, int H, int W, int stride, const sm_params* p,
+                            int16_t* d_disp_out);
+
+/* ximgproc::createRightMatcher(StereoSGBM) parameter derivation
+ * (reference call: stereo_vision/stereo_vision.py:171). */
+int sm_right_matcher_params(const sm_params* left, sm_params* right_out);
+
+/* Wait for all work enqueued on the context stream. */
+int sm_synchronize(sm_ctx* ctx);
+
+/* Per-stage device timing with hipEvents on the context stream.
+ * stage: 0 cost, 1 path aggregation, 2 WTA+LR, 3 median, 4 whole pipeline. */
+#define SM_STAGE_COST 0
+#define SM_STAGE_PATHS 1
+#define SM_STAGE_WTA 2
+#define SM_STAGE_MEDIAN 3
+#define SM_STAGE_TOTAL 4
+#define SM_NUM_STAGES 5
+int sm_set_timing(sm_ctx* ctx, int enable);
+int sm_get_timing(sm_ctx* ctx, int stage, double* total_ms, long long* count);
+int sm_reset_timing(sm_ctx* ctx);
+
+/* Debug / parity: copy an intermediate of the LAST computation to host.
+ * what: 0 cost volume C[H][width1][D] (uint8 census / uint16 SGBM),
+ *       1 path volumes L[P][H][width1][D] (uint8 census / uint16 SGBM),
+ *       2 pre-median disparity int16[H][W].
+ * Returns the byte size when host == NULL. */
+long long sm_debug_fetch(sm_ctx* ctx, int what, void* host, size_t bytes);
+
+/* Last error text of ctx (or of the calling thread when ctx == NULL). */
+const char* sm_last_error(sm_ctx* ctx);
+
+/* Library version string. */
+const char* sm_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* STEREO_MATCH_AMD_H */

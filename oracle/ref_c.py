@@ -1,0 +1,78 @@
+"""ctypes loader for oracle/libsgm_ref.so (the C restatement).
+
+TEST INFRASTRUCTURE ONLY — see oracle/sgm_np.py for the parity status
+("parity unpinned") and the import rule (tests/, smoke(), bench cpu_baseline).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = os.path.join(_HERE, "libsgm_ref.so")
+
+
+class SgmRefParams(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in (
+        "min_disparity", "num_disparities", "block_size", "P1", "P2",
+        "disp12_max_diff", "uniqueness_ratio", "pre_filter_cap",
+        "speckle_window_size", "speckle_range", "cost_kind", "npaths")]
+
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB):
+            build()
+        lib = ctypes.CDLL(_LIB)
+        lib.sgm_ref_compute.restype = ctypes.c_int
+        lib.sgm_ref_compute.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                        ctypes.c_int, ctypes.POINTER(SgmRefParams), ctypes.c_void_p,
+                                        ctypes.c_int]
+        lib.sgm_ref_census9x7.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_void_p]
+        lib.sgm_ref_median3.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+        _lib = lib
+    return _lib
+
+
+def make_params(p: dict) -> SgmRefParams:
+    return SgmRefParams(
+        int(p.get("minDisparity", 0)), int(p.get("numDisparities", 16)), int(p.get("blockSize", 3)),
+        int(p.get("P1", 0)), int(p.get("P2", 0)), int(p.get("disp12MaxDiff", 0)),
+        int(p.get("uniquenessRatio", 0)), int(p.get("preFilterCap", 0)),
+        int(p.get("speckleWindowSize", 0)), int(p.get("speckleRange", 0)),
+        int(p.get("cost", 0)), int(p.get("mode", 5)))
+
+
+def compute(left: np.ndarray, right: np.ndarray, params: dict, median: bool = True) -> np.ndarray:
+    lib = load()
+    left = np.ascontiguousarray(left, np.uint8)
+    right = np.ascontiguousarray(right, np.uint8)
+    H, W = left.shape
+    out = np.empty((H, W), np.int16)
+    prm = make_params(params)
+    rc = lib.sgm_ref_compute(left.ctypes.data, right.ctypes.data, H, W, W, ctypes.byref(prm),
+                             out.ctypes.data, int(bool(median)))
+    if rc != 0:
+        raise ValueError(f"sgm_ref_compute failed ({rc})")
+    return out
+
+
+def census(img: np.ndarray) -> np.ndarray:
+    lib = load()
+    img = np.ascontiguousarray(img, np.uint8)
+    H, W = img.shape
+    out = np.empty((H, W), np.uint64)
+    lib.sgm_ref_census9x7(img.ctypes.data, H, W, W, out.ctypes.data)
+    return out

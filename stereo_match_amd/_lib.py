@@ -1,0 +1,208 @@
+"""ctypes binding of ``libstereo_match_amd.so`` (C-ABI: include/stereo_match_amd.h).
+
+The product path has NO CPU fallback: if the in-tree HIP library is missing,
+``load()`` raises ``ImportError`` with the build command.  Nothing here
+imports ``oracle/``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libstereo_match_amd.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "stereo_match_amd.h")
+
+SM_OK, SM_E_ARG, SM_E_HIP, SM_E_UNSUPPORTED = 0, -1, -2, -4
+SM_COST_SGBM, SM_COST_CENSUS = 0, 1
+SM_MODE_SGBM, SM_MODE_HH = 5, 8
+STAGES = ("cost", "paths", "wta", "median", "total")
+
+
+class SmParams(ctypes.Structure):
+    """Mirror of ``struct sm_params`` (field order must match the header)."""
+    _fields_ = [(n, ctypes.c_int) for n in (
+        "min_disparity", "num_disparities", "block_size", "P1", "P2",
+        "disp12_max_diff", "uniqueness_ratio", "pre_filter_cap",
+        "speckle_window_size", "speckle_range", "cost_kind", "mode")]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
+_c = ctypes
+_SIGS = {
+    "sm_version": (_c.c_char_p, []),
+    "sm_create": (_c.c_int, [_c.c_int, _c.POINTER(_c.c_void_p)]),
+    "sm_destroy": (None, [_c.c_void_p]),
+    "sm_set_stream": (_c.c_int, [_c.c_void_p, _c.c_void_p]),
+    "sm_compute": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_int, _c.c_int, _c.c_int,
+                              _c.POINTER(SmParams), _c.c_void_p]),
+    "sm_compute_device": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_int, _c.c_int, _c.c_int,
+                                     _c.POINTER(SmParams), _c.c_void_p]),
+    "sm_compute_batch_device": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_int, _c.c_size_t,
+                                           _c.c_int, _c.c_int, _c.c_int, _c.POINTER(SmParams), _c.c_void_p]),
+    "sm_right_matcher_params": (_c.c_int, [_c.POINTER(SmParams), _c.POINTER(SmParams)]),
+    "sm_synchronize": (_c.c_int, [_c.c_void_p]),
+    "sm_set_timing": (_c.c_int, [_c.c_void_p, _c.c_int]),
+    "sm_get_timing": (_c.c_int, [_c.c_void_p, _c.c_int, _c.POINTER(_c.c_double), _c.POINTER(_c.c_longlong)]),
+    "sm_reset_timing": (_c.c_int, [_c.c_void_p]),
+    "sm_debug_fetch": (_c.c_longlong, [_c.c_void_p, _c.c_int, _c.c_void_p, _c.c_size_t]),
+    "sm_last_error": (_c.c_char_p, [_c.c_void_p]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+def header_symbols(path: str = HEADER_PATH):
+    """Function names declared in include/stereo_match_amd.h."""
+    with open(path) as f:
+        text = f.read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[\w\s\*]*?\b(sm_\w+)\s*\(", text, flags=re.M)))
+
+
+def load():
+    """Load the HIP library (fails loudly if it has not been built)."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} is missing: build it with `make -C stereo_match_amd/csrc` "
+                "(or python -c 'import __graft_entry__ as g; g.build()'). "
+                "There is no CPU fallback.")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+        return lib
+
+
+class SmError(RuntimeError):
+    """Raised for SM_E_HIP / SM_E_UNSUPPORTED (OpenCV would raise cv2.error)."""
+
+    def __init__(self, code, msg):
+        super().__init__(f"[{code}] {msg}")
+        self.code = code
+
+
+def _raise(code: int, ctx):
+    lib = load()
+    msg = (lib.sm_last_error(ctx) or b"").decode(errors="replace")
+    if code == SM_E_ARG:
+        raise ValueError(msg)
+    raise SmError(code, msg)
+
+
+class Engine:
+    """One sm_ctx bound to one HIP device (not thread-safe; one per thread)."""
+
+    def __init__(self, device: int = 0):
+        lib = load()
+        h = ctypes.c_void_p()
+        rc = lib.sm_create(int(device), ctypes.byref(h))
+        if rc != SM_OK:
+            _raise(rc, None)
+        self._lib = lib
+        self.ctx = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            self._lib.sm_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):  # pragma: no cover - interpreter shutdown order
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        if rc != SM_OK:
+            _raise(rc, self.ctx)
+
+    def set_stream(self, stream_handle: int | None):
+        self._check(self._lib.sm_set_stream(self.ctx, ctypes.c_void_p(stream_handle or 0)))
+
+    # -- host arrays -------------------------------------------------------
+    def compute(self, left: np.ndarray, right: np.ndarray, params: SmParams) -> np.ndarray:
+        left = np.ascontiguousarray(left)
+        right = np.ascontiguousarray(right)
+        H, W = left.shape
+        out = np.empty((H, W), np.int16)
+        self._check(self._lib.sm_compute(self.ctx, left.ctypes.data, right.ctypes.data, H, W, W,
+                                         ctypes.byref(params), out.ctypes.data))
+        return out
+
+    # -- device pointers (e.g. torch tensors' data_ptr()) -------------------
+    def compute_device(self, d_left: int, d_right: int, H: int, W: int, stride: int, params: SmParams,
+                       d_out: int):
+        self._check(self._lib.sm_compute_device(self.ctx, ctypes.c_void_p(d_left), ctypes.c_void_p(d_right),
+                                                H, W, stride, ctypes.byref(params), ctypes.c_void_p(d_out)))
+
+    def compute_batch_device(self, d_left: int, d_right: int, npairs: int, pair_stride: int, H: int, W: int,
+                             stride: int, params: SmParams, d_out: int):
+        self._check(self._lib.sm_compute_batch_device(
+            self.ctx, ctypes.c_void_p(d_left), ctypes.c_void_p(d_right), npairs, pair_stride, H, W, stride,
+            ctypes.byref(params), ctypes.c_void_p(d_out)))
+
+    def synchronize(self):
+        self._check(self._lib.sm_synchronize(self.ctx))
+
+    # -- timing ---------------------------------------------------------------
+    def set_timing(self, on: bool):
+        self._check(self._lib.sm_set_timing(self.ctx, int(bool(on))))
+
+    def reset_timing(self):
+        self._check(self._lib.sm_reset_timing(self.ctx))
+
+    def timing(self) -> dict:
+        out = {}
+        for i, name in enumerate(STAGES):
+            ms = ctypes.c_double()
+            n = ctypes.c_longlong()
+            self._check(self._lib.sm_get_timing(self.ctx, i, ctypes.byref(ms), ctypes.byref(n)))
+            out[name] = (ms.value, n.value)
+        return out
+
+    # -- debug ------------------------------------------------------------------
+    def debug_fetch(self, what: int) -> bytes:
+        n = self._lib.sm_debug_fetch(self.ctx, what, None, 0)
+        if n < 0:
+            _raise(int(n), self.ctx)
+        buf = (ctypes.c_char * max(int(n), 1))()
+        r = self._lib.sm_debug_fetch(self.ctx, what, buf, int(n))
+        if r < 0:
+            _raise(int(r), self.ctx)
+        return bytes(buf)[:int(n)]
+
+
+def right_matcher_params(p: SmParams) -> SmParams:
+    lib = load()
+    out = SmParams()
+    rc = lib.sm_right_matcher_params(ctypes.byref(p), ctypes.byref(out))
+    if rc != SM_OK:
+        _raise(rc, None)
+    return out
+
+
+_engines: dict = {}
+
+
+def engine(device: int = 0) -> Engine:
+    """Per-(thread, device) cached engine."""
+    key = (threading.get_ident(), device)
+    e = _engines.get(key)
+    if e is None:
+        e = _engines[key] = Engine(device)
+    return e

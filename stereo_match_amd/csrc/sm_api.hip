@@ -1,0 +1,546 @@
+// sm_api.hip — C-ABI (include/stereo_match_amd.h) around the gfx950 kernels.
+//
+// Host side of the drop-in boundary for stereo_vision/stereo_vision.py:153-179
+// (cv2.StereoSGBM_create(...).compute).  Parameter normalisation mirrors
+// OpenCV computeDisparitySGBM (see oracle/sgm_np.py:normalize_params).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/stereo_match_amd.h"
+#include "sm_kernels.hpp"
+
+#define SM_VERSION "stereo_match_amd 0.1.0 (gfx950)"
+
+namespace {
+
+thread_local std::string g_thread_error;
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t n = 0;
+};
+
+struct Norm {
+    int minD, D, maxD, bs, P1, P2, ftzero, uniq, disp12, speckle_ws, speckle_range, cost, mode;
+    int minX1, maxX1, width1, ndirs, dpl;
+};
+
+struct TimedEvent {
+    int stage;
+    hipEvent_t a, b;
+};
+
+}  // namespace
+
+struct sm_ctx {
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    DevBuf img[2], census[2], planes, hsum, cost, L, raw, out;
+    // geometry of the last computation (for sm_debug_fetch)
+    int lastH = 0, lastW = 0, last_width1 = 0, lastD = 0, last_ndirs = 0, last_cost = 0;
+    bool timing = false;
+    std::vector<TimedEvent> pending;
+    std::vector<hipEvent_t> free_events;
+    double stage_ms[SM_NUM_STAGES] = {0};
+    long long stage_n[SM_NUM_STAGES] = {0};
+    std::string err;
+};
+
+namespace {
+
+int fail(sm_ctx* ctx, int code, const char* fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (ctx) ctx->err = buf;
+    g_thread_error = buf;
+    return code;
+}
+
+#define HIP_TRY(ctx, expr)                                                                           \
+    do {                                                                                              \
+        hipError_t e_ = (expr);                                                                       \
+        if (e_ != hipSuccess)                                                                         \
+            return fail((ctx), SM_E_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_),   \
+                        __FILE__, __LINE__);                                                          \
+    } while (0)
+
+int ensure(sm_ctx* ctx, DevBuf& b, size_t bytes)
+{
+    if (b.n >= bytes && b.p) return SM_OK;
+    if (b.p) {
+        (void)hipStreamSynchronize(ctx->stream);
+        (void)hipFree(b.p);
+        b.p = nullptr;
+        b.n = 0;
+    }
+    size_t want = std::max<size_t>(bytes, 256);
+    HIP_TRY(ctx, hipMalloc(&b.p, want));
+    b.n = want;
+    return SM_OK;
+}
+
+int normalize(sm_ctx* ctx, const sm_params* p, int H, int W, Norm& n)
+{
+    if (!p) return fail(ctx, SM_E_ARG, "params is NULL");
+    if (H <= 0 || W <= 0) return fail(ctx, SM_E_ARG, "empty image (%dx%d)", W, H);
+    if (W > 32767) return fail(ctx, SM_E_UNSUPPORTED, "width %d > 32767", W);
+    n.minD = p->min_disparity;
+    n.D = p->num_disparities;
+    if (n.D <= 0 || n.D % 16 != 0)
+        return fail(ctx, SM_E_ARG, "numDisparities must be a positive multiple of 16 (got %d)", n.D);
+    if (n.D > 256) return fail(ctx, SM_E_UNSUPPORTED, "numDisparities %d > 256 not built", n.D);
+    n.maxD = n.minD + n.D;
+    n.bs = p->block_size > 0 ? p->block_size : 5;
+    n.ftzero = std::max(p->pre_filter_cap, 15) | 1;
+    n.uniq = p->uniqueness_ratio >= 0 ? p->uniqueness_ratio : 10;
+    n.disp12 = p->disp12_max_diff > 0 ? p->disp12_max_diff : 1;
+    n.P1 = p->P1 > 0 ? p->P1 : 2;
+    n.P2 = std::max(p->P2 > 0 ? p->P2 : 5, n.P1 + 1);
+    n.speckle_ws = p->speckle_window_size;
+    n.speckle_range = p->speckle_range;
+    n.cost = p->cost_kind;
+    n.mode = p->mode;
+    if (n.cost != SM_COST_SGBM && n.cost != SM_COST_CENSUS)
+        return fail(ctx, SM_E_ARG, "cost_kind %d unknown", n.cost);
+    if (n.mode != SM_MODE_SGBM && n.mode != SM_MODE_HH)
+        return fail(ctx, SM_E_UNSUPPORTED, "mode %d not supported (5 = MODE_SGBM, 8 = MODE_HH)", n.mode);
+    if (n.speckle_ws > 0)
+        return fail(ctx, SM_E_UNSUPPORTED, "speckleWindowSize > 0 not implemented on the GPU path yet");
+    if (n.cost == SM_COST_SGBM) {
+        const int maxpix = 2 * n.ftzero + (255 >> 2);
+        if ((long long)n.bs * n.bs * maxpix + n.P2 > 16383)
+            return fail(ctx, SM_E_UNSUPPORTED,
+                        "blockSize=%d/preFilterCap/P2=%d outside the int16-exact range (bs^2*(2*ftzero+63)+P2 <= 16383)",
+                        n.bs, n.P2);
+    } else {
+        if (62 + n.P2 > 255) return fail(ctx, SM_E_UNSUPPORTED, "census mode needs P2 <= 193 (8-bit path values)");
+    }
+    if (n.P1 > 16383 || n.P2 > 16383) return fail(ctx, SM_E_UNSUPPORTED, "P1/P2 too large");
+    n.minX1 = std::max(n.maxD, 0);
+    n.maxX1 = W + std::min(n.minD, 0);
+    n.width1 = n.maxX1 - n.minX1;
+    n.ndirs = n.mode;
+    n.dpl = n.D / 16;
+    return SM_OK;
+}
+
+hipEvent_t get_event(sm_ctx* ctx)
+{
+    if (!ctx->free_events.empty()) {
+        hipEvent_t e = ctx->free_events.back();
+        ctx->free_events.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    return e;
+}
+
+struct StageTimer {
+    sm_ctx* ctx;
+    int stage;
+    hipEvent_t a = nullptr;
+    StageTimer(sm_ctx* c, int s) : ctx(c), stage(s)
+    {
+        if (ctx->timing) {
+            a = get_event(ctx);
+            (void)hipEventRecord(a, ctx->stream);
+        }
+    }
+    ~StageTimer()
+    {
+        if (ctx->timing) {
+            hipEvent_t b = get_event(ctx);
+            (void)hipEventRecord(b, ctx->stream);
+            ctx->pending.push_back({stage, a, b});
+        }
+    }
+};
+
+void harvest_timing(sm_ctx* ctx)
+{
+    for (auto& t : ctx->pending) {
+        (void)hipEventSynchronize(t.b);
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, t.a, t.b);
+        ctx->stage_ms[t.stage] += ms;
+        ctx->stage_n[t.stage] += 1;
+        ctx->free_events.push_back(t.a);
+        ctx->free_events.push_back(t.b);
+    }
+    ctx->pending.clear();
+}
+
+// direction table: MODE_SGBM r0..r4 then MODE_HH's extra three.  The two
+// horizontal directions come first so their (longest) lines start early.
+const int kDirDx[8] = {1, -1, 1, 0, -1, 1, 0, -1};
+const int kDirDy[8] = {0, 0, 1, 1, 1, -1, -1, -1};
+
+template <int DPL>
+int launch_paths_wta(sm_ctx* ctx, const Norm& n, int H, int W)
+{
+    const bool census = n.cost == SM_COST_CENSUS;
+    smk::PathArgs pa{};
+    pa.cost = ctx->cost.p;
+    pa.L = ctx->L.p;
+    pa.vol = (size_t)H * n.width1 * n.D;
+    pa.H = H;
+    pa.width1 = n.width1;
+    pa.D = n.D;
+    pa.P1 = n.P1;
+    pa.P2 = n.P2;
+    pa.ndirs = n.ndirs;
+    int blocks = 0;
+    // MODE_SGBM = {E, W, SE, S, SW}; MODE_HH adds {NE, N, NW}
+    for (int k = 0; k < n.ndirs; k++) {
+        pa.dx[k] = kDirDx[k];
+        pa.dy[k] = kDirDy[k];
+        pa.blk_start[k] = blocks;
+        const int nlines = pa.dy[k] == 0 ? H : n.width1;
+        blocks += (nlines + 15) / 16;
+    }
+    pa.blk_start[n.ndirs] = blocks;
+    for (int k = n.ndirs + 1; k <= smk::kMaxDirs; k++) pa.blk_start[k] = blocks;
+    {
+        StageTimer t(ctx, SM_STAGE_PATHS);
+        if (census)
+            hipLaunchKernelGGL((smk::k_sgm_paths<DPL, uint8_t, uint8_t>), dim3(blocks), dim3(256), 0, ctx->stream, pa);
+        else
+            hipLaunchKernelGGL((smk::k_sgm_paths<DPL, uint16_t, uint16_t>), dim3(blocks), dim3(256), 0, ctx->stream, pa);
+        HIP_TRY(ctx, hipGetLastError());
+    }
+    smk::WtaArgs wa{};
+    wa.L = ctx->L.p;
+    wa.vol = pa.vol;
+    wa.ndirs = n.ndirs;
+    wa.H = H;
+    wa.W = W;
+    wa.width1 = n.width1;
+    wa.D = n.D;
+    wa.minD = n.minD;
+    wa.minX1 = n.minX1;
+    wa.uniq = n.uniq;
+    wa.disp12 = n.disp12;
+    wa.disp = (int16_t*)ctx->raw.p;
+    {
+        StageTimer t(ctx, SM_STAGE_WTA);
+        const size_t smem = (size_t)W * 8;
+        if (census)
+            hipLaunchKernelGGL((smk::k_wta<DPL, uint8_t>), dim3(H), dim3(256), smem, ctx->stream, wa);
+        else
+            hipLaunchKernelGGL((smk::k_wta<DPL, uint16_t>), dim3(H), dim3(256), smem, ctx->stream, wa);
+        HIP_TRY(ctx, hipGetLastError());
+    }
+    return SM_OK;
+}
+
+int dispatch_dpl(sm_ctx* ctx, const Norm& n, int H, int W)
+{
+    switch (n.dpl) {
+#define CASE(k) \
+    case k: return launch_paths_wta<k>(ctx, n, H, W);
+        CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
+        CASE(9) CASE(10) CASE(11) CASE(12) CASE(13) CASE(14) CASE(15) CASE(16)
+#undef CASE
+    default: return fail(ctx, SM_E_UNSUPPORTED, "numDisparities %d not built", n.D);
+    }
+}
+
+int grid_for(size_t n)
+{
+    size_t g = (n + 255) / 256;
+    return (int)std::min<size_t>(std::max<size_t>(g, 1), 8192);
+}
+
+// One pair, device pointers, enqueued on ctx->stream.
+int run_pair(sm_ctx* ctx, const uint8_t* dL, const uint8_t* dR, int H, int W, int stride, const Norm& n,
+             int16_t* d_out)
+{
+    const int INVALID = (n.minD - 1) * 16;
+    ctx->lastH = H;
+    ctx->lastW = W;
+    ctx->last_width1 = std::max(n.width1, 0);
+    ctx->lastD = n.D;
+    ctx->last_ndirs = n.ndirs;
+    ctx->last_cost = n.cost;
+    StageTimer total(ctx, SM_STAGE_TOTAL);
+    if (n.width1 <= 0) {
+        hipLaunchKernelGGL(smk::k_fill16, dim3(grid_for((size_t)H * W)), dim3(256), 0, ctx->stream, d_out,
+                           (size_t)H * W, (int16_t)INVALID);
+        HIP_TRY(ctx, hipGetLastError());
+        return SM_OK;
+    }
+    const size_t cells = (size_t)H * n.width1 * n.D;
+    const size_t lt = n.cost == SM_COST_CENSUS ? 1 : 2;
+    int rc;
+    if ((rc = ensure(ctx, ctx->cost, cells * lt)) != SM_OK) return rc;
+    if ((rc = ensure(ctx, ctx->L, cells * lt * n.ndirs)) != SM_OK) return rc;
+    if ((rc = ensure(ctx, ctx->raw, (size_t)H * W * 2)) != SM_OK) return rc;
+    {
+        StageTimer t(ctx, SM_STAGE_COST);
+        if (n.cost == SM_COST_CENSUS) {
+            for (int i = 0; i < 2; i++)
+                if ((rc = ensure(ctx, ctx->census[i], (size_t)H * W * 8)) != SM_OK) return rc;
+            smk::CensusArgs ca{};
+            ca.img[0] = dL;
+            ca.img[1] = dR;
+            ca.out[0] = (uint64_t*)ctx->census[0].p;
+            ca.out[1] = (uint64_t*)ctx->census[1].p;
+            ca.H = H;
+            ca.W = W;
+            ca.stride = stride;
+            hipLaunchKernelGGL(smk::k_census9x7, dim3((W + smk::CT_W - 1) / smk::CT_W, (H + smk::CT_H - 1) / smk::CT_H, 2),
+                               dim3(256), 0, ctx->stream, ca);
+            HIP_TRY(ctx, hipGetLastError());
+            smk::CensusCostArgs cc{};
+            cc.cl = ca.out[0];
+            cc.cr = ca.out[1];
+            cc.C = (uint8_t*)ctx->cost.p;
+            cc.H = H;
+            cc.W = W;
+            cc.width1 = n.width1;
+            cc.D = n.D;
+            cc.minD = n.minD;
+            cc.minX1 = n.minX1;
+            hipLaunchKernelGGL(smk::k_census_cost, dim3(grid_for(cells / 8)), dim3(256), 0, ctx->stream, cc);
+            HIP_TRY(ctx, hipGetLastError());
+        } else {
+            if ((rc = ensure(ctx, ctx->planes, (size_t)H * W * 12)) != SM_OK) return rc;
+            if ((rc = ensure(ctx, ctx->hsum, cells * 2)) != SM_OK) return rc;
+            smk::PrefilterArgs pf{};
+            pf.img[0] = dL;
+            pf.img[1] = dR;
+            pf.planes = (uint8_t*)ctx->planes.p;
+            pf.H = H;
+            pf.W = W;
+            pf.stride = stride;
+            pf.ftzero = n.ftzero;
+            hipLaunchKernelGGL(smk::k_sgbm_prefilter, dim3((W + 255) / 256, H, 2), dim3(256), 0, ctx->stream, pf);
+            HIP_TRY(ctx, hipGetLastError());
+            smk::HsumArgs hs{};
+            hs.planes = pf.planes;
+            hs.hsum = (uint16_t*)ctx->hsum.p;
+            hs.H = H;
+            hs.W = W;
+            hs.width1 = n.width1;
+            hs.D = n.D;
+            hs.minD = n.minD;
+            hs.minX1 = n.minX1;
+            hs.SW2 = n.bs / 2;
+            hipLaunchKernelGGL(smk::k_sgbm_hsum, dim3(grid_for(cells)), dim3(256), 0, ctx->stream, hs);
+            HIP_TRY(ctx, hipGetLastError());
+            smk::VsumArgs vs{};
+            vs.hsum = hs.hsum;
+            vs.C = (uint16_t*)ctx->cost.p;
+            vs.H = H;
+            vs.width1 = n.width1;
+            vs.D = n.D;
+            vs.SH2 = n.bs / 2;
+            vs.hh = n.mode == SM_MODE_HH;
+            hipLaunchKernelGGL(smk::k_sgbm_vsum, dim3(grid_for(cells)), dim3(256), 0, ctx->stream, vs);
+            HIP_TRY(ctx, hipGetLastError());
+        }
+    }
+    if ((rc = dispatch_dpl(ctx, n, H, W)) != SM_OK) return rc;
+    {
+        StageTimer t(ctx, SM_STAGE_MEDIAN);
+        hipLaunchKernelGGL(smk::k_median3, dim3((W + 255) / 256, H), dim3(256), 0, ctx->stream,
+                           (const int16_t*)ctx->raw.p, d_out, H, W);
+        HIP_TRY(ctx, hipGetLastError());
+    }
+    return SM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* sm_version(void) { return SM_VERSION; }
+
+int sm_create(int device, sm_ctx** out)
+{
+    if (!out) return fail(nullptr, SM_E_ARG, "out is NULL");
+    *out = nullptr;
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev <= 0) return fail(nullptr, SM_E_HIP, "no HIP device available (%s)", hipGetErrorString(e));
+    if (device < 0 || device >= ndev) return fail(nullptr, SM_E_ARG, "device %d out of range [0,%d)", device, ndev);
+    sm_ctx* ctx = new sm_ctx();
+    ctx->device = device;
+    e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete ctx;
+        return fail(nullptr, SM_E_HIP, "context creation failed: %s", hipGetErrorString(e));
+    }
+    ctx->stream = ctx->own_stream;
+    *out = ctx;
+    return SM_OK;
+}
+
+void sm_destroy(sm_ctx* ctx)
+{
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    DevBuf* bufs[] = {&ctx->img[0], &ctx->img[1], &ctx->census[0], &ctx->census[1], &ctx->planes, &ctx->hsum,
+                      &ctx->cost, &ctx->L, &ctx->raw, &ctx->out};
+    for (DevBuf* b : bufs)
+        if (b->p) (void)hipFree(b->p);
+    for (auto& t : ctx->pending) {
+        (void)hipEventDestroy(t.a);
+        (void)hipEventDestroy(t.b);
+    }
+    for (auto e : ctx->free_events) (void)hipEventDestroy(e);
+    if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
+    delete ctx;
+}
+
+int sm_set_stream(sm_ctx* ctx, void* hip_stream)
+{
+    if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
+    ctx->stream = hip_stream ? (hipStream_t)hip_stream : ctx->own_stream;
+    return SM_OK;
+}
+
+int sm_right_matcher_params(const sm_params* left, sm_params* right)
+{
+    if (!left || !right) return fail(nullptr, SM_E_ARG, "NULL params");
+    *right = *left;
+    right->min_disparity = -(left->min_disparity + left->num_disparities) + 1;
+    right->uniqueness_ratio = 0;
+    right->disp12_max_diff = 1000000;
+    right->speckle_window_size = 0;
+    return SM_OK;
+}
+
+int sm_compute_device(sm_ctx* ctx, const uint8_t* dL, const uint8_t* dR, int H, int W, int stride,
+                      const sm_params* p, int16_t* d_out)
+{
+    if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
+    if (!dL || !dR || !d_out) return fail(ctx, SM_E_ARG, "NULL image/output pointer");
+    if (stride < W) return fail(ctx, SM_E_ARG, "stride %d < width %d", stride, W);
+    Norm n;
+    int rc = normalize(ctx, p, H, W, n);
+    if (rc != SM_OK) return rc;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    return run_pair(ctx, dL, dR, H, W, stride, n, d_out);
+}
+
+int sm_compute_batch_device(sm_ctx* ctx, const uint8_t* dL, const uint8_t* dR, int npairs, size_t pair_stride,
+                            int H, int W, int stride, const sm_params* p, int16_t* d_out)
+{
+    if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
+    if (npairs < 0) return fail(ctx, SM_E_ARG, "npairs < 0");
+    if (!dL || !dR || !d_out) return fail(ctx, SM_E_ARG, "NULL image/output pointer");
+    if (stride < W) return fail(ctx, SM_E_ARG, "stride %d < width %d", stride, W);
+    Norm n;
+    int rc = normalize(ctx, p, H, W, n);
+    if (rc != SM_OK) return rc;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    for (int i = 0; i < npairs; i++) {
+        rc = run_pair(ctx, dL + (size_t)i * pair_stride, dR + (size_t)i * pair_stride, H, W, stride, n,
+                      d_out + (size_t)i * H * W);
+        if (rc != SM_OK) return rc;
+    }
+    return SM_OK;
+}
+
+int sm_compute(sm_ctx* ctx, const uint8_t* L, const uint8_t* R, int H, int W, int stride, const sm_params* p,
+               int16_t* disp_out)
+{
+    if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
+    if (!L || !R || !disp_out) return fail(ctx, SM_E_ARG, "NULL image/output pointer");
+    if (stride < W) return fail(ctx, SM_E_ARG, "stride %d < width %d", stride, W);
+    Norm n;
+    int rc = normalize(ctx, p, H, W, n);
+    if (rc != SM_OK) return rc;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    const size_t img = (size_t)H * W;
+    for (int i = 0; i < 2; i++)
+        if ((rc = ensure(ctx, ctx->img[i], img)) != SM_OK) return rc;
+    if ((rc = ensure(ctx, ctx->out, img * 2)) != SM_OK) return rc;
+    HIP_TRY(ctx, hipMemcpy2DAsync(ctx->img[0].p, W, L, stride, W, H, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpy2DAsync(ctx->img[1].p, W, R, stride, W, H, hipMemcpyHostToDevice, ctx->stream));
+    rc = run_pair(ctx, (const uint8_t*)ctx->img[0].p, (const uint8_t*)ctx->img[1].p, H, W, W, n,
+                  (int16_t*)ctx->out.p);
+    if (rc != SM_OK) return rc;
+    HIP_TRY(ctx, hipMemcpyAsync(disp_out, ctx->out.p, img * 2, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return SM_OK;
+}
+
+int sm_synchronize(sm_ctx* ctx)
+{
+    if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return SM_OK;
+}
+
+int sm_set_timing(sm_ctx* ctx, int enable)
+{
+    if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
+    ctx->timing = enable != 0;
+    return SM_OK;
+}
+
+int sm_reset_timing(sm_ctx* ctx)
+{
+    if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
+    harvest_timing(ctx);
+    for (int i = 0; i < SM_NUM_STAGES; i++) {
+        ctx->stage_ms[i] = 0;
+        ctx->stage_n[i] = 0;
+    }
+    return SM_OK;
+}
+
+int sm_get_timing(sm_ctx* ctx, int stage, double* total_ms, long long* count)
+{
+    if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
+    if (stage < 0 || stage >= SM_NUM_STAGES) return fail(ctx, SM_E_ARG, "stage %d out of range", stage);
+    harvest_timing(ctx);
+    if (total_ms) *total_ms = ctx->stage_ms[stage];
+    if (count) *count = ctx->stage_n[stage];
+    return SM_OK;
+}
+
+long long sm_debug_fetch(sm_ctx* ctx, int what, void* host, size_t bytes)
+{
+    if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
+    const size_t et = ctx->last_cost == SM_COST_CENSUS ? 1 : 2;
+    const size_t cells = (size_t)ctx->lastH * ctx->last_width1 * ctx->lastD;
+    size_t need;
+    const void* src;
+    switch (what) {
+    case 0: need = cells * et; src = ctx->cost.p; break;
+    case 1: need = cells * et * ctx->last_ndirs; src = ctx->L.p; break;
+    case 2: need = (size_t)ctx->lastH * ctx->lastW * 2; src = ctx->raw.p; break;
+    default: return fail(ctx, SM_E_ARG, "debug item %d unknown", what);
+    }
+    if (!host) return (long long)need;
+    if (bytes < need) return fail(ctx, SM_E_ARG, "host buffer too small (%zu < %zu)", bytes, need);
+    if (!src || need == 0) return 0;
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    HIP_TRY(ctx, hipMemcpy(host, src, need, hipMemcpyDeviceToHost));
+    return (long long)need;
+}
+
+const char* sm_last_error(sm_ctx* ctx)
+{
+    if (ctx) return ctx->err.c_str();
+    return g_thread_error.c_str();
+}
+
+}  // extern "C"

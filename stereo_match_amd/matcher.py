@@ -1,0 +1,164 @@
+"""OpenCV-compatible matcher objects backed by the gfx950 engine.
+
+Mirrors the surface the reference scripts use:
+
+* ``cv2.StereoSGBM_create(...)`` / ``.compute(left, right)`` —
+  ``stereo_vision/stereo_vision.py:153-163,178``, ``disparity_test.py:165,191``,
+  ``try_try.py:69,81``, ``mapTo3D_mc_cnn.py:81``.
+* ``cv2.ximgproc.createRightMatcher(left_matcher)`` —
+  ``stereo_vision/stereo_vision.py:171``.
+
+Return contract is OpenCV's: a fresh C-contiguous ``int16[H, W]`` holding
+disparity × 16, invalid pixels = ``(minDisparity - 1) * 16``.  Bad
+arguments raise ``ValueError`` (OpenCV raises ``cv2.error`` from CV_Assert);
+configurations the GPU path does not reproduce raise ``SmError``.
+
+Extension (north-star mode, no OpenCV counterpart): ``cost="census"``
+selects the 9×7 census + Hamming cost; ``mode=STEREO_SGBM_MODE_HH`` selects
+8 paths.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _lib
+from ._lib import SmError, SmParams
+
+# cv2.StereoSGBM mode constants
+STEREO_SGBM_MODE_SGBM = 0
+STEREO_SGBM_MODE_HH = 1
+STEREO_SGBM_MODE_SGBM_3WAY = 2
+STEREO_SGBM_MODE_HH4 = 3
+
+_COSTS = {"sgbm": _lib.SM_COST_SGBM, "census": _lib.SM_COST_CENSUS}
+
+
+def _is_torch_cuda(x) -> bool:
+    return type(x).__module__.startswith("torch") and getattr(x, "is_cuda", False)
+
+
+class StereoSGBM:
+    """cv2.StereoSGBM work-alike (same kwargs, getters/setters, compute)."""
+
+    def __init__(self, minDisparity=0, numDisparities=16, blockSize=3, P1=0, P2=0, disp12MaxDiff=0,
+                 preFilterCap=0, uniquenessRatio=0, speckleWindowSize=0, speckleRange=0,
+                 mode=STEREO_SGBM_MODE_SGBM, cost="sgbm", device=0):
+        self.minDisparity = int(minDisparity)
+        self.numDisparities = int(numDisparities)
+        self.blockSize = int(blockSize)
+        self.P1 = int(P1)
+        self.P2 = int(P2)
+        self.disp12MaxDiff = int(disp12MaxDiff)
+        self.preFilterCap = int(preFilterCap)
+        self.uniquenessRatio = int(uniquenessRatio)
+        self.speckleWindowSize = int(speckleWindowSize)
+        self.speckleRange = int(speckleRange)
+        self.mode = int(mode)
+        if cost not in _COSTS:
+            raise ValueError(f"cost must be one of {sorted(_COSTS)}")
+        self.cost = cost
+        self.device = int(device)
+
+    # --- cv::StereoMatcher / cv::StereoSGBM accessors --------------------
+    def getMinDisparity(self): return self.minDisparity
+    def setMinDisparity(self, v): self.minDisparity = int(v)
+    def getNumDisparities(self): return self.numDisparities
+    def setNumDisparities(self, v): self.numDisparities = int(v)
+    def getBlockSize(self): return self.blockSize
+    def setBlockSize(self, v): self.blockSize = int(v)
+    def getP1(self): return self.P1
+    def setP1(self, v): self.P1 = int(v)
+    def getP2(self): return self.P2
+    def setP2(self, v): self.P2 = int(v)
+    def getDisp12MaxDiff(self): return self.disp12MaxDiff
+    def setDisp12MaxDiff(self, v): self.disp12MaxDiff = int(v)
+    def getPreFilterCap(self): return self.preFilterCap
+    def setPreFilterCap(self, v): self.preFilterCap = int(v)
+    def getUniquenessRatio(self): return self.uniquenessRatio
+    def setUniquenessRatio(self, v): self.uniquenessRatio = int(v)
+    def getSpeckleWindowSize(self): return self.speckleWindowSize
+    def setSpeckleWindowSize(self, v): self.speckleWindowSize = int(v)
+    def getSpeckleRange(self): return self.speckleRange
+    def setSpeckleRange(self, v): self.speckleRange = int(v)
+    def getMode(self): return self.mode
+    def setMode(self, v): self.mode = int(v)
+
+    def params(self) -> SmParams:
+        if self.mode == STEREO_SGBM_MODE_SGBM:
+            paths = _lib.SM_MODE_SGBM
+        elif self.mode == STEREO_SGBM_MODE_HH:
+            paths = _lib.SM_MODE_HH
+        else:
+            raise SmError(_lib.SM_E_UNSUPPORTED,
+                          f"StereoSGBM mode {self.mode} (3WAY/HH4) is not implemented on the GPU path")
+        return SmParams(self.minDisparity, self.numDisparities, self.blockSize, self.P1, self.P2,
+                        self.disp12MaxDiff, self.uniquenessRatio, self.preFilterCap,
+                        self.speckleWindowSize, self.speckleRange, _COSTS[self.cost], paths)
+
+    def compute(self, left, right, disparity=None):
+        """StereoSGBM::compute.  numpy in → numpy out (synchronous);
+        torch CUDA tensors in → torch int16 tensor out on the same device
+        (enqueued on torch's current stream)."""
+        prm = self.params()
+        if _is_torch_cuda(left) or _is_torch_cuda(right):
+            return _compute_torch(left, right, prm)
+        left = np.asarray(left)
+        right = np.asarray(right)
+        _check_pair(left, right)
+        out = _lib.engine(self.device).compute(left, right, prm)
+        if disparity is not None:
+            np.copyto(disparity, out)
+            return disparity
+        return out
+
+
+def _check_pair(left, right):
+    if left.shape != right.shape or left.dtype != right.dtype:
+        raise ValueError("left and right images must have the same size and type")
+    if left.dtype != np.uint8:
+        raise ValueError("images must be CV_8U (uint8)")
+    if left.ndim == 3:
+        raise SmError(_lib.SM_E_UNSUPPORTED, "multi-channel input is not implemented on the GPU path; "
+                      "convert with cvtColor(BGR2GRAY) as disparity_calculation.py:286 does")
+    if left.ndim != 2 or left.size == 0:
+        raise ValueError("images must be non-empty 2-D arrays")
+
+
+def _compute_torch(left, right, prm: SmParams):
+    import torch
+
+    if left.shape != right.shape or left.dtype != torch.uint8 or right.dtype != torch.uint8:
+        raise ValueError("left/right must be same-shape torch.uint8 tensors")
+    if left.dim() != 2 or left.device != right.device:
+        raise ValueError("left/right must be 2-D tensors on the same device")
+    left = left.contiguous()
+    right = right.contiguous()
+    H, W = left.shape
+    out = torch.empty((H, W), dtype=torch.int16, device=left.device)
+    eng = _lib.engine(left.device.index or 0)
+    eng.set_stream(torch.cuda.current_stream(left.device).cuda_stream)
+    eng.compute_device(left.data_ptr(), right.data_ptr(), H, W, W, prm, out.data_ptr())
+    return out
+
+
+def StereoSGBM_create(minDisparity=0, numDisparities=16, blockSize=3, P1=0, P2=0, disp12MaxDiff=0,
+                      preFilterCap=0, uniquenessRatio=0, speckleWindowSize=0, speckleRange=0,
+                      mode=STEREO_SGBM_MODE_SGBM, cost="sgbm", device=0):
+    """cv2.StereoSGBM_create (reference: stereo_vision/stereo_vision.py:153)."""
+    return StereoSGBM(minDisparity, numDisparities, blockSize, P1, P2, disp12MaxDiff, preFilterCap,
+                      uniquenessRatio, speckleWindowSize, speckleRange, mode, cost, device)
+
+
+def createRightMatcher(matcher_left: StereoSGBM) -> StereoSGBM:
+    """cv2.ximgproc.createRightMatcher (reference: stereo_vision/stereo_vision.py:171).
+
+    minDisparity = -(minD + numD) + 1, uniquenessRatio 0, disp12MaxDiff 1e6,
+    speckleWindowSize 0; P1, P2, mode, preFilterCap and blockSize copied.
+    """
+    if not isinstance(matcher_left, StereoSGBM):
+        raise SmError(_lib.SM_E_UNSUPPORTED, "createRightMatcher: only StereoSGBM matchers are implemented")
+    m = matcher_left
+    return StereoSGBM(minDisparity=-(m.minDisparity + m.numDisparities) + 1, numDisparities=m.numDisparities,
+                      blockSize=m.blockSize, P1=m.P1, P2=m.P2, disp12MaxDiff=1000000,
+                      preFilterCap=m.preFilterCap, uniquenessRatio=0, speckleWindowSize=0,
+                      speckleRange=m.speckleRange, mode=m.mode, cost=m.cost, device=m.device)

@@ -1,0 +1,193 @@
+"""GPU parity: the HIP path (through the C-ABI) against the CPU restatement.
+
+Bar: bit-exact int16 output (integer WTA index AND the integer sub-pixel
+value — OpenCV's sub-pixel step is integer arithmetic, so the north-star's
+1e-4 float tolerance is met with zero error).  Parity with OpenCV itself is
+unpinned (see oracle/sgm_np.py).
+"""
+import numpy as np
+import pytest
+
+from oracle import ref_c, sgm_np
+from stereo_match_amd import _lib, synthetic
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    e = _lib.Engine(0)
+    yield e
+    e.close()
+
+
+def run(eng, left, right, p):
+    return eng.compute(left, right, synthetic.to_sm_params(p))
+
+
+def test_golden_fixtures(eng, golden_cases):
+    for name, left, right, p, expected, raw in golden_cases:
+        out = run(eng, left, right, p)
+        assert np.array_equal(out, expected), f"{name}: {np.sum(out != expected)} px differ"
+        got_raw = np.frombuffer(eng.debug_fetch(2), np.int16).reshape(left.shape)
+        assert np.array_equal(got_raw, raw), name
+
+
+@pytest.mark.parametrize("cost", [0, 1])
+def test_cost_volume_matches_oracle(eng, cost):
+    left, right, _ = synthetic.random_dot_pair(40, 120, 32, seed=7)
+    p = synthetic.headline_params(32) if cost else synthetic.parity_params(32)
+    run(eng, left, right, p)
+    C = sgm_np.cost_volume(left, right, sgm_np.normalize_params(p))
+    dt = np.uint8 if cost else np.uint16
+    got = np.frombuffer(eng.debug_fetch(0), dt).reshape(C.shape)
+    assert np.array_equal(got.astype(np.int64), C)
+
+
+@pytest.mark.parametrize("cost,mode", [(1, 8), (0, 5), (0, 8)])
+def test_path_volumes_match_oracle(eng, cost, mode):
+    left, right, _ = synthetic.random_dot_pair(33, 101, 32, seed=8)
+    p = dict(synthetic.headline_params(32) if cost else synthetic.parity_params(32), mode=mode)
+    run(eng, left, right, p)
+    prm = sgm_np.normalize_params(p)
+    C = sgm_np.cost_volume(left, right, prm)
+    dt = np.uint8 if cost else np.uint16
+    vols = np.frombuffer(eng.debug_fetch(1), dt).reshape((mode,) + C.shape)
+    # engine direction order: E, W, SE, S, SW, NE, N, NW
+    order = [(1, 0), (-1, 0), (1, 1), (0, 1), (-1, 1), (1, -1), (0, -1), (-1, -1)][:mode]
+    for k, d in enumerate(order):
+        L = sgm_np.aggregate_path(C, d, prm["P1"], prm["P2"])
+        assert np.array_equal(vols[k].astype(np.int64), L), f"direction {d}"
+
+
+CASES = []
+_rng = np.random.default_rng(1234)
+for _i in range(36):
+    D = int(_rng.choice([16, 32, 48, 64, 96, 128, 160, 256]))
+    H = int(_rng.integers(1, 50))
+    W = int(_rng.integers(D + 1, D + 200)) if _rng.random() < 0.8 else int(_rng.integers(1, D + 3))
+    CASES.append(dict(H=H, W=W, D=D, minD=int(_rng.choice([0, 0, 0, 5, -9, -D + 1])),
+                      cost=int(_rng.integers(0, 2)), mode=int(_rng.choice([5, 8])),
+                      bs=int(_rng.choice([1, 3, 5, 7])), uniq=int(_rng.choice([0, 10, 15])),
+                      d12=int(_rng.choice([1, 2, 1000000])), seed=int(_rng.integers(0, 1 << 30))))
+
+
+@pytest.mark.parametrize("c", CASES, ids=lambda c: "H{H}W{W}D{D}m{minD}c{cost}p{mode}".format(**c))
+def test_random_shapes_vs_c_oracle(eng, c):
+    left, right, _ = synthetic.random_dot_pair(c["H"], c["W"], c["D"], seed=c["seed"])
+    if c["cost"]:
+        p = dict(synthetic.headline_params(c["D"]), minDisparity=c["minD"], mode=c["mode"],
+                 uniquenessRatio=c["uniq"], disp12MaxDiff=c["d12"])
+    else:
+        bs = c["bs"]
+        p = dict(synthetic.parity_params(c["D"]), minDisparity=c["minD"], mode=c["mode"], blockSize=bs,
+                 P1=8 * bs * bs, P2=32 * bs * bs, uniquenessRatio=c["uniq"], disp12MaxDiff=c["d12"])
+    expected = ref_c.compute(left, right, p)
+    out = run(eng, left, right, p)
+    assert np.array_equal(out, expected), f"{np.sum(out != expected)} px differ"
+
+
+@pytest.mark.parametrize("name,cost,mode", [("kitti", 1, 8), ("kitti", 0, 5), ("kitti", 0, 8),
+                                            ("kitti", 1, 5), ("mccnn", 1, 8)])
+def test_full_size_bit_exact(eng, name, cost, mode):
+    H, W, D = synthetic.CONFIGS[name]
+    left, right, gt = synthetic.random_dot_pair(H, W, D, seed=42)
+    p = dict(synthetic.headline_params(D) if cost else synthetic.parity_params(D), mode=mode)
+    out = run(eng, left, right, p)
+    expected = ref_c.compute(left, right, p)
+    assert np.array_equal(out, expected), f"{np.sum(out != expected)} px differ"
+    valid = out >= 0
+    assert valid.mean() > 0.8
+    assert np.mean(np.abs(((out.astype(np.int64) + 8) >> 4) - gt)[valid] <= 1) > 0.98
+
+
+@pytest.mark.slow
+def test_middlebury_full_size(eng):
+    H, W, D = synthetic.CONFIGS["middlebury"]
+    left, right, gt = synthetic.random_dot_pair(H, W, D, seed=9)
+    p = synthetic.headline_params(D)
+    out = run(eng, left, right, p)
+    again = run(eng, left, right, p)
+    assert np.array_equal(out, again)  # deterministic
+    valid = out >= 0
+    assert valid.mean() > 0.8
+    assert np.mean(np.abs(((out.astype(np.int64) + 8) >> 4) - gt)[valid] <= 1) > 0.98
+    # bit-exact on a full-width band (rows cut so the C oracle stays quick;
+    # a band is a valid image of its own)
+    band = slice(700, 900)
+    lb, rb = np.ascontiguousarray(left[band]), np.ascontiguousarray(right[band])
+    assert np.array_equal(run(eng, lb, rb, p), ref_c.compute(lb, rb, p))
+
+
+def test_batch_device_matches_single(eng):
+    import torch
+
+    H, W, D = 60, 200, 64
+    pairs = [synthetic.random_dot_pair(H, W, D, seed=s)[:2] for s in range(3)]
+    L = torch.tensor(np.stack([a for a, _ in pairs]), device="cuda")
+    R = torch.tensor(np.stack([b for _, b in pairs]), device="cuda")
+    out = torch.empty((3, H, W), dtype=torch.int16, device="cuda")
+    p = synthetic.headline_params(D)
+    eng.set_stream(torch.cuda.current_stream().cuda_stream)
+    eng.compute_batch_device(L.data_ptr(), R.data_ptr(), 3, H * W, H, W, W, synthetic.to_sm_params(p),
+                             out.data_ptr())
+    torch.cuda.synchronize()
+    eng.set_stream(None)
+    for i, (a, b) in enumerate(pairs):
+        assert np.array_equal(out[i].cpu().numpy(), ref_c.compute(a, b, p))
+
+
+def test_torch_tensor_interface():
+    import torch
+
+    import stereo_match_amd as sm
+
+    left, right, _ = synthetic.random_dot_pair(50, 150, 32, seed=3)
+    m = sm.StereoSGBM_create(numDisparities=32, blockSize=5, P1=600, P2=2400, disp12MaxDiff=1,
+                             uniquenessRatio=15, preFilterCap=63)
+    a = m.compute(left, right)
+    t = m.compute(torch.tensor(left, device="cuda"), torch.tensor(right, device="cuda"))
+    assert t.dtype == torch.int16 and t.is_cuda
+    assert np.array_equal(t.cpu().numpy(), a)
+    assert np.array_equal(a, ref_c.compute(left, right, synthetic.parity_params(32)))
+
+
+def test_compute_disparity_left_matcher_semantics():
+    """compute_disparity's displ: createDisparityWLSFilter (called before
+    compute, stereo_vision.py:172 vs :178) sets uniqueness 0 / disp12 1e6."""
+    import stereo_match_amd as sm
+    from stereo_match_amd import wls
+
+    s = dict(sm.DEFAULT_SETTINGS, window_size=5, num_disparities=32)
+    left, right, _ = synthetic.random_dot_pair(48, 160, 32, seed=4)
+    lm = sm.matcher_from_settings(s)
+    rm = sm.createRightMatcher(lm)
+    wls.createDisparityWLSFilter(lm)
+    displ = lm.compute(left, right)
+    dispr = rm.compute(right, left)
+    p = dict(synthetic.parity_params(32), uniquenessRatio=0, disp12MaxDiff=1000000)
+    assert np.array_equal(displ, ref_c.compute(left, right, p))
+    assert np.array_equal(dispr, ref_c.compute(right, left, sgm_np.right_matcher_params(
+        synthetic.parity_params(32))))
+
+
+def test_unsupported_and_bad_args_raise(eng):
+    l = np.zeros((10, 40), np.uint8)
+    with pytest.raises(_lib.SmError):
+        run(eng, l, l, dict(synthetic.parity_params(16), speckleWindowSize=50))
+    with pytest.raises(ValueError):
+        run(eng, l, l, dict(synthetic.parity_params(16), numDisparities=24))
+    with pytest.raises(_lib.SmError):
+        run(eng, l, l, dict(synthetic.parity_params(16), blockSize=23))
+
+
+def test_timing_counters(eng):
+    left, right, _ = synthetic.random_dot_pair(40, 200, 64, seed=5)
+    eng.set_timing(True)
+    eng.reset_timing()
+    for _ in range(3):
+        run(eng, left, right, synthetic.headline_params(64))
+    t = eng.timing()
+    eng.set_timing(False)
+    assert t["paths"][1] == 3 and t["total"][1] == 3
+    assert 0 < t["paths"][0] <= t["total"][0]

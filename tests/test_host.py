@@ -1,0 +1,112 @@
+"""Host-side logic of the drop-in (no GPU compute): settings parsing,
+matcher construction, argument checks, the C-ABI symbol table."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+import stereo_match_amd as sm
+from stereo_match_amd import _lib, matcher, settings, wls
+from stereo_match_amd.stereo_vision import matcher_from_settings
+
+
+def test_library_exports_every_header_symbol():
+    lib = _lib.load()
+    names = _lib.header_symbols()
+    assert len(names) >= 14
+    for n in names:
+        assert hasattr(lib, n), n
+    assert lib.sm_version().startswith(b"stereo_match_amd")
+
+
+def test_c_abi_struct_matches_header():
+    text = open(_lib.HEADER_PATH).read()
+    body = text[text.index("typedef struct sm_params"):text.index("} sm_params;")]
+    import re
+    body = re.sub(r"/\*.*?\*/", "", body.split("{", 1)[1], flags=re.S)
+    fields = [n.strip() for decl in body.split(";") if decl.strip()
+              for n in decl.strip()[len("int"):].split(",")]
+    assert [f for f, _ in _lib.SmParams._fields_] == fields
+
+
+def test_right_matcher_params_via_abi():
+    p = _lib.SmParams(0, 160, 5, 600, 2400, 1, 15, 63, 0, 2, 0, 5)
+    r = _lib.right_matcher_params(p)
+    assert (r.min_disparity, r.num_disparities, r.uniqueness_ratio, r.disp12_max_diff,
+            r.speckle_window_size) == (-159, 160, 0, 1000000, 0)
+    assert (r.P1, r.P2, r.block_size, r.pre_filter_cap, r.mode) == (600, 2400, 5, 63, 5)
+
+
+def test_parse_config_file(tmp_path):
+    assert settings.parse_config_file(None) == settings.DEFAULT_SETTINGS
+    assert settings.parse_config_file(str(tmp_path / "missing.ini")) == settings.DEFAULT_SETTINGS
+    ini = tmp_path / "settings.ini"
+    ini.write_text("[disparity]\nwindow_size = 5\nmin_disparity = 0\nnum_disparities = 160\nblock_size = 5\n"
+                   "disp12_max_diff = 1\nuniqueness_ratio = 15\nspeckle_window_size = 0\nspeckle_range=2\n"
+                   "pre_filter_cap = 63\nlmbda = 80000\nsigma = 1.2\ncost = census\npaths = 8\n")
+    s = settings.parse_config_file(str(ini))
+    assert s["window_size"] == 5 and s["num_disparities"] == 160 and s["sigma"] == 1.2
+    assert s["cost"] == "census" and s["paths"] == 8 and s["mode"] == "P"
+
+
+def test_matcher_from_settings_p1_p2():
+    s = dict(settings.DEFAULT_SETTINGS, window_size=5)
+    m = matcher_from_settings(s)
+    assert (m.getP1(), m.getP2()) == (600, 2400)
+    assert m.getNumDisparities() == 160 and m.getBlockSize() == 5 and m.getMode() == sm.STEREO_SGBM_MODE_SGBM
+    m3 = matcher_from_settings(settings.DEFAULT_SETTINGS)
+    assert (m3.getP1(), m3.getP2()) == (216, 864)
+    assert matcher_from_settings(dict(s, paths=8, cost="census")).params().mode == 8
+
+
+def test_method_errors_like_reference():
+    with pytest.raises(RuntimeError, match="Method not supported"):
+        matcher_from_settings(settings.DEFAULT_SETTINGS, method="ELAS")
+    with pytest.raises(sm.SmError):
+        matcher_from_settings(settings.DEFAULT_SETTINGS, method="BM")
+
+
+def test_create_right_matcher():
+    m = sm.StereoSGBM_create(minDisparity=3, numDisparities=64, blockSize=7, P1=10, P2=50,
+                             disp12MaxDiff=2, uniquenessRatio=9, preFilterCap=31, mode=sm.STEREO_SGBM_MODE_HH)
+    r = sm.createRightMatcher(m)
+    assert r.getMinDisparity() == -(3 + 64) + 1 and r.getNumDisparities() == 64
+    assert (r.getUniquenessRatio(), r.getDisp12MaxDiff(), r.getSpeckleWindowSize()) == (0, 1000000, 0)
+    assert (r.getP1(), r.getP2(), r.getBlockSize(), r.getPreFilterCap(), r.getMode()) == (10, 50, 7, 31, 1)
+
+
+def test_wls_factory_mutates_left_matcher_like_ximgproc():
+    m = sm.StereoSGBM_create(numDisparities=160, blockSize=5, disp12MaxDiff=1, uniquenessRatio=15,
+                             speckleWindowSize=100)
+    f = wls.createDisparityWLSFilter(m)
+    assert (m.getDisp12MaxDiff(), m.getSpeckleWindowSize(), m.getUniquenessRatio()) == (1000000, 0, 0)
+    assert f.getDepthDiscontinuityRadius() == 3 and f.left_offset == 160 and f.right_offset == 0
+
+
+@pytest.mark.parametrize("left,right,exc", [
+    (np.zeros((4, 40), np.uint8), np.zeros((4, 41), np.uint8), ValueError),
+    (np.zeros((4, 40), np.uint16), np.zeros((4, 40), np.uint16), ValueError),
+    (np.zeros((0, 40), np.uint8), np.zeros((0, 40), np.uint8), ValueError),
+    (np.zeros((4, 40, 3), np.uint8), np.zeros((4, 40, 3), np.uint8), sm.SmError),
+])
+def test_bad_inputs_raise_before_gpu(left, right, exc):
+    with pytest.raises(exc):
+        sm.StereoSGBM_create().compute(left, right)
+
+
+def test_unsupported_modes_raise():
+    with pytest.raises(sm.SmError):
+        sm.StereoSGBM_create(mode=sm.STEREO_SGBM_MODE_SGBM_3WAY).params()
+    with pytest.raises(ValueError):
+        sm.StereoSGBM_create(cost="sad")
+
+
+def test_product_package_never_imports_oracle():
+    root = os.path.dirname(sm.__file__)
+    for dirpath, _, files in os.walk(root):
+        for f in files:
+            if f.endswith(".py"):
+                src = open(os.path.join(dirpath, f)).read()
+                assert "oracle" not in src.replace("oracle/", "").split("\n")[0:0] or True
+                assert "import oracle" not in src and "from oracle" not in src, f
