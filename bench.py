@@ -124,12 +124,17 @@ def main():
         width1 = W - D
         vol = H * width1 * D
         P_dirs = 8 if args.mode == "census8" else 5
-        eb = 1 if args.mode == "census8" else 2  # bytes per cost / path element
-        paths_ms, paths_n = stages["paths"]
-        paths_avg_s = paths_ms / 1e3 / max(paths_n, 1)
-        # dominant kernel = SGM path aggregation: reads the cost volume once per
-        # direction and writes one path volume per direction
-        alg_bytes_paths = P_dirs * vol * eb * 2
+        eb = 1 if args.mode == "census8" else 2  # bytes per path element
+        paths_ms, paths_launches, paths_pairs = stages["paths"]
+        paths_avg_s = paths_ms / 1e3 / max(paths_launches, 1)
+        pairs_per_launch = paths_pairs / max(paths_launches, 1)
+        # dominant kernel = SGM path aggregation: per pair it must
+        # write one path volume per direction and read its cost source once —
+        # the two census images (census on the fly) or, in OpenCV-parity mode,
+        # the int16 cost volume once per direction.
+        src_bytes = 2 * H * W * 8 if args.mode == "census8" else P_dirs * vol * 2
+        alg_bytes_pair = P_dirs * vol * eb + src_bytes
+        alg_bytes_paths = alg_bytes_pair * pairs_per_launch
         achieved = alg_bytes_paths / paths_avg_s / 1e9 if paths_avg_s > 0 else None
         traffic = None
         if os.path.exists(args.traffic_file):
@@ -142,8 +147,8 @@ def main():
                 traffic = None
         # SURVEY.md §8(d) whole-pipeline model: H·W·D·(1+P+4) + 2HW + 4HW per pair
         survey_bytes = cells * (1 + P_dirs + 4) + 2 * H * W + 4 * H * W
-        tot_ms, tot_n = stages["total"]
-        pair_s = tot_ms / 1e3 / max(tot_n, 1)
+        tot_ms, _, tot_pairs = stages["total"]
+        pair_s = tot_ms / 1e3 / max(tot_pairs, 1)
         line = {
             "metric": "stereo pairs/sec + Mpix·disp/sec, KITTI 1242×375 D=128 SGM, 1/2/4/8 GPU",
             "value": value,
@@ -173,6 +178,7 @@ def main():
                 "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                 "traffic": traffic,
                 "alg_bytes_per_launch": alg_bytes_paths,
+                "pairs_per_launch": pairs_per_launch,
                 "avg_launch_us": paths_avg_s * 1e6,
             },
             "pipeline_roofline": {
@@ -182,7 +188,7 @@ def main():
                 "achieved_GBs": survey_bytes / pair_s / 1e9 if pair_s > 0 else None,
                 "frac": survey_bytes / pair_s / 1e9 / HBM_PEAK_GBS if pair_s > 0 else None,
             },
-            "stage_us_per_pair": {k: v[0] * 1e3 / max(v[1], 1) for k, v in stages.items()},
+            "stage_us_per_pair": {k: v[0] * 1e3 / max(v[2], 1) for k, v in stages.items()},
             "valid_frac_pair0": valid_frac,
         }
         if world == 1 and args.cpu_baseline_pairs > 0:

@@ -60,9 +60,11 @@ typedef struct sm_ctx sm_ctx;
 int sm_create(int device, sm_ctx** out);
 void sm_destroy(sm_ctx* ctx);
 
-/* Use an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream);
- * NULL restores the context's own stream. */
+/* Enqueue on an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream);
+ * NULL means the device's default (null) stream. */
 int sm_set_stream(sm_ctx* ctx, void* hip_stream);
+/* Go back to the context's own non-blocking stream. */
+int sm_reset_stream(sm_ctx* ctx);
 
 /* StereoSGBM::compute(left, right) on host buffers (uint8, row stride in
  * bytes >= W).  disp_out: int16[H*W], disparity x16, invalid = (minD-1)*16.
@@ -78,7 +80,9 @@ int sm_compute_device(sm_ctx* ctx, const uint8_t* d_left, const uint8_t* d_right
 
 /* Batch of npairs same-size pairs on device pointers: pair i reads
  * d_left + i*pair_stride_bytes (same for right) and writes
- * d_disp_out + i*H*W.  Asynchronous on the context stream. */
+ * d_disp_out + i*H*W.  Asynchronous on the context stream.  Pairs are
+ * processed in launch groups (several pairs per kernel launch) so that one
+ * pair's serial horizontal paths overlap other pairs' work. */
 int sm_compute_batch_device(sm_ctx* ctx, const uint8_t* d_left, const uint8_t* d_right, int npairs,
                             size_t pair_stride_bytes, int H, int W, int stride, const sm_params* p,
                             int16_t* d_disp_out);
@@ -91,7 +95,8 @@ int sm_right_matcher_params(const sm_params* left, sm_params* right_out);
 int sm_synchronize(sm_ctx* ctx);
 
 /* Per-stage device timing with hipEvents on the context stream.
- * stage: 0 cost, 1 path aggregation, 2 WTA+LR, 3 median, 4 whole pipeline. */
+ * stage: 0 cost, 1 path aggregation, 2 WTA+LR, 3 median, 4 whole pipeline.
+ * total_ms: summed duration; launches: timed launches; pairs: pairs they covered. */
 #define SM_STAGE_COST 0
 #define SM_STAGE_PATHS 1
 #define SM_STAGE_WTA 2
@@ -99,13 +104,15 @@ int sm_synchronize(sm_ctx* ctx);
 #define SM_STAGE_TOTAL 4
 #define SM_NUM_STAGES 5
 int sm_set_timing(sm_ctx* ctx, int enable);
-int sm_get_timing(sm_ctx* ctx, int stage, double* total_ms, long long* count);
+int sm_get_timing(sm_ctx* ctx, int stage, double* total_ms, long long* launches, long long* pairs);
 int sm_reset_timing(sm_ctx* ctx);
 
-/* Debug / parity: copy an intermediate of the LAST computation to host.
+/* Debug / parity: copy an intermediate of the LAST pair computed to host.
  * what: 0 cost volume C[H][width1][D] (uint8 census / uint16 SGBM),
  *       1 path volumes L[P][H][width1][D] (uint8 census / uint16 SGBM),
- *       2 pre-median disparity int16[H][W].
+ *         direction order E, W, SE, S, SW, NE, N, NW,
+ *       2 pre-median disparity int16[H][W],
+ *       3 census images uint64[2][H][W] (census mode).
  * Returns the byte size when host == NULL. */
 long long sm_debug_fetch(sm_ctx* ctx, int what, void* host, size_t bytes);
 

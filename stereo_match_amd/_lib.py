@@ -40,6 +40,7 @@ _SIGS = {
     "sm_create": (_c.c_int, [_c.c_int, _c.POINTER(_c.c_void_p)]),
     "sm_destroy": (None, [_c.c_void_p]),
     "sm_set_stream": (_c.c_int, [_c.c_void_p, _c.c_void_p]),
+    "sm_reset_stream": (_c.c_int, [_c.c_void_p]),
     "sm_compute": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_int, _c.c_int, _c.c_int,
                               _c.POINTER(SmParams), _c.c_void_p]),
     "sm_compute_device": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_int, _c.c_int, _c.c_int,
@@ -49,7 +50,8 @@ _SIGS = {
     "sm_right_matcher_params": (_c.c_int, [_c.POINTER(SmParams), _c.POINTER(SmParams)]),
     "sm_synchronize": (_c.c_int, [_c.c_void_p]),
     "sm_set_timing": (_c.c_int, [_c.c_void_p, _c.c_int]),
-    "sm_get_timing": (_c.c_int, [_c.c_void_p, _c.c_int, _c.POINTER(_c.c_double), _c.POINTER(_c.c_longlong)]),
+    "sm_get_timing": (_c.c_int, [_c.c_void_p, _c.c_int, _c.POINTER(_c.c_double), _c.POINTER(_c.c_longlong),
+                                 _c.POINTER(_c.c_longlong)]),
     "sm_reset_timing": (_c.c_int, [_c.c_void_p]),
     "sm_debug_fetch": (_c.c_longlong, [_c.c_void_p, _c.c_int, _c.c_void_p, _c.c_size_t]),
     "sm_last_error": (_c.c_char_p, [_c.c_void_p]),
@@ -131,8 +133,13 @@ class Engine:
         if rc != SM_OK:
             _raise(rc, self.ctx)
 
-    def set_stream(self, stream_handle: int | None):
-        self._check(self._lib.sm_set_stream(self.ctx, ctypes.c_void_p(stream_handle or 0)))
+    def set_stream(self, stream_handle):
+        """Enqueue on this hipStream_t handle (0 = the null stream, e.g. torch's
+        default stream); None = back to the context's own stream."""
+        if stream_handle is None:
+            self._check(self._lib.sm_reset_stream(self.ctx))
+        else:
+            self._check(self._lib.sm_set_stream(self.ctx, ctypes.c_void_p(int(stream_handle))))
 
     # -- host arrays -------------------------------------------------------
     def compute(self, left: np.ndarray, right: np.ndarray, params: SmParams) -> np.ndarray:
@@ -167,12 +174,14 @@ class Engine:
         self._check(self._lib.sm_reset_timing(self.ctx))
 
     def timing(self) -> dict:
+        """{stage: (total_ms, launches, pairs)}"""
         out = {}
         for i, name in enumerate(STAGES):
             ms = ctypes.c_double()
             n = ctypes.c_longlong()
-            self._check(self._lib.sm_get_timing(self.ctx, i, ctypes.byref(ms), ctypes.byref(n)))
-            out[name] = (ms.value, n.value)
+            np_ = ctypes.c_longlong()
+            self._check(self._lib.sm_get_timing(self.ctx, i, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(np_)))
+            out[name] = (ms.value, n.value, np_.value)
         return out
 
     # -- debug ------------------------------------------------------------------

@@ -10,10 +10,13 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/stereo_match_amd.h"
-#include "sm_kernels.hpp"
+#include "sm_cost.hpp"
+#include "sm_paths.hpp"
+#include "sm_post.hpp"
 
 #define SM_VERSION "stereo_match_amd 0.1.0 (gfx950)"
 
@@ -32,7 +35,7 @@ struct Norm {
 };
 
 struct TimedEvent {
-    int stage;
+    int stage, pairs;
     hipEvent_t a, b;
 };
 
@@ -42,14 +45,17 @@ struct sm_ctx {
     int device = 0;
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
-    DevBuf img[2], census[2], planes, hsum, cost, L, raw, out;
-    // geometry of the last computation (for sm_debug_fetch)
-    int lastH = 0, lastW = 0, last_width1 = 0, lastD = 0, last_ndirs = 0, last_cost = 0;
+    DevBuf img[2], census[2], planes, hsum, cost, L, raw, out, dbg;
+    // geometry of the last computation (for sm_debug_fetch): its last pair
+    int lastH = 0, lastW = 0, last_width1 = 0, lastD = 0, last_ndirs = 0, last_cost = 0, last_minD = 0;
+    int last_minX1 = 0, last_index = 0;
+    size_t last_L_pair = 0;
     bool timing = false;
     std::vector<TimedEvent> pending;
     std::vector<hipEvent_t> free_events;
     double stage_ms[SM_NUM_STAGES] = {0};
-    long long stage_n[SM_NUM_STAGES] = {0};
+    long long stage_launches[SM_NUM_STAGES] = {0};
+    long long stage_pairs[SM_NUM_STAGES] = {0};
     std::string err;
 };
 
@@ -149,9 +155,9 @@ hipEvent_t get_event(sm_ctx* ctx)
 
 struct StageTimer {
     sm_ctx* ctx;
-    int stage;
+    int stage, pairs;
     hipEvent_t a = nullptr;
-    StageTimer(sm_ctx* c, int s) : ctx(c), stage(s)
+    StageTimer(sm_ctx* c, int s, int np) : ctx(c), stage(s), pairs(np)
     {
         if (ctx->timing) {
             a = get_event(ctx);
@@ -163,7 +169,7 @@ struct StageTimer {
         if (ctx->timing) {
             hipEvent_t b = get_event(ctx);
             (void)hipEventRecord(b, ctx->stream);
-            ctx->pending.push_back({stage, a, b});
+            ctx->pending.push_back({stage, pairs, a, b});
         }
     }
 };
@@ -175,55 +181,73 @@ void harvest_timing(sm_ctx* ctx)
         float ms = 0.f;
         (void)hipEventElapsedTime(&ms, t.a, t.b);
         ctx->stage_ms[t.stage] += ms;
-        ctx->stage_n[t.stage] += 1;
+        ctx->stage_launches[t.stage] += 1;
+        ctx->stage_pairs[t.stage] += t.pairs;
         ctx->free_events.push_back(t.a);
         ctx->free_events.push_back(t.b);
     }
     ctx->pending.clear();
 }
 
-// direction table: MODE_SGBM r0..r4 then MODE_HH's extra three.  The two
-// horizontal directions come first so their (longest) lines start early.
-const int kDirDx[8] = {1, -1, 1, 0, -1, 1, 0, -1};
-const int kDirDy[8] = {0, 0, 1, 1, 1, -1, -1, -1};
+// Output slots: 0 E, 1 W (horizontal family), 2 SE, 3 S, 4 SW (MODE_SGBM adds
+// these three), 5 NE, 6 N, 7 NW (MODE_HH / 8-path adds these three).
+const int kVdx[6] = {1, 0, -1, 1, 0, -1};
+const int kVdy[6] = {1, 1, 1, -1, -1, -1};
 
-template <int DPL>
-int launch_paths_wta(sm_ctx* ctx, const Norm& n, int H, int W)
+constexpr size_t kGroupBudget = size_t(24) << 30;  // bytes of path volumes per launch group
+constexpr int kMaxGroup = 16;
+
+template <int DPLV, bool CENSUS>
+int launch_paths_wta(sm_ctx* ctx, const Norm& n, int H, int W, int G, size_t L_pair, size_t slot_bytes,
+                     size_t census_pair, size_t cost_pair)
 {
-    const bool census = n.cost == SM_COST_CENSUS;
-    smk::PathArgs pa{};
-    pa.cost = ctx->cost.p;
-    pa.L = ctx->L.p;
-    pa.vol = (size_t)H * n.width1 * n.D;
+    using LT = typename std::conditional<CENSUS, uint8_t, uint16_t>::type;
+    constexpr int D = 16 * DPLV;
+    constexpr bool WIDE = D % 64 == 0;
+    constexpr int LANESH = WIDE ? 64 : 16;
+    constexpr int DPLH = D / LANESH;
+    smk::PathsArgs pa{};
+    pa.cl = (const uint64_t*)ctx->census[0].p;
+    pa.cr = (const uint64_t*)ctx->census[1].p;
+    pa.census_pair = census_pair;
+    pa.cost = (const uint16_t*)ctx->cost.p;
+    pa.cost_pair = cost_pair;
+    pa.L = (uint8_t*)ctx->L.p;
+    pa.slot_bytes = slot_bytes;
+    pa.L_pair_bytes = L_pair;
     pa.H = H;
+    pa.W = W;
     pa.width1 = n.width1;
     pa.D = n.D;
+    pa.minD = n.minD;
+    pa.minX1 = n.minX1;
     pa.P1 = n.P1;
     pa.P2 = n.P2;
-    pa.ndirs = n.ndirs;
+    const int lines_per_wg = 4 * (64 / LANESH);
+    pa.hblocks = (H + lines_per_wg - 1) / lines_per_wg;
+    pa.nv = n.ndirs - 2;
     int blocks = 0;
-    // MODE_SGBM = {E, W, SE, S, SW}; MODE_HH adds {NE, N, NW}
-    for (int k = 0; k < n.ndirs; k++) {
-        pa.dx[k] = kDirDx[k];
-        pa.dy[k] = kDirDy[k];
-        pa.blk_start[k] = blocks;
-        const int nlines = pa.dy[k] == 0 ? H : n.width1;
-        blocks += (nlines + 15) / 16;
+    for (int k = 0; k < pa.nv; k++) {
+        pa.v_dx[k] = kVdx[k];
+        pa.v_dy[k] = kVdy[k];
+        pa.v_slot[k] = 2 + k;
+        pa.v_line_lo[k] = kVdx[k] > 0 ? -(H - 1) : 0;
+        pa.v_nlines[k] = kVdx[k] == 0 ? n.width1 : n.width1 + H - 1;
+        pa.v_blk_start[k] = blocks;
+        blocks += (pa.v_nlines[k] + 15) / 16;
     }
-    pa.blk_start[n.ndirs] = blocks;
-    for (int k = n.ndirs + 1; k <= smk::kMaxDirs; k++) pa.blk_start[k] = blocks;
+    for (int k = pa.nv; k <= 6; k++) pa.v_blk_start[k] = blocks;
     {
-        StageTimer t(ctx, SM_STAGE_PATHS);
-        if (census)
-            hipLaunchKernelGGL((smk::k_sgm_paths<DPL, uint8_t, uint8_t>), dim3(blocks), dim3(256), 0, ctx->stream, pa);
-        else
-            hipLaunchKernelGGL((smk::k_sgm_paths<DPL, uint16_t, uint16_t>), dim3(blocks), dim3(256), 0, ctx->stream, pa);
+        StageTimer t(ctx, SM_STAGE_PATHS, G);
+        hipLaunchKernelGGL((smk::k_sgm_paths<DPLV, LANESH, DPLH, CENSUS, LT>), dim3(2 * pa.hblocks + blocks, G),
+                           dim3(256), 0, ctx->stream, pa);
         HIP_TRY(ctx, hipGetLastError());
     }
     smk::WtaArgs wa{};
-    wa.L = ctx->L.p;
-    wa.vol = pa.vol;
-    wa.ndirs = n.ndirs;
+    wa.L = (const uint8_t*)ctx->L.p;
+    wa.slot_bytes = slot_bytes;
+    wa.L_pair_bytes = L_pair;
+    wa.nslots = n.ndirs;
     wa.H = H;
     wa.W = W;
     wa.width1 = n.width1;
@@ -234,22 +258,23 @@ int launch_paths_wta(sm_ctx* ctx, const Norm& n, int H, int W)
     wa.disp12 = n.disp12;
     wa.disp = (int16_t*)ctx->raw.p;
     {
-        StageTimer t(ctx, SM_STAGE_WTA);
+        StageTimer t(ctx, SM_STAGE_WTA, G);
         const size_t smem = (size_t)W * 8;
-        if (census)
-            hipLaunchKernelGGL((smk::k_wta<DPL, uint8_t>), dim3(H), dim3(256), smem, ctx->stream, wa);
-        else
-            hipLaunchKernelGGL((smk::k_wta<DPL, uint16_t>), dim3(H), dim3(256), smem, ctx->stream, wa);
+        hipLaunchKernelGGL((smk::k_wta<DPLV, LT, 1024>), dim3(H, G), dim3(1024), smem, ctx->stream, wa);
         HIP_TRY(ctx, hipGetLastError());
     }
     return SM_OK;
 }
 
-int dispatch_dpl(sm_ctx* ctx, const Norm& n, int H, int W)
+int dispatch_dpl(sm_ctx* ctx, const Norm& n, int H, int W, int G, size_t L_pair, size_t slot_bytes,
+                 size_t census_pair, size_t cost_pair)
 {
+    const bool census = n.cost == SM_COST_CENSUS;
     switch (n.dpl) {
-#define CASE(k) \
-    case k: return launch_paths_wta<k>(ctx, n, H, W);
+#define CASE(k)                                                                                          \
+    case k:                                                                                              \
+        return census ? launch_paths_wta<k, true>(ctx, n, H, W, G, L_pair, slot_bytes, census_pair, cost_pair) \
+                      : launch_paths_wta<k, false>(ctx, n, H, W, G, L_pair, slot_bytes, census_pair, cost_pair);
         CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
         CASE(9) CASE(10) CASE(11) CASE(12) CASE(13) CASE(14) CASE(15) CASE(16)
 #undef CASE
@@ -263,105 +288,129 @@ int grid_for(size_t n)
     return (int)std::min<size_t>(std::max<size_t>(g, 1), 8192);
 }
 
-// One pair, device pointers, enqueued on ctx->stream.
-int run_pair(sm_ctx* ctx, const uint8_t* dL, const uint8_t* dR, int H, int W, int stride, const Norm& n,
-             int16_t* d_out)
+size_t elem_bytes(const Norm& n) { return n.cost == SM_COST_CENSUS ? 1 : 2; }
+
+int group_size(const Norm& n, int H, int npairs)
+{
+    const size_t per = (size_t)H * std::max(n.width1, 1) * n.D * elem_bytes(n) * n.ndirs;
+    size_t g = std::max<size_t>(1, kGroupBudget / std::max<size_t>(per, 1));
+    return (int)std::min<size_t>({g, (size_t)kMaxGroup, (size_t)std::max(npairs, 1)});
+}
+
+// G pairs (device pointers; pair i at dL + i*pair_stride), enqueued on ctx->stream.
+int run_group(sm_ctx* ctx, const uint8_t* dL, const uint8_t* dR, size_t pair_stride, int G, int H, int W,
+              int stride, const Norm& n, int16_t* d_out)
 {
     const int INVALID = (n.minD - 1) * 16;
-    ctx->lastH = H;
-    ctx->lastW = W;
-    ctx->last_width1 = std::max(n.width1, 0);
-    ctx->lastD = n.D;
-    ctx->last_ndirs = n.ndirs;
-    ctx->last_cost = n.cost;
-    StageTimer total(ctx, SM_STAGE_TOTAL);
+    StageTimer total(ctx, SM_STAGE_TOTAL, G);
     if (n.width1 <= 0) {
-        hipLaunchKernelGGL(smk::k_fill16, dim3(grid_for((size_t)H * W)), dim3(256), 0, ctx->stream, d_out,
-                           (size_t)H * W, (int16_t)INVALID);
-        HIP_TRY(ctx, hipGetLastError());
+        for (int i = 0; i < G; i++) {
+            hipLaunchKernelGGL(smk::k_fill16, dim3(grid_for((size_t)H * W)), dim3(256), 0, ctx->stream,
+                               d_out + (size_t)i * H * W, (size_t)H * W, (int16_t)INVALID);
+            HIP_TRY(ctx, hipGetLastError());
+        }
+        ctx->last_width1 = 0;
         return SM_OK;
     }
-    const size_t cells = (size_t)H * n.width1 * n.D;
-    const size_t lt = n.cost == SM_COST_CENSUS ? 1 : 2;
+    const size_t vol = (size_t)H * n.width1 * n.D;
+    const size_t eb = elem_bytes(n);
+    const size_t slot_bytes = (vol * eb + 255) & ~size_t(255);
+    const size_t L_pair = slot_bytes * n.ndirs;
+    const size_t census_pair = (size_t)H * W;
+    const size_t cost_pair = n.cost == SM_COST_CENSUS ? 0 : vol;
     int rc;
-    if ((rc = ensure(ctx, ctx->cost, cells * lt)) != SM_OK) return rc;
-    if ((rc = ensure(ctx, ctx->L, cells * lt * n.ndirs)) != SM_OK) return rc;
-    if ((rc = ensure(ctx, ctx->raw, (size_t)H * W * 2)) != SM_OK) return rc;
+    if ((rc = ensure(ctx, ctx->L, L_pair * G)) != SM_OK) return rc;
+    if ((rc = ensure(ctx, ctx->raw, (size_t)G * H * W * 2)) != SM_OK) return rc;
     {
-        StageTimer t(ctx, SM_STAGE_COST);
+        StageTimer t(ctx, SM_STAGE_COST, G);
         if (n.cost == SM_COST_CENSUS) {
             for (int i = 0; i < 2; i++)
-                if ((rc = ensure(ctx, ctx->census[i], (size_t)H * W * 8)) != SM_OK) return rc;
+                if ((rc = ensure(ctx, ctx->census[i], (size_t)G * census_pair * 8)) != SM_OK) return rc;
             smk::CensusArgs ca{};
             ca.img[0] = dL;
             ca.img[1] = dR;
             ca.out[0] = (uint64_t*)ctx->census[0].p;
             ca.out[1] = (uint64_t*)ctx->census[1].p;
+            ca.in_pair = pair_stride;
             ca.H = H;
             ca.W = W;
             ca.stride = stride;
-            hipLaunchKernelGGL(smk::k_census9x7, dim3((W + smk::CT_W - 1) / smk::CT_W, (H + smk::CT_H - 1) / smk::CT_H, 2),
+            hipLaunchKernelGGL(smk::k_census9x7,
+                               dim3((W + smk::CT_W - 1) / smk::CT_W, (H + smk::CT_H - 1) / smk::CT_H, 2 * G),
                                dim3(256), 0, ctx->stream, ca);
-            HIP_TRY(ctx, hipGetLastError());
-            smk::CensusCostArgs cc{};
-            cc.cl = ca.out[0];
-            cc.cr = ca.out[1];
-            cc.C = (uint8_t*)ctx->cost.p;
-            cc.H = H;
-            cc.W = W;
-            cc.width1 = n.width1;
-            cc.D = n.D;
-            cc.minD = n.minD;
-            cc.minX1 = n.minX1;
-            hipLaunchKernelGGL(smk::k_census_cost, dim3(grid_for(cells / 8)), dim3(256), 0, ctx->stream, cc);
             HIP_TRY(ctx, hipGetLastError());
         } else {
             if ((rc = ensure(ctx, ctx->planes, (size_t)H * W * 12)) != SM_OK) return rc;
-            if ((rc = ensure(ctx, ctx->hsum, cells * 2)) != SM_OK) return rc;
-            smk::PrefilterArgs pf{};
-            pf.img[0] = dL;
-            pf.img[1] = dR;
-            pf.planes = (uint8_t*)ctx->planes.p;
-            pf.H = H;
-            pf.W = W;
-            pf.stride = stride;
-            pf.ftzero = n.ftzero;
-            hipLaunchKernelGGL(smk::k_sgbm_prefilter, dim3((W + 255) / 256, H, 2), dim3(256), 0, ctx->stream, pf);
-            HIP_TRY(ctx, hipGetLastError());
-            smk::HsumArgs hs{};
-            hs.planes = pf.planes;
-            hs.hsum = (uint16_t*)ctx->hsum.p;
-            hs.H = H;
-            hs.W = W;
-            hs.width1 = n.width1;
-            hs.D = n.D;
-            hs.minD = n.minD;
-            hs.minX1 = n.minX1;
-            hs.SW2 = n.bs / 2;
-            hipLaunchKernelGGL(smk::k_sgbm_hsum, dim3(grid_for(cells)), dim3(256), 0, ctx->stream, hs);
-            HIP_TRY(ctx, hipGetLastError());
-            smk::VsumArgs vs{};
-            vs.hsum = hs.hsum;
-            vs.C = (uint16_t*)ctx->cost.p;
-            vs.H = H;
-            vs.width1 = n.width1;
-            vs.D = n.D;
-            vs.SH2 = n.bs / 2;
-            vs.hh = n.mode == SM_MODE_HH;
-            hipLaunchKernelGGL(smk::k_sgbm_vsum, dim3(grid_for(cells)), dim3(256), 0, ctx->stream, vs);
-            HIP_TRY(ctx, hipGetLastError());
+            if ((rc = ensure(ctx, ctx->hsum, vol * 2)) != SM_OK) return rc;
+            if ((rc = ensure(ctx, ctx->cost, (size_t)G * vol * 2)) != SM_OK) return rc;
+            for (int i = 0; i < G; i++) {
+                smk::PrefilterArgs pf{};
+                pf.img[0] = dL + (size_t)i * pair_stride;
+                pf.img[1] = dR + (size_t)i * pair_stride;
+                pf.planes = (uint8_t*)ctx->planes.p;
+                pf.H = H;
+                pf.W = W;
+                pf.stride = stride;
+                pf.ftzero = n.ftzero;
+                hipLaunchKernelGGL(smk::k_sgbm_prefilter, dim3((W + 255) / 256, H, 2), dim3(256), 0, ctx->stream, pf);
+                HIP_TRY(ctx, hipGetLastError());
+                smk::HsumArgs hs{};
+                hs.planes = pf.planes;
+                hs.hsum = (uint16_t*)ctx->hsum.p;
+                hs.H = H;
+                hs.W = W;
+                hs.width1 = n.width1;
+                hs.D = n.D;
+                hs.minD = n.minD;
+                hs.minX1 = n.minX1;
+                hs.SW2 = n.bs / 2;
+                hipLaunchKernelGGL(smk::k_sgbm_hsum, dim3(grid_for(vol)), dim3(256), 0, ctx->stream, hs);
+                HIP_TRY(ctx, hipGetLastError());
+                smk::VsumArgs vs{};
+                vs.hsum = hs.hsum;
+                vs.C = (uint16_t*)ctx->cost.p + (size_t)i * vol;
+                vs.H = H;
+                vs.width1 = n.width1;
+                vs.D = n.D;
+                vs.SH2 = n.bs / 2;
+                vs.hh = n.mode == SM_MODE_HH;
+                hipLaunchKernelGGL(smk::k_sgbm_vsum, dim3(grid_for(vol)), dim3(256), 0, ctx->stream, vs);
+                HIP_TRY(ctx, hipGetLastError());
+            }
         }
     }
-    if ((rc = dispatch_dpl(ctx, n, H, W)) != SM_OK) return rc;
+    if ((rc = dispatch_dpl(ctx, n, H, W, G, L_pair, slot_bytes, census_pair, cost_pair)) != SM_OK) return rc;
     {
-        StageTimer t(ctx, SM_STAGE_MEDIAN);
-        hipLaunchKernelGGL(smk::k_median3, dim3((W + 255) / 256, H), dim3(256), 0, ctx->stream,
-                           (const int16_t*)ctx->raw.p, d_out, H, W);
+        StageTimer t(ctx, SM_STAGE_MEDIAN, G);
+        hipLaunchKernelGGL(smk::k_median3, dim3((W + 255) / 256, H, G), dim3(256), 0, ctx->stream,
+                           (const int16_t*)ctx->raw.p, d_out, H, W, (size_t)H * W);
         HIP_TRY(ctx, hipGetLastError());
     }
+    ctx->last_width1 = n.width1;
+    ctx->last_index = G - 1;
+    ctx->last_L_pair = L_pair;
     return SM_OK;
 }
 
+int run_pairs(sm_ctx* ctx, const uint8_t* dL, const uint8_t* dR, size_t pair_stride, int npairs, int H, int W,
+              int stride, const Norm& n, int16_t* d_out)
+{
+    ctx->lastH = H;
+    ctx->lastW = W;
+    ctx->lastD = n.D;
+    ctx->last_ndirs = n.ndirs;
+    ctx->last_cost = n.cost;
+    ctx->last_minD = n.minD;
+    ctx->last_minX1 = n.minX1;
+    const int G = group_size(n, H, npairs);
+    for (int i = 0; i < npairs; i += G) {
+        const int g = std::min(G, npairs - i);
+        int rc = run_group(ctx, dL + (size_t)i * pair_stride, dR + (size_t)i * pair_stride, pair_stride, g, H, W,
+                           stride, n, d_out + (size_t)i * H * W);
+        if (rc != SM_OK) return rc;
+    }
+    return SM_OK;
+}
 }  // namespace
 
 extern "C" {
@@ -395,7 +444,7 @@ void sm_destroy(sm_ctx* ctx)
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
     DevBuf* bufs[] = {&ctx->img[0], &ctx->img[1], &ctx->census[0], &ctx->census[1], &ctx->planes, &ctx->hsum,
-                      &ctx->cost, &ctx->L, &ctx->raw, &ctx->out};
+                      &ctx->cost, &ctx->L, &ctx->raw, &ctx->out, &ctx->dbg};
     for (DevBuf* b : bufs)
         if (b->p) (void)hipFree(b->p);
     for (auto& t : ctx->pending) {
@@ -410,7 +459,14 @@ void sm_destroy(sm_ctx* ctx)
 int sm_set_stream(sm_ctx* ctx, void* hip_stream)
 {
     if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
-    ctx->stream = hip_stream ? (hipStream_t)hip_stream : ctx->own_stream;
+    ctx->stream = (hipStream_t)hip_stream;  // NULL = the device's default (null) stream
+    return SM_OK;
+}
+
+int sm_reset_stream(sm_ctx* ctx)
+{
+    if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
+    ctx->stream = ctx->own_stream;
     return SM_OK;
 }
 
@@ -435,7 +491,7 @@ int sm_compute_device(sm_ctx* ctx, const uint8_t* dL, const uint8_t* dR, int H, 
     int rc = normalize(ctx, p, H, W, n);
     if (rc != SM_OK) return rc;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    return run_pair(ctx, dL, dR, H, W, stride, n, d_out);
+    return run_pairs(ctx, dL, dR, 0, 1, H, W, stride, n, d_out);
 }
 
 int sm_compute_batch_device(sm_ctx* ctx, const uint8_t* dL, const uint8_t* dR, int npairs, size_t pair_stride,
@@ -449,12 +505,7 @@ int sm_compute_batch_device(sm_ctx* ctx, const uint8_t* dL, const uint8_t* dR, i
     int rc = normalize(ctx, p, H, W, n);
     if (rc != SM_OK) return rc;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    for (int i = 0; i < npairs; i++) {
-        rc = run_pair(ctx, dL + (size_t)i * pair_stride, dR + (size_t)i * pair_stride, H, W, stride, n,
-                      d_out + (size_t)i * H * W);
-        if (rc != SM_OK) return rc;
-    }
-    return SM_OK;
+    return run_pairs(ctx, dL, dR, pair_stride, npairs, H, W, stride, n, d_out);
 }
 
 int sm_compute(sm_ctx* ctx, const uint8_t* L, const uint8_t* R, int H, int W, int stride, const sm_params* p,
@@ -473,8 +524,8 @@ int sm_compute(sm_ctx* ctx, const uint8_t* L, const uint8_t* R, int H, int W, in
     if ((rc = ensure(ctx, ctx->out, img * 2)) != SM_OK) return rc;
     HIP_TRY(ctx, hipMemcpy2DAsync(ctx->img[0].p, W, L, stride, W, H, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipMemcpy2DAsync(ctx->img[1].p, W, R, stride, W, H, hipMemcpyHostToDevice, ctx->stream));
-    rc = run_pair(ctx, (const uint8_t*)ctx->img[0].p, (const uint8_t*)ctx->img[1].p, H, W, W, n,
-                  (int16_t*)ctx->out.p);
+    rc = run_pairs(ctx, (const uint8_t*)ctx->img[0].p, (const uint8_t*)ctx->img[1].p, 0, 1, H, W, W, n,
+                   (int16_t*)ctx->out.p);
     if (rc != SM_OK) return rc;
     HIP_TRY(ctx, hipMemcpyAsync(disp_out, ctx->out.p, img * 2, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
@@ -501,18 +552,20 @@ int sm_reset_timing(sm_ctx* ctx)
     harvest_timing(ctx);
     for (int i = 0; i < SM_NUM_STAGES; i++) {
         ctx->stage_ms[i] = 0;
-        ctx->stage_n[i] = 0;
+        ctx->stage_launches[i] = 0;
+        ctx->stage_pairs[i] = 0;
     }
     return SM_OK;
 }
 
-int sm_get_timing(sm_ctx* ctx, int stage, double* total_ms, long long* count)
+int sm_get_timing(sm_ctx* ctx, int stage, double* total_ms, long long* launches, long long* pairs)
 {
     if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
     if (stage < 0 || stage >= SM_NUM_STAGES) return fail(ctx, SM_E_ARG, "stage %d out of range", stage);
     harvest_timing(ctx);
     if (total_ms) *total_ms = ctx->stage_ms[stage];
-    if (count) *count = ctx->stage_n[stage];
+    if (launches) *launches = ctx->stage_launches[stage];
+    if (pairs) *pairs = ctx->stage_pairs[stage];
     return SM_OK;
 }
 
@@ -520,20 +573,56 @@ long long sm_debug_fetch(sm_ctx* ctx, int what, void* host, size_t bytes)
 {
     if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
     const size_t et = ctx->last_cost == SM_COST_CENSUS ? 1 : 2;
-    const size_t cells = (size_t)ctx->lastH * ctx->last_width1 * ctx->lastD;
+    const size_t vol = (size_t)ctx->lastH * ctx->last_width1 * ctx->lastD;
+    const size_t slot_bytes = (vol * et + 255) & ~size_t(255);
+    const size_t img = (size_t)ctx->lastH * ctx->lastW;
+    const int li = ctx->last_index;
     size_t need;
-    const void* src;
     switch (what) {
-    case 0: need = cells * et; src = ctx->cost.p; break;
-    case 1: need = cells * et * ctx->last_ndirs; src = ctx->L.p; break;
-    case 2: need = (size_t)ctx->lastH * ctx->lastW * 2; src = ctx->raw.p; break;
+    case 0: need = vol * et; break;
+    case 1: need = vol * et * ctx->last_ndirs; break;
+    case 2: need = img * 2; break;
+    case 3: need = img * 16; break;
     default: return fail(ctx, SM_E_ARG, "debug item %d unknown", what);
     }
     if (!host) return (long long)need;
     if (bytes < need) return fail(ctx, SM_E_ARG, "host buffer too small (%zu < %zu)", bytes, need);
-    if (!src || need == 0) return 0;
+    if (need == 0) return 0;
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    HIP_TRY(ctx, hipMemcpy(host, src, need, hipMemcpyDeviceToHost));
+    if (what == 0 && ctx->last_cost == SM_COST_CENSUS) {
+        int rc = ensure(ctx, ctx->dbg, need);
+        if (rc != SM_OK) return rc;
+        smk::CensusCostArgs cc{};
+        cc.cl = (const uint64_t*)ctx->census[0].p + (size_t)li * img;
+        cc.cr = (const uint64_t*)ctx->census[1].p + (size_t)li * img;
+        cc.C = (uint8_t*)ctx->dbg.p;
+        cc.H = ctx->lastH;
+        cc.W = ctx->lastW;
+        cc.width1 = ctx->last_width1;
+        cc.D = ctx->lastD;
+        cc.minD = ctx->last_minD;
+        cc.minX1 = ctx->last_minX1;
+        hipLaunchKernelGGL(smk::k_census_cost, dim3(grid_for(vol / 8)), dim3(256), 0, ctx->stream, cc);
+        HIP_TRY(ctx, hipGetLastError());
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        HIP_TRY(ctx, hipMemcpy(host, ctx->dbg.p, need, hipMemcpyDeviceToHost));
+        return (long long)need;
+    }
+    switch (what) {
+    case 0: HIP_TRY(ctx, hipMemcpy(host, (uint8_t*)ctx->cost.p + (size_t)li * vol * et, need, hipMemcpyDeviceToHost)); break;
+    case 1:
+        for (int k = 0; k < ctx->last_ndirs; k++)
+            HIP_TRY(ctx, hipMemcpy((uint8_t*)host + k * vol * et,
+                                   (uint8_t*)ctx->L.p + (size_t)li * ctx->last_L_pair + k * slot_bytes, vol * et,
+                                   hipMemcpyDeviceToHost));
+        break;
+    case 2: HIP_TRY(ctx, hipMemcpy(host, (int16_t*)ctx->raw.p + (size_t)li * img, need, hipMemcpyDeviceToHost)); break;
+    case 3:
+        HIP_TRY(ctx, hipMemcpy(host, (uint64_t*)ctx->census[0].p + (size_t)li * img, img * 8, hipMemcpyDeviceToHost));
+        HIP_TRY(ctx, hipMemcpy((uint8_t*)host + img * 8, (uint64_t*)ctx->census[1].p + (size_t)li * img, img * 8,
+                               hipMemcpyDeviceToHost));
+        break;
+    }
     return (long long)need;
 }
 

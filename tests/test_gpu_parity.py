@@ -44,6 +44,14 @@ def test_cost_volume_matches_oracle(eng, cost):
     assert np.array_equal(got.astype(np.int64), C)
 
 
+def test_census_images_match_oracle(eng):
+    left, right, _ = synthetic.random_dot_pair(37, 131, 32, seed=17)
+    run(eng, left, right, synthetic.headline_params(32))
+    got = np.frombuffer(eng.debug_fetch(3), np.uint64).reshape(2, 37, 131)
+    assert np.array_equal(got[0], sgm_np.census9x7(left))
+    assert np.array_equal(got[1], sgm_np.census9x7(right))
+
+
 @pytest.mark.parametrize("cost,mode", [(1, 8), (0, 5), (0, 8)])
 def test_path_volumes_match_oracle(eng, cost, mode):
     left, right, _ = synthetic.random_dot_pair(33, 101, 32, seed=8)
@@ -131,10 +139,18 @@ def test_batch_device_matches_single(eng):
     eng.set_stream(torch.cuda.current_stream().cuda_stream)
     eng.compute_batch_device(L.data_ptr(), R.data_ptr(), 3, H * W, H, W, W, synthetic.to_sm_params(p),
                              out.data_ptr())
-    torch.cuda.synchronize()
+    got = out.cpu().numpy()  # ordered after the engine's work: same stream
     eng.set_stream(None)
     for i, (a, b) in enumerate(pairs):
-        assert np.array_equal(out[i].cpu().numpy(), ref_c.compute(a, b, p))
+        assert np.array_equal(got[i], ref_c.compute(a, b, p))
+    # SGBM mode batch too (cost volume per pair inside one launch group)
+    q = synthetic.parity_params(D)
+    eng.compute_batch_device(L.data_ptr(), R.data_ptr(), 3, H * W, H, W, W, synthetic.to_sm_params(q),
+                             out.data_ptr())
+    eng.synchronize()
+    got = out.cpu().numpy()
+    for i, (a, b) in enumerate(pairs):
+        assert np.array_equal(got[i], ref_c.compute(a, b, q))
 
 
 def test_torch_tensor_interface():
