@@ -31,12 +31,20 @@ __device__ __forceinline__ uint32_t dpp(uint32_t old, uint32_t src)
     return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)src, CTRL, 0xF, 0xF, false);
 }
 
+// full permutations (every source lane valid): bound_ctrl lets the compiler
+// fuse the DPP move into the consuming VALU op (v_min_u32_dpp ...).
+template <int CTRL>
+__device__ __forceinline__ uint32_t perm_dpp(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true);
+}
+
 __device__ __forceinline__ uint32_t row16_min(uint32_t v)
 {
-    v = min(v, dpp<DPP_QP_XOR1>(v, v));
-    v = min(v, dpp<DPP_QP_XOR2>(v, v));
-    v = min(v, dpp<DPP_ROW_HALF_MIRROR>(v, v));
-    v = min(v, dpp<DPP_ROW_MIRROR>(v, v));
+    v = min(v, perm_dpp<DPP_QP_XOR1>(v));
+    v = min(v, perm_dpp<DPP_QP_XOR2>(v));
+    v = min(v, perm_dpp<DPP_ROW_HALF_MIRROR>(v));
+    v = min(v, perm_dpp<DPP_ROW_MIRROR>(v));
     return v;
 }
 
@@ -90,10 +98,10 @@ struct Line<64> {
 
 __device__ __forceinline__ uint32_t row16_or(uint32_t v)
 {
-    v |= dpp<DPP_QP_XOR1>(v, v);
-    v |= dpp<DPP_QP_XOR2>(v, v);
-    v |= dpp<DPP_ROW_HALF_MIRROR>(v, v);
-    v |= dpp<DPP_ROW_MIRROR>(v, v);
+    v |= perm_dpp<DPP_QP_XOR1>(v);
+    v |= perm_dpp<DPP_QP_XOR2>(v);
+    v |= perm_dpp<DPP_ROW_HALF_MIRROR>(v);
+    v |= perm_dpp<DPP_ROW_MIRROR>(v);
     return v;
 }
 
@@ -167,5 +175,134 @@ __device__ __forceinline__ void store_n(T* __restrict__ p, const uint32_t (&in)[
         for (int i = 0; i < N; i++) p[i] = (T)in[i];
     }
 }
+
+
+// ---------------------------------------------------------- buffer ops
+// Raw buffer descriptors (T8/T20 of the CDNA guide): 32-bit byte offsets,
+// hardware range check.  Stores at an offset >= num_records are dropped and
+// loads there return 0, which lets every per-step memory op stay
+// unconditional (no control-flow merge -> the compiler keeps counted
+// vmcnt waits instead of vmcnt(0)).
+using rsrc_t = __amdgpu_buffer_rsrc_t;
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+constexpr uint32_t kOOB = 0x80000000u;
+
+__device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint64_t bytes)
+{
+    const uint64_t p = (uint64_t)base;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
+    const uint32_t n = __builtin_amdgcn_readfirstlane((uint32_t)(bytes > 0xFFFFFFFFull ? 0xFFFFFFFFull : bytes));
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, (int)n, 0x00020000);
+}
+
+__device__ __forceinline__ uint64_t bload_u64(rsrc_t r, uint32_t off)
+{
+    const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+    return ((uint64_t)v.y << 32) | v.x;
+}
+
+// pack N small values (< 2^(8*sizeof(T))) into little-endian 32-bit words
+template <typename T, int N>
+__device__ __forceinline__ void pack_words(const uint32_t (&in)[N], uint32_t (&w)[(N * sizeof(T) + 3) / 4])
+{
+    constexpr int NW = (N * (int)sizeof(T) + 3) / 4;
+    if constexpr (sizeof(T) == 1) {
+#pragma unroll
+        for (int k = 0; k < NW; k++) {
+            const uint32_t a = in[4 * k];
+            const uint32_t b = 4 * k + 1 < N ? in[4 * k + 1] : 0u;
+            const uint32_t c = 4 * k + 2 < N ? in[4 * k + 2] : 0u;
+            const uint32_t d = 4 * k + 3 < N ? in[4 * k + 3] : 0u;
+            const uint32_t lo = __builtin_amdgcn_perm(b, a, 0x0c0c0400u);  // [a0, b0, 0, 0]
+            const uint32_t hi = __builtin_amdgcn_perm(d, c, 0x0c0c0400u);  // [c0, d0, 0, 0]
+            w[k] = __builtin_amdgcn_perm(hi, lo, 0x05040100u);             // [a0, b0, c0, d0]
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < NW; k++) {
+            const uint32_t a = in[2 * k];
+            const uint32_t b = 2 * k + 1 < N ? in[2 * k + 1] : 0u;
+            w[k] = __builtin_amdgcn_perm(b, a, 0x05040100u);  // [a0, a1, b0, b1]
+        }
+    }
+}
+
+// store N values of T at byte offset `off` (N*sizeof(T) bytes), split in
+// naturally aligned chunks of gcd(N*sizeof(T), 16) bytes
+template <typename T, int N>
+__device__ __forceinline__ void bstore_n(rsrc_t r, uint32_t off, const uint32_t (&in)[N])
+{
+    constexpr int BYTES = N * (int)sizeof(T);
+    constexpr int CH = (BYTES % 16 == 0) ? 16 : (BYTES % 8 == 0) ? 8 : (BYTES % 4 == 0) ? 4 : (BYTES % 2 == 0) ? 2 : 1;
+    if constexpr (CH >= 4) {
+        uint32_t w[(BYTES + 3) / 4];
+        pack_words<T, N>(in, w);
+#pragma unroll
+        for (int c = 0; c < BYTES / CH; c++) {
+            if constexpr (CH == 16) {
+                const u32x4 v = {w[4 * c], w[4 * c + 1], w[4 * c + 2], w[4 * c + 3]};
+                __builtin_amdgcn_raw_buffer_store_b128(v, r, off + 16 * c, 0, 0);
+            } else if constexpr (CH == 8) {
+                const u32x2 v = {w[2 * c], w[2 * c + 1]};
+                __builtin_amdgcn_raw_buffer_store_b64(v, r, off + 8 * c, 0, 0);
+            } else {
+                __builtin_amdgcn_raw_buffer_store_b32(w[c], r, off + 4 * c, 0, 0);
+            }
+        }
+    } else if constexpr (CH == 2) {
+        if constexpr (sizeof(T) == 2) {
+#pragma unroll
+            for (int i = 0; i < N; i++) __builtin_amdgcn_raw_buffer_store_b16((uint16_t)in[i], r, off + 2 * i, 0, 0);
+        } else {
+#pragma unroll
+            for (int i = 0; i < N / 2; i++)
+                __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(in[2 * i] | (in[2 * i + 1] << 8)), r, off + 2 * i, 0, 0);
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < N; i++) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)in[i], r, off + i, 0, 0);
+    }
+}
+
+// load N uint16 (raw words, unpacked later)
+template <int N>
+struct RawU16 {
+    static constexpr int BYTES = 2 * N;
+    static constexpr int WORDS = (BYTES + 3) / 4;
+    uint32_t w[WORDS];
+    __device__ __forceinline__ void load(rsrc_t r, uint32_t off)
+    {
+        if constexpr (BYTES % 16 == 0) {
+#pragma unroll
+            for (int c = 0; c < BYTES / 16; c++) {
+                const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off + 16 * c, 0, 0);
+                w[4 * c] = v.x; w[4 * c + 1] = v.y; w[4 * c + 2] = v.z; w[4 * c + 3] = v.w;
+            }
+        } else if constexpr (BYTES % 8 == 0) {
+#pragma unroll
+            for (int c = 0; c < BYTES / 8; c++) {
+                const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, off + 8 * c, 0, 0);
+                w[2 * c] = v.x; w[2 * c + 1] = v.y;
+            }
+        } else if constexpr (BYTES % 4 == 0) {
+#pragma unroll
+            for (int c = 0; c < WORDS; c++) w[c] = __builtin_amdgcn_raw_buffer_load_b32(r, off + 4 * c, 0, 0);
+        } else {
+#pragma unroll
+            for (int c = 0; c < N; c++) {
+                const uint32_t h = __builtin_amdgcn_raw_buffer_load_b16(r, off + 2 * c, 0, 0);
+                if (c & 1) w[c >> 1] |= h << 16;
+                else w[c >> 1] = h;
+            }
+        }
+    }
+    __device__ __forceinline__ void unpack(uint32_t (&C)[N]) const
+    {
+#pragma unroll
+        for (int i = 0; i < N; i++) C[i] = (w[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+    }
+};
 
 }  // namespace smk

@@ -61,61 +61,31 @@ __device__ __forceinline__ uint32_t sgm_step(const uint32_t (&Lp)[DPL], uint32_t
     return Line<LANES>::min(mn);
 }
 
-// raw (packed) cost words of DPL uint16 disparities, loaded ahead of use
-template <int DPL>
-struct RawCost {
-    static constexpr int WORDS = (DPL * 2 + 3) / 4;
-    uint32_t w[WORDS];
-    __device__ __forceinline__ void load(const uint16_t* p)
-    {
-        if constexpr (DPL % 8 == 0) {
-#pragma unroll
-            for (int c = 0; c < DPL / 8; c++) {
-                uint4 v = reinterpret_cast<const uint4*>(p)[c];
-                w[4 * c] = v.x; w[4 * c + 1] = v.y; w[4 * c + 2] = v.z; w[4 * c + 3] = v.w;
-            }
-        } else if constexpr (DPL % 4 == 0) {
-#pragma unroll
-            for (int c = 0; c < DPL / 4; c++) {
-                uint2 v = reinterpret_cast<const uint2*>(p)[c];
-                w[2 * c] = v.x; w[2 * c + 1] = v.y;
-            }
-        } else if constexpr (DPL % 2 == 0) {
-#pragma unroll
-            for (int c = 0; c < DPL / 2; c++) w[c] = reinterpret_cast<const uint32_t*>(p)[c];
-        } else {
-#pragma unroll
-            for (int c = 0; c < WORDS; c++) {
-                uint32_t lo = p[2 * c];
-                uint32_t hi = 2 * c + 1 < DPL ? p[2 * c + 1] : 0u;
-                w[c] = lo | (hi << 16);
-            }
-        }
-    }
-    __device__ __forceinline__ void unpack(uint32_t (&C)[DPL]) const
-    {
-#pragma unroll
-        for (int i = 0; i < DPL; i++) C[i] = (w[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
-    }
-};
-
 // ------------------------------------------------------- horizontal family
-template <int LANES, int DPL, bool CENSUS, typename LT>
-__device__ __forceinline__ void horz_family(const PathsArgs& a, int pair, int hb, uint64_t* stage)
+// Steps run in chunks of LANES; each chunk's left-census values and entering
+// right-census values (one per step and line) are loaded one chunk ahead and
+// staged in wave-private LDS.  Steps past the row end still execute (their
+// stores land out of range and are dropped) so the inner loop has no
+// conditional memory operation.
+template <int DIR, int LANES, int DPL, bool CENSUS, typename LT>
+__device__ __forceinline__ void horz_impl(const PathsArgs& a, int pair, int hb, uint64_t* stage)
 {
     constexpr int LPW = 64 / LANES;
-    const int dir = hb >= a.hblocks ? 1 : 0;  // 0: E (x increasing), 1: W (x decreasing)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int g = lane % LANES, kl = lane / LANES;
-    const int wline = ((hb - dir * a.hblocks) * 4 + wave) * LPW;
+    const int wline = ((hb - DIR * a.hblocks) * 4 + wave) * LPW;
     const int H = a.H, W = a.W, W1 = a.width1, D = a.D, minD = a.minD, minX1 = a.minX1;
     if (wline >= H) return;  // wave-uniform
     const bool line_ok = wline + kl < H;
     const int y = min(wline + kl, H - 1);
     const uint32_t P1 = (uint32_t)a.P1, P2 = (uint32_t)a.P2;
-    LT* __restrict__ Lrow = (LT*)(a.L + (size_t)pair * a.L_pair_bytes + (size_t)dir * a.slot_bytes) +
-                            (size_t)y * W1 * D + g * DPL;
-    auto Xof = [&](int s) { return dir == 0 ? minX1 + s : minX1 + W1 - 1 - s; };
+    const rsrc_t rout = make_rsrc(a.L + (size_t)pair * a.L_pair_bytes + (size_t)DIR * a.slot_bytes,
+                                  (uint64_t)H * W1 * D * sizeof(LT));
+    // byte offset of this lane's slice at step s: row y, x1 = DIR ? W1-1-s : s
+    constexpr int SGN = DIR == 0 ? 1 : -1;
+    const int step_bytes = SGN * D * (int)sizeof(LT);
+    const int off0 = (y * W1 + (DIR == 0 ? 0 : W1 - 1)) * D * (int)sizeof(LT) + g * DPL * (int)sizeof(LT);
+    const int nchunks = (W1 + LANES - 1) / LANES;
 
     uint32_t Lp[DPL];
 #pragma unroll
@@ -123,41 +93,34 @@ __device__ __forceinline__ void horz_family(const PathsArgs& a, int pair, int hb
     uint32_t minLp = 0;
 
     if constexpr (CENSUS) {
-        const uint64_t* __restrict__ clrow = a.cl + (size_t)pair * a.census_pair + (size_t)y * W;
-        const uint64_t* __restrict__ crrow = a.cr + (size_t)pair * a.census_pair + (size_t)y * W;
-        const int fr_off = dir == 0 ? -minD : -minD - (D - 1);
-        uint64_t* st_cl = stage + kl * LANES;  // [LPW][LANES] left census per step
+        const rsrc_t rcl = make_rsrc(a.cl + (size_t)pair * a.census_pair, (uint64_t)H * W * 8);
+        const rsrc_t rcr = make_rsrc(a.cr + (size_t)pair * a.census_pair, (uint64_t)H * W * 8);
+        const int fr_off = DIR == 0 ? -minD : -minD - (D - 1);
+        uint64_t* st_cl = stage + kl * LANES;       // [LPW][LANES] left census per step
         uint64_t* st_fr = stage + 64 + kl * LANES;  // [LPW][LANES] entering right census per step
-        uint64_t ccl, cfr;
-        auto load_chunk = [&](int c) {
-            const int X = Xof(min(c * LANES + g, W1 - 1));
-            ccl = clrow[X];
-            cfr = crrow[X + fr_off];
-        };
+        const int X0 = DIR == 0 ? minX1 : minX1 + W1 - 1;
+        auto chunk_off = [&](int c) { return (uint32_t)((y * W + X0 + SGN * min(c * LANES + g, W1 - 1)) * 8); };
+        // window for "step -1"; step 0's shift brings in its entering value
+        // (the one element that would sit outside the image is shifted out)
         uint64_t wnd[DPL];
-        {
-            const int X = Xof(0);
 #pragma unroll
-            for (int i = 0; i < DPL; i++) wnd[i] = crrow[X - minD - (g * DPL + i)];
-        }
-        load_chunk(0);
-        st_cl[g] = ccl;
-        st_fr[g] = cfr;
-        const int nchunks = (W1 + LANES - 1) / LANES;
-        if (nchunks > 1) load_chunk(1);
-        for (int s = 0; s < W1; s++) {
-            const int sl = s % LANES;
-            if (sl == 0 && s > 0) {
-                st_cl[g] = ccl;
-                st_fr[g] = cfr;
-                const int c = s / LANES + 1;
-                if (c < nchunks) load_chunk(c);
-            }
+        for (int i = 0; i < DPL; i++)
+            wnd[i] = bload_u64(rcr, (uint32_t)((y * W + X0 - SGN - minD - (g * DPL + i)) * 8));
+        uint64_t ccl = bload_u64(rcl, chunk_off(0));
+        uint64_t cfr = bload_u64(rcr, chunk_off(0) + fr_off * 8);
+        int off = off0;
+        for (int c = 0; c < nchunks; c++) {
+            st_cl[g] = ccl;
+            st_fr[g] = cfr;
+            const uint32_t nxt = chunk_off(min(c + 1, nchunks - 1));
+            ccl = bload_u64(rcl, nxt);
+            cfr = bload_u64(rcr, nxt + fr_off * 8);
             __builtin_amdgcn_wave_barrier();
-            const uint64_t clv = st_cl[sl];
-            const uint64_t frv = st_fr[sl];
-            if (s > 0) {
-                if (dir == 0) {
+            const int lim = W1 - c * LANES;  // steps of this chunk inside the row
+            for (int t = 0; t < LANES; t++) {
+                const uint64_t clv = st_cl[t];
+                const uint64_t frv = st_fr[t];
+                if constexpr (DIR == 0) {
                     const uint64_t in = Line<LANES>::prev(frv, wnd[DPL - 1]);
 #pragma unroll
                     for (int i = DPL - 1; i > 0; i--) wnd[i] = wnd[i - 1];
@@ -168,31 +131,46 @@ __device__ __forceinline__ void horz_family(const PathsArgs& a, int pair, int hb
                     for (int i = 0; i < DPL - 1; i++) wnd[i] = wnd[i + 1];
                     wnd[DPL - 1] = in;
                 }
+                uint32_t C[DPL], Ln[DPL];
+#pragma unroll
+                for (int i = 0; i < DPL; i++) C[i] = (uint32_t)__popcll(clv ^ wnd[i]);
+                const uint32_t mn = sgm_step<LANES, DPL>(Lp, minLp, C, P1, P2, Ln);
+                bstore_n<LT, DPL>(rout, (line_ok && t < lim) ? (uint32_t)off : kOOB, Ln);
+                off += step_bytes;
+#pragma unroll
+                for (int i = 0; i < DPL; i++) Lp[i] = Ln[i];
+                minLp = mn;
             }
-            uint32_t C[DPL], Ln[DPL];
-#pragma unroll
-            for (int i = 0; i < DPL; i++) C[i] = (uint32_t)__popcll(clv ^ wnd[i]);
-            const uint32_t mn = sgm_step<LANES, DPL>(Lp, minLp, C, P1, P2, Ln);
-            if (line_ok) store_n<DPL>(Lrow + (size_t)(Xof(s) - minX1) * D, Ln);
-#pragma unroll
-            for (int i = 0; i < DPL; i++) Lp[i] = Ln[i];
-            minLp = mn;
+            __builtin_amdgcn_wave_barrier();
         }
     } else {
-        const uint16_t* __restrict__ crow = a.cost + (size_t)pair * a.cost_pair + (size_t)y * W1 * D + g * DPL;
-        RawCost<DPL> nxt;
-        nxt.load(crow + (size_t)(Xof(0) - minX1) * D);
+        const rsrc_t rc = make_rsrc(a.cost + (size_t)pair * a.cost_pair, (uint64_t)H * W1 * D * 2);
+        const int coff0 = off0 / (int)sizeof(LT) * 2, cstep = step_bytes / (int)sizeof(LT) * 2;
+        RawU16<DPL> nxt;
+        nxt.load(rc, (uint32_t)coff0);
+        int off = off0, coff = coff0;
         for (int s = 0; s < W1; s++) {
             uint32_t C[DPL], Ln[DPL];
             nxt.unpack(C);
-            if (s + 1 < W1) nxt.load(crow + (size_t)(Xof(s + 1) - minX1) * D);
+            coff += cstep;
+            nxt.load(rc, s + 1 < W1 ? (uint32_t)coff : kOOB);
             const uint32_t mn = sgm_step<LANES, DPL>(Lp, minLp, C, P1, P2, Ln);
-            if (line_ok) store_n<DPL>(Lrow + (size_t)(Xof(s) - minX1) * D, Ln);
+            bstore_n<LT, DPL>(rout, line_ok ? (uint32_t)off : kOOB, Ln);
+            off += step_bytes;
 #pragma unroll
             for (int i = 0; i < DPL; i++) Lp[i] = Ln[i];
             minLp = mn;
         }
     }
+}
+
+template <int LANES, int DPL, bool CENSUS, typename LT>
+__device__ __forceinline__ void horz_family(const PathsArgs& a, int pair, int hb, uint64_t* stage)
+{
+    if (hb < a.hblocks)
+        horz_impl<0, LANES, DPL, CENSUS, LT>(a, pair, hb, stage);
+    else
+        horz_impl<1, LANES, DPL, CENSUS, LT>(a, pair, hb, stage);
 }
 
 // --------------------------------------------------------- vertical family
@@ -224,7 +202,14 @@ __device__ __forceinline__ void vert_family(const PathsArgs& a, int pair, int vb
         s_lo = max(0, b0 - W1 + 1);
         s_hi = min(H, b0 + 4);
     }
-    LT* __restrict__ Lv = (LT*)(a.L + (size_t)pair * a.L_pair_bytes + (size_t)a.v_slot[k] * a.slot_bytes) + g * DPL;
+    const int ysgn = dy > 0 ? 1 : -1;
+    const int y_lo = dy > 0 ? s_lo : H - 1 - s_lo;
+    const rsrc_t rout = make_rsrc(a.L + (size_t)pair * a.L_pair_bytes + (size_t)a.v_slot[k] * a.slot_bytes,
+                                  (uint64_t)H * W1 * D * sizeof(LT));
+    // this lane's output slice at step s: (y_lo + ysgn*(s-s_lo), x1 = b0 + kl + dx*s)
+    int x1 = b0 + kl + dx * s_lo;
+    int64_t off = ((int64_t)y_lo * W1 + x1) * D * sizeof(LT) + (int64_t)g * DPL * sizeof(LT);
+    const int64_t step_bytes = ((int64_t)ysgn * W1 + dx) * D * (int)sizeof(LT);
 
     uint32_t Lp[DPL];
 #pragma unroll
@@ -232,63 +217,63 @@ __device__ __forceinline__ void vert_family(const PathsArgs& a, int pair, int vb
     uint32_t minLp = 0;
 
     if constexpr (CENSUS) {
-        const uint64_t* __restrict__ clp = a.cl + (size_t)pair * a.census_pair;
-        const uint64_t* __restrict__ crp = a.cr + (size_t)pair * a.census_pair;
+        const rsrc_t rcl = make_rsrc(a.cl + (size_t)pair * a.census_pair, (uint64_t)H * W * 8);
+        const rsrc_t rcr = make_rsrc(a.cr + (size_t)pair * a.census_pair, (uint64_t)H * W * 8);
+        // window entry j at step s = right census (y, X0 - minD - D + 1 + j), X0 = minX1 + b0 + dx*s.
+        // Offsets outside the image belong to inactive lines only (range check returns 0).
+        int64_t woff = ((int64_t)y_lo * W + (minX1 + b0 + dx * s_lo) - minD - D + 1 + lane) * 8;
+        int64_t coff = ((int64_t)y_lo * W + (minX1 + b0 + dx * s_lo) + kl) * 8;
+        const int64_t wstep = ((int64_t)ysgn * W + dx) * 8;
         uint64_t pw[NW];
         uint64_t pcl;
-        auto fetch = [&](int s) {
-            const int y = dy > 0 ? s : H - 1 - s;
-            const int X0 = minX1 + b0 + dx * s;
-            const uint64_t* row = crp + (size_t)y * W;
-            const int base = X0 - minD - D + 1;
+        auto fetch = [&]() {
 #pragma unroll
-            for (int j = 0; j < NW; j++) pw[j] = row[min(max(base + lane + 64 * j, 0), W - 1)];
-            pcl = clp[(size_t)y * W + min(max(X0 + kl, 0), W - 1)];
+            for (int j = 0; j < NW; j++) pw[j] = bload_u64(rcr, (uint32_t)(woff + 512 * j));
+            pcl = bload_u64(rcl, (uint32_t)coff);
         };
-        fetch(s_lo);
+        fetch();
         for (int s = s_lo; s < s_hi; s++) {
 #pragma unroll
             for (int j = 0; j < NW; j++)
                 if (j < NW - 1 || lane + 64 * j < D + 3) win[lane + 64 * j] = pw[j];
             const uint64_t clv = pcl;
             __builtin_amdgcn_wave_barrier();
-            if (s + 1 < s_hi) fetch(s + 1);
+            woff += wstep;
+            coff += wstep;
+            fetch();  // next step (one redundant fetch after the last step)
             uint32_t C[DPL], Ln[DPL];
             const int e0 = kl + D - 1 - g * DPL;
 #pragma unroll
             for (int i = 0; i < DPL; i++) C[i] = (uint32_t)__popcll(clv ^ win[e0 - i]);
             const uint32_t mn = sgm_step<16, DPL>(Lp, minLp, C, P1, P2, Ln);
-            const int x1 = b0 + kl + dx * s;
-            if (line_ok && x1 >= 0 && x1 < W1) {
-                const int y = dy > 0 ? s : H - 1 - s;
-                store_n<DPL>(Lv + ((size_t)y * W1 + x1) * D, Ln);
+            const bool active = line_ok && x1 >= 0 && x1 < W1;
+            bstore_n<LT, DPL>(rout, active ? (uint32_t)off : kOOB, Ln);
 #pragma unroll
-                for (int i = 0; i < DPL; i++) Lp[i] = Ln[i];
-                minLp = mn;
-            }
+            for (int i = 0; i < DPL; i++) Lp[i] = active ? Ln[i] : Lp[i];
+            minLp = active ? mn : minLp;
+            off += step_bytes;
+            x1 += dx;
+            __builtin_amdgcn_wave_barrier();
         }
     } else {
-        const uint16_t* __restrict__ cp = a.cost + (size_t)pair * a.cost_pair + g * DPL;
-        RawCost<DPL> nxt;
-        auto fetch = [&](int s) {
-            const int y = dy > 0 ? s : H - 1 - s;
-            const int x1 = min(max(b0 + kl + dx * s, 0), W1 - 1);
-            nxt.load(cp + ((size_t)y * W1 + x1) * D);
-        };
-        fetch(s_lo);
+        const rsrc_t rc = make_rsrc(a.cost + (size_t)pair * a.cost_pair, (uint64_t)H * W1 * D * 2);
+        int64_t coff = (off / (int64_t)sizeof(LT)) * 2;
+        const int64_t cstep = step_bytes / (int64_t)sizeof(LT) * 2;
+        RawU16<DPL> nxt;
+        nxt.load(rc, (x1 >= 0 && x1 < W1) ? (uint32_t)coff : kOOB);
         for (int s = s_lo; s < s_hi; s++) {
             uint32_t C[DPL], Ln[DPL];
             nxt.unpack(C);
-            if (s + 1 < s_hi) fetch(s + 1);
+            coff += cstep;
+            nxt.load(rc, (x1 + dx >= 0 && x1 + dx < W1) ? (uint32_t)coff : kOOB);
             const uint32_t mn = sgm_step<16, DPL>(Lp, minLp, C, P1, P2, Ln);
-            const int x1 = b0 + kl + dx * s;
-            if (line_ok && x1 >= 0 && x1 < W1) {
-                const int y = dy > 0 ? s : H - 1 - s;
-                store_n<DPL>(Lv + ((size_t)y * W1 + x1) * D, Ln);
+            const bool active = line_ok && x1 >= 0 && x1 < W1;
+            bstore_n<LT, DPL>(rout, active ? (uint32_t)off : kOOB, Ln);
 #pragma unroll
-                for (int i = 0; i < DPL; i++) Lp[i] = Ln[i];
-                minLp = mn;
-            }
+            for (int i = 0; i < DPL; i++) Lp[i] = active ? Ln[i] : Lp[i];
+            minLp = active ? mn : minLp;
+            off += step_bytes;
+            x1 += dx;
         }
     }
 }
