@@ -116,6 +116,12 @@ int sm_reset_timing(sm_ctx* ctx);
  * Returns the byte size when host == NULL. */
 long long sm_debug_fetch(sm_ctx* ctx, int what, void* host, size_t bytes);
 
+/* Timing ablations ONLY (results become wrong): bit 0 skips the horizontal
+ * path family, bit 1 the vertical/diagonal family, bit 2 drops every path
+ * store; bit 3 (valid results) selects 16-lane instead of 8-lane vertical
+ * lines at D = 128.  0 = normal operation. */
+int sm_set_debug_flags(sm_ctx* ctx, int flags);
+
 /* Last error text of ctx (or of the calling thread when ctx == NULL). */
 const char* sm_last_error(sm_ctx* ctx);
 

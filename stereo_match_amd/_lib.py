@@ -53,6 +53,7 @@ _SIGS = {
     "sm_get_timing": (_c.c_int, [_c.c_void_p, _c.c_int, _c.POINTER(_c.c_double), _c.POINTER(_c.c_longlong),
                                  _c.POINTER(_c.c_longlong)]),
     "sm_reset_timing": (_c.c_int, [_c.c_void_p]),
+    "sm_set_debug_flags": (_c.c_int, [_c.c_void_p, _c.c_int]),
     "sm_debug_fetch": (_c.c_longlong, [_c.c_void_p, _c.c_int, _c.c_void_p, _c.c_size_t]),
     "sm_last_error": (_c.c_char_p, [_c.c_void_p]),
 }
@@ -185,6 +186,10 @@ class Engine:
         return out
 
     # -- debug ------------------------------------------------------------------
+    def set_debug_flags(self, flags: int):
+        """Timing ablations only (results become wrong); 0 = normal."""
+        self._check(self._lib.sm_set_debug_flags(self.ctx, int(flags)))
+
     def debug_fetch(self, what: int) -> bytes:
         n = self._lib.sm_debug_fetch(self.ctx, what, None, 0)
         if n < 0:

@@ -51,6 +51,7 @@ struct sm_ctx {
     int last_minX1 = 0, last_index = 0;
     size_t last_L_pair = 0;
     bool timing = false;
+    int dbg_flags = 0;
     std::vector<TimedEvent> pending;
     std::vector<hipEvent_t> free_events;
     double stage_ms[SM_NUM_STAGES] = {0};
@@ -197,10 +198,15 @@ const int kVdy[6] = {1, 1, 1, -1, -1, -1};
 constexpr size_t kGroupBudget = size_t(24) << 30;  // bytes of path volumes per launch group
 constexpr int kMaxGroup = 16;
 
-template <int DPLV, bool CENSUS>
+template <int DPLV, bool CENSUS, int VL = 16>
 int launch_paths_wta(sm_ctx* ctx, const Norm& n, int H, int W, int G, size_t L_pair, size_t slot_bytes,
                      size_t census_pair, size_t cost_pair)
 {
+    // 8-lane vertical lines for D = 128 (ablation flag 8 selects 16-lane lines)
+    if constexpr (VL == 16 && DPLV == 8) {
+        if (!(ctx->dbg_flags & 8))
+            return launch_paths_wta<DPLV, CENSUS, 8>(ctx, n, H, W, G, L_pair, slot_bytes, census_pair, cost_pair);
+    }
     using LT = typename std::conditional<CENSUS, uint8_t, uint16_t>::type;
     constexpr int D = 16 * DPLV;
     constexpr bool WIDE = D % 64 == 0;
@@ -223,6 +229,7 @@ int launch_paths_wta(sm_ctx* ctx, const Norm& n, int H, int W, int G, size_t L_p
     pa.minX1 = n.minX1;
     pa.P1 = n.P1;
     pa.P2 = n.P2;
+    pa.dbg = ctx->dbg_flags;
     const int lines_per_wg = 4 * (64 / LANESH);
     pa.hblocks = (H + lines_per_wg - 1) / lines_per_wg;
     pa.nv = n.ndirs - 2;
@@ -234,12 +241,14 @@ int launch_paths_wta(sm_ctx* ctx, const Norm& n, int H, int W, int G, size_t L_p
         pa.v_line_lo[k] = kVdx[k] > 0 ? -(H - 1) : 0;
         pa.v_nlines[k] = kVdx[k] == 0 ? n.width1 : n.width1 + H - 1;
         pa.v_blk_start[k] = blocks;
-        blocks += (pa.v_nlines[k] + 15) / 16;
+        // waves come in groups of 8 covering 8*LPW lines (lines w + 8*kl)
+        constexpr int LPWV = 64 / VL;
+        blocks += ((pa.v_nlines[k] + 8 * LPWV - 1) / (8 * LPWV)) * 2;
     }
     for (int k = pa.nv; k <= 6; k++) pa.v_blk_start[k] = blocks;
     {
         StageTimer t(ctx, SM_STAGE_PATHS, G);
-        hipLaunchKernelGGL((smk::k_sgm_paths<DPLV, LANESH, DPLH, CENSUS, LT>), dim3(2 * pa.hblocks + blocks, G),
+        hipLaunchKernelGGL((smk::k_sgm_paths<VL, DPLV * 16 / VL, LANESH, DPLH, CENSUS, LT>), dim3(2 * pa.hblocks + blocks, G),
                            dim3(256), 0, ctx->stream, pa);
         HIP_TRY(ctx, hipGetLastError());
     }
@@ -543,6 +552,13 @@ int sm_set_timing(sm_ctx* ctx, int enable)
 {
     if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
     ctx->timing = enable != 0;
+    return SM_OK;
+}
+
+int sm_set_debug_flags(sm_ctx* ctx, int flags)
+{
+    if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
+    ctx->dbg_flags = flags;
     return SM_OK;
 }
 

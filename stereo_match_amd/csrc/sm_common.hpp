@@ -96,6 +96,28 @@ struct Line<64> {
     static __device__ __forceinline__ uint32_t min(uint32_t v);
 };
 
+// 8-lane lines (two per DPP row): row shifts plus a fix-up at the half-row edge
+template <>
+struct Line<8> {
+    template <typename T>
+    static __device__ __forceinline__ T prev(T edge, T v)
+    {
+        T r;
+        if constexpr (sizeof(T) == 8) r = dpp64<DPP_ROW_SHR1>(edge, v);
+        else r = dpp<DPP_ROW_SHR1>(edge, v);
+        return (threadIdx.x & 7) == 0 ? edge : r;
+    }
+    template <typename T>
+    static __device__ __forceinline__ T next(T edge, T v)
+    {
+        T r;
+        if constexpr (sizeof(T) == 8) r = dpp64<DPP_ROW_SHL1>(edge, v);
+        else r = dpp<DPP_ROW_SHL1>(edge, v);
+        return (threadIdx.x & 7) == 7 ? edge : r;
+    }
+    static __device__ __forceinline__ uint32_t min(uint32_t v);
+};
+
 __device__ __forceinline__ uint32_t row16_or(uint32_t v)
 {
     v |= perm_dpp<DPP_QP_XOR1>(v);
@@ -106,6 +128,14 @@ __device__ __forceinline__ uint32_t row16_or(uint32_t v)
 }
 
 __device__ __forceinline__ uint32_t Line<16>::min(uint32_t v) { return row16_min(v); }
+
+__device__ __forceinline__ uint32_t Line<8>::min(uint32_t v)
+{
+    v = ::min(v, perm_dpp<DPP_QP_XOR1>(v));
+    v = ::min(v, perm_dpp<DPP_QP_XOR2>(v));
+    v = ::min(v, perm_dpp<DPP_ROW_HALF_MIRROR>(v));
+    return v;
+}
 
 // whole-wave minimum, returned wave-uniform (SGPR)
 __device__ __forceinline__ uint32_t Line<64>::min(uint32_t v)

@@ -37,6 +37,7 @@ struct PathsArgs {
     size_t slot_bytes, L_pair_bytes;
     int H, W, width1, D, minD, minX1, P1, P2;
     int hblocks;  // workgroups per horizontal direction (slots 0 = E, 1 = W)
+    int dbg;      // timing ablations only: 1 skip horizontal, 2 skip vertical, 4 drop stores
     int nv;       // vertical-family directions in this launch
     int v_dx[6], v_dy[6], v_slot[6], v_blk_start[7], v_line_lo[6], v_nlines[6];
 };
@@ -80,7 +81,7 @@ __device__ __forceinline__ void horz_impl(const PathsArgs& a, int pair, int hb, 
     const int y = min(wline + kl, H - 1);
     const uint32_t P1 = (uint32_t)a.P1, P2 = (uint32_t)a.P2;
     const rsrc_t rout = make_rsrc(a.L + (size_t)pair * a.L_pair_bytes + (size_t)DIR * a.slot_bytes,
-                                  (uint64_t)H * W1 * D * sizeof(LT));
+                                  (a.dbg & 4) ? 0 : (uint64_t)H * W1 * D * sizeof(LT));
     // byte offset of this lane's slice at step s: row y, x1 = DIR ? W1-1-s : s
     constexpr int SGN = DIR == 0 ? 1 : -1;
     const int step_bytes = SGN * D * (int)sizeof(LT);
@@ -174,129 +175,179 @@ __device__ __forceinline__ void horz_family(const PathsArgs& a, int pair, int hb
 }
 
 // --------------------------------------------------------- vertical family
-template <int DPL, bool CENSUS, typename LT>
+// A wave owns LPW = 64/VL lines b0 + 8*kl (lines of VL lanes, VL = 16 or 8):
+// all on one image row per step, 8 columns apart.  The right-census window
+// (D + 8*(LPW-1) values) is staged per step
+// in wave-private LDS in class-major order, phys(e) = (e & 7)*S + (e >> 3)
+// with S = 2 (mod 16): the coalesced window writes hit 16 distinct bank
+// pairs per 16 lanes, and every per-element read is 16 consecutive slots per
+// line with the 4 lines mostly reading the SAME slots (broadcast), so both
+// are conflict-free and each read is a ds_read_b64 with an immediate offset.
+template <int D, int LPW>
+struct VWin {
+    static constexpr int ENTRIES = D + 8 * (LPW - 1);
+    static constexpr int S0 = (ENTRIES + 7) / 8;
+    static constexpr int S = S0 + ((2 - S0 % 16) + 16) % 16;  // smallest S >= S0 with S % 16 == 2
+    static constexpr int WORDS = 8 * S;                       // u64 per wave
+    static constexpr int NW = (ENTRIES + 63) / 64;            // window values loaded per lane
+    static __device__ __forceinline__ int phys(int e) { return (e & 7) * S + (e >> 3); }
+};
+
+template <int VL, int DPL, bool CENSUS, typename LT>
 __device__ __forceinline__ void vert_family(const PathsArgs& a, int pair, int vb, uint64_t* win)
 {
-    constexpr int NW = (16 * DPL + 3 + 63) / 64;  // window entries per lane
+    constexpr int LPW = 64 / VL;
+    using VW = VWin<VL * DPL, LPW>;
     int k = 0;
 #pragma unroll
     for (int i = 1; i < 6; i++)
         if (i < a.nv && vb >= a.v_blk_start[i]) k = i;
     const int dx = a.v_dx[k], dy = a.v_dy[k];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int g = lane & 15, kl = lane >> 4;
-    const int wline = ((vb - a.v_blk_start[k]) * 4 + wave) * 4;
-    if (wline >= a.v_nlines[k]) return;  // wave-uniform
-    const bool line_ok = wline + kl < a.v_nlines[k];
+    const int g = lane % VL, kl = lane / VL;
+    // line numbering: 8 waves cover 8*LPW lines; wave w of the group owns lines w + 8*kl
+    const int wv = (vb - a.v_blk_start[k]) * 4 + wave;
+    const int wline = (wv >> 3) * (8 * LPW) + (wv & 7);  // relative line index of kl = 0
+    if (wline >= a.v_nlines[k]) return;          // wave-uniform
+    const bool line_ok = wline + 8 * kl < a.v_nlines[k];
     const int b0 = a.v_line_lo[k] + wline;  // x1 of line 0 at step 0 (unwrapped)
     const int H = a.H, W = a.W, W1 = a.width1, D = a.D, minD = a.minD, minX1 = a.minX1;
     const uint32_t P1 = (uint32_t)a.P1, P2 = (uint32_t)a.P2;
-    int s_lo, s_hi;
+    int s_lo, s_hi;  // steps where at least one of the wave's lines is inside [0, W1)
     if (dx == 0) {
         s_lo = 0;
         s_hi = H;
     } else if (dx > 0) {
-        s_lo = max(0, -(b0 + 3));
+        s_lo = max(0, -(b0 + 8 * (LPW - 1)));
         s_hi = min(H, W1 - b0);
     } else {
         s_lo = max(0, b0 - W1 + 1);
-        s_hi = min(H, b0 + 4);
+        s_hi = min(H, b0 + 8 * (LPW - 1) + 1);
     }
     const int ysgn = dy > 0 ? 1 : -1;
     const int y_lo = dy > 0 ? s_lo : H - 1 - s_lo;
     const rsrc_t rout = make_rsrc(a.L + (size_t)pair * a.L_pair_bytes + (size_t)a.v_slot[k] * a.slot_bytes,
-                                  (uint64_t)H * W1 * D * sizeof(LT));
-    // this lane's output slice at step s: (y_lo + ysgn*(s-s_lo), x1 = b0 + kl + dx*s)
-    int x1 = b0 + kl + dx * s_lo;
-    int64_t off = ((int64_t)y_lo * W1 + x1) * D * sizeof(LT) + (int64_t)g * DPL * sizeof(LT);
-    const int64_t step_bytes = ((int64_t)ysgn * W1 + dx) * D * (int)sizeof(LT);
+                                  (a.dbg & 4) ? 0 : (uint64_t)H * W1 * D * sizeof(LT));
+    // this lane's output slice at step s: (y_lo + ysgn*(s-s_lo), x1 = b0 + 8kl + dx*s)
+    int x1 = b0 + 8 * kl + dx * s_lo;
+    int off = (y_lo * W1 + x1) * D * (int)sizeof(LT) + g * DPL * (int)sizeof(LT);
+    const int step_bytes = (ysgn * W1 + dx) * D * (int)sizeof(LT);
+    // a line enters the domain one step after x1 == enter_x; its state must be 0 then
+    const int enter_x = dx > 0 ? -1 : W1;
 
     uint32_t Lp[DPL];
 #pragma unroll
     for (int i = 0; i < DPL; i++) Lp[i] = 0;
     uint32_t minLp = 0;
 
+    auto reset_entering = [&]() {
+        if (dx != 0) {
+            const bool ent = x1 == enter_x;
+            if (__builtin_amdgcn_ballot_w64(ent)) {  // wave-uniform, at most 4 times per wave
+#pragma unroll
+                for (int i = 0; i < DPL; i++) Lp[i] = ent ? 0u : Lp[i];
+                minLp = ent ? 0u : minLp;
+            }
+        }
+    };
+
     if constexpr (CENSUS) {
         const rsrc_t rcl = make_rsrc(a.cl + (size_t)pair * a.census_pair, (uint64_t)H * W * 8);
         const rsrc_t rcr = make_rsrc(a.cr + (size_t)pair * a.census_pair, (uint64_t)H * W * 8);
-        // window entry j at step s = right census (y, X0 - minD - D + 1 + j), X0 = minX1 + b0 + dx*s.
-        // Offsets outside the image belong to inactive lines only (range check returns 0).
-        int64_t woff = ((int64_t)y_lo * W + (minX1 + b0 + dx * s_lo) - minD - D + 1 + lane) * 8;
-        int64_t coff = ((int64_t)y_lo * W + (minX1 + b0 + dx * s_lo) + kl) * 8;
-        const int64_t wstep = ((int64_t)ysgn * W + dx) * 8;
-        uint64_t pw[NW];
+        // window entry e at step s = right census (y, X0 - minD - D + 1 + e), X0 = minX1 + b0 + dx*s;
+        // entries outside the image are read only by inactive lines (range check returns 0).
+        int woff = (y_lo * W + (minX1 + b0 + dx * s_lo) - minD - D + 1 + lane) * 8;
+        int coff = (y_lo * W + (minX1 + b0 + dx * s_lo) + 8 * kl) * 8;
+        const int wstep = (ysgn * W + dx) * 8;
+        int wdst[VW::NW];
+#pragma unroll
+        for (int j = 0; j < VW::NW; j++) wdst[j] = VW::phys(lane + 64 * j);
+        // line kl, element i reads e = D-1 + 8kl - g*DPL - i
+        const int ebase = D - 1 + 8 * kl - g * DPL;
+        uint64_t pw[VW::NW];
         uint64_t pcl;
         auto fetch = [&]() {
 #pragma unroll
-            for (int j = 0; j < NW; j++) pw[j] = bload_u64(rcr, (uint32_t)(woff + 512 * j));
+            for (int j = 0; j < VW::NW; j++) pw[j] = bload_u64(rcr, (uint32_t)(woff + 512 * j));
             pcl = bload_u64(rcl, (uint32_t)coff);
         };
         fetch();
         for (int s = s_lo; s < s_hi; s++) {
 #pragma unroll
-            for (int j = 0; j < NW; j++)
-                if (j < NW - 1 || lane + 64 * j < D + 3) win[lane + 64 * j] = pw[j];
+            for (int j = 0; j < VW::NW; j++)
+                if (j < VW::NW - 1 || lane + 64 * j < VW::ENTRIES) win[wdst[j]] = pw[j];
             const uint64_t clv = pcl;
             __builtin_amdgcn_wave_barrier();
             woff += wstep;
             coff += wstep;
             fetch();  // next step (one redundant fetch after the last step)
             uint32_t C[DPL], Ln[DPL];
-            const int e0 = kl + D - 1 - g * DPL;
+            if constexpr (DPL % 8 == 0) {
+                // ebase = 7 (mod 8): phys(ebase - i) = (7 - i%8)*S + ebase/8 - i/8 -> immediate offsets
+                const uint64_t* wl = win + (ebase >> 3);
 #pragma unroll
-            for (int i = 0; i < DPL; i++) C[i] = (uint32_t)__popcll(clv ^ win[e0 - i]);
-            const uint32_t mn = sgm_step<16, DPL>(Lp, minLp, C, P1, P2, Ln);
+                for (int i = 0; i < DPL; i++)
+                    C[i] = (uint32_t)__popcll(clv ^ wl[(7 - (i & 7)) * VW::S - (i >> 3)]);
+            } else {
+#pragma unroll
+                for (int i = 0; i < DPL; i++) C[i] = (uint32_t)__popcll(clv ^ win[VW::phys(ebase - i)]);
+            }
+            const uint32_t mn = sgm_step<VL, DPL>(Lp, minLp, C, P1, P2, Ln);
             const bool active = line_ok && x1 >= 0 && x1 < W1;
             bstore_n<LT, DPL>(rout, active ? (uint32_t)off : kOOB, Ln);
 #pragma unroll
-            for (int i = 0; i < DPL; i++) Lp[i] = active ? Ln[i] : Lp[i];
-            minLp = active ? mn : minLp;
+            for (int i = 0; i < DPL; i++) Lp[i] = Ln[i];
+            minLp = mn;
+            reset_entering();
             off += step_bytes;
             x1 += dx;
             __builtin_amdgcn_wave_barrier();
         }
     } else {
         const rsrc_t rc = make_rsrc(a.cost + (size_t)pair * a.cost_pair, (uint64_t)H * W1 * D * 2);
-        int64_t coff = (off / (int64_t)sizeof(LT)) * 2;
-        const int64_t cstep = step_bytes / (int64_t)sizeof(LT) * 2;
+        int coff = off / (int)sizeof(LT) * 2;
+        const int cstep = step_bytes / (int)sizeof(LT) * 2;
         RawU16<DPL> nxt;
-        nxt.load(rc, (x1 >= 0 && x1 < W1) ? (uint32_t)coff : kOOB);
+        nxt.load(rc, (uint32_t)coff);
         for (int s = s_lo; s < s_hi; s++) {
             uint32_t C[DPL], Ln[DPL];
             nxt.unpack(C);
             coff += cstep;
-            nxt.load(rc, (x1 + dx >= 0 && x1 + dx < W1) ? (uint32_t)coff : kOOB);
-            const uint32_t mn = sgm_step<16, DPL>(Lp, minLp, C, P1, P2, Ln);
+            nxt.load(rc, (uint32_t)coff);  // out-of-range offsets read 0 (inactive lines only)
+            const uint32_t mn = sgm_step<VL, DPL>(Lp, minLp, C, P1, P2, Ln);
             const bool active = line_ok && x1 >= 0 && x1 < W1;
             bstore_n<LT, DPL>(rout, active ? (uint32_t)off : kOOB, Ln);
 #pragma unroll
-            for (int i = 0; i < DPL; i++) Lp[i] = active ? Ln[i] : Lp[i];
-            minLp = active ? mn : minLp;
+            for (int i = 0; i < DPL; i++) Lp[i] = Ln[i];
+            minLp = mn;
+            reset_entering();
             off += step_bytes;
             x1 += dx;
         }
     }
 }
 
-// LDS per wave: vertical window (D+3 u64) or horizontal staging (2 x 64 u64)
-template <int DPLV>
+// LDS per wave: vertical window (class-major, VWin::WORDS u64) or horizontal staging (2 x 64 u64)
+template <int D, int LPW>
 constexpr int lds_per_wave()
 {
-    return (16 * DPLV + 3) > 128 ? (16 * DPLV + 3 + 1) & ~1 : 128;
+    return VWin<D, LPW>::WORDS > 128 ? VWin<D, LPW>::WORDS : 128;
 }
 
-template <int DPLV, int LANESH, int DPLH, bool CENSUS, typename LT>
+// VL: lanes per vertical-family line (16 or 8); DPLV = D / VL
+template <int VL, int DPLV, int LANESH, int DPLH, bool CENSUS, typename LT>
 __global__ void __launch_bounds__(256) k_sgm_paths(PathsArgs a)
 {
-    constexpr int PW = lds_per_wave<DPLV>();
+    constexpr int PW = lds_per_wave<VL * DPLV, 64 / VL>();
     __shared__ __attribute__((aligned(16))) uint64_t lds[4 * PW];
     uint64_t* mine = lds + (threadIdx.x >> 6) * PW;
     const int pair = blockIdx.y;
     const int b = blockIdx.x;
-    if (b < 2 * a.hblocks)
-        horz_family<LANESH, DPLH, CENSUS, LT>(a, pair, b, mine);
-    else
-        vert_family<DPLV, CENSUS, LT>(a, pair, b - 2 * a.hblocks, mine);
+    if (b < 2 * a.hblocks) {
+        if (!(a.dbg & 1)) horz_family<LANESH, DPLH, CENSUS, LT>(a, pair, b, mine);
+    } else {
+        if (!(a.dbg & 2)) vert_family<VL, DPLV, CENSUS, LT>(a, pair, b - 2 * a.hblocks, mine);
+    }
 }
 
 // --------------------------------------------------------------------- WTA
