@@ -125,6 +125,7 @@ int normalize(sm_ctx* ctx, const sm_params* p, int H, int W, Norm& n)
     if (n.speckle_ws > 0)
         return fail(ctx, SM_E_UNSUPPORTED, "speckleWindowSize > 0 not implemented on the GPU path yet");
     if (n.cost == SM_COST_SGBM) {
+        if (n.bs > 2 * 5 + 1) return fail(ctx, SM_E_UNSUPPORTED, "blockSize %d > 11 not built", n.bs);
         const int maxpix = 2 * n.ftzero + (255 >> 2);
         if ((long long)n.bs * n.bs * maxpix + n.P2 > 16383)
             return fail(ctx, SM_E_UNSUPPORTED,
@@ -350,7 +351,6 @@ int run_group(sm_ctx* ctx, const uint8_t* dL, const uint8_t* dR, size_t pair_str
             HIP_TRY(ctx, hipGetLastError());
         } else {
             if ((rc = ensure(ctx, ctx->planes, (size_t)H * W * 12)) != SM_OK) return rc;
-            if ((rc = ensure(ctx, ctx->hsum, vol * 2)) != SM_OK) return rc;
             if ((rc = ensure(ctx, ctx->cost, (size_t)G * vol * 2)) != SM_OK) return rc;
             for (int i = 0; i < G; i++) {
                 smk::PrefilterArgs pf{};
@@ -363,27 +363,28 @@ int run_group(sm_ctx* ctx, const uint8_t* dL, const uint8_t* dR, size_t pair_str
                 pf.ftzero = n.ftzero;
                 hipLaunchKernelGGL(smk::k_sgbm_prefilter, dim3((W + 255) / 256, H, 2), dim3(256), 0, ctx->stream, pf);
                 HIP_TRY(ctx, hipGetLastError());
-                smk::HsumArgs hs{};
-                hs.planes = pf.planes;
-                hs.hsum = (uint16_t*)ctx->hsum.p;
-                hs.H = H;
-                hs.W = W;
-                hs.width1 = n.width1;
-                hs.D = n.D;
-                hs.minD = n.minD;
-                hs.minX1 = n.minX1;
-                hs.SW2 = n.bs / 2;
-                hipLaunchKernelGGL(smk::k_sgbm_hsum, dim3(grid_for(vol)), dim3(256), 0, ctx->stream, hs);
+                smk::SgbmCostArgs sc{};
+                sc.planes = pf.planes;
+                sc.C = (uint16_t*)ctx->cost.p + (size_t)i * vol;
+                sc.H = H;
+                sc.W = W;
+                sc.width1 = n.width1;
+                sc.D = n.D;
+                sc.minD = n.minD;
+                sc.minX1 = n.minX1;
+                sc.SW2 = n.bs / 2;
+                sc.SH2 = n.bs / 2;
+                sc.Yc = std::max(1, H - n.bs / 2);
+                hipLaunchKernelGGL(smk::k_sgbm_cost,
+                                   dim3((n.width1 + smk::SC_TX - 1) / smk::SC_TX, (sc.Yc + smk::SC_TY - 1) / smk::SC_TY,
+                                        n.D / 8),
+                                   dim3(256), 0, ctx->stream, sc);
                 HIP_TRY(ctx, hipGetLastError());
-                smk::VsumArgs vs{};
-                vs.hsum = hs.hsum;
-                vs.C = (uint16_t*)ctx->cost.p + (size_t)i * vol;
-                vs.H = H;
-                vs.width1 = n.width1;
-                vs.D = n.D;
-                vs.SH2 = n.bs / 2;
-                vs.hh = n.mode == SM_MODE_HH;
-                hipLaunchKernelGGL(smk::k_sgbm_vsum, dim3(grid_for(vol)), dim3(256), 0, ctx->stream, vs);
+                if (sc.Yc < H) {
+                    const size_t row = (size_t)n.width1 * n.D;
+                    hipLaunchKernelGGL(smk::k_sgbm_cost_tail, dim3(grid_for((size_t)(H - sc.Yc) * row / 8)), dim3(256), 0,
+                                       ctx->stream, sc.C, H, sc.Yc, row, (int)(n.mode == SM_MODE_HH));
+                }
                 HIP_TRY(ctx, hipGetLastError());
             }
         }

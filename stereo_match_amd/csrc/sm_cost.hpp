@@ -143,55 +143,122 @@ __device__ __forceinline__ int bt_pix(const uint8_t* planes, size_t plane, int W
     return acc;
 }
 
-// hsum[y][x1][d] = sum_{j=-SW2..SW2} pix(y, clamp(x1+j, 0, width1-1), d)
-struct HsumArgs {
+// C_true[y][x1][d] for the rows OpenCV's incremental box filter actually
+// updates (y < Yc = max(1, H - SH2)):
+//   sum_{k=y-SH2..y+SH2} sum_{j=-SW2..SW2} pix(clamp(k,0,H-1), clamp(x1+j,0,width1-1), d)
+// Tile of SC_TY rows x SC_TX columns x 8 disparities per workgroup: BT pixel
+// costs of the halo tile -> LDS, horizontal then vertical sums in LDS.
+constexpr int SC_TX = 64, SC_TY = 8, SC_MAXR = 5;  // blockSize <= 11
+
+struct SgbmCostArgs {
     const uint8_t* planes;
-    uint16_t* hsum;
-    int H, W, width1, D, minD, minX1, SW2;
+    uint16_t* C;
+    int H, W, width1, D, minD, minX1, SW2, SH2, Yc;
 };
 
-__global__ void __launch_bounds__(256) k_sgbm_hsum(HsumArgs a)
+__device__ __forceinline__ int bt_cost2(uint2 L, uint2 R)
 {
-    const size_t plane = (size_t)a.H * a.W;
-    const size_t n = (size_t)a.H * a.width1 * a.D;
-    for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
-        int d = (int)(i % a.D);
-        size_t pix = i / a.D;
-        int x1 = (int)(pix % a.width1), y = (int)(pix / a.width1);
-        int acc = 0;
-        for (int j = -a.SW2; j <= a.SW2; j++) {
-            int X = min(max(x1 + j, 0), a.width1 - 1) + a.minX1;
-            acc += bt_pix(a.planes, plane, a.W, y, X, X - a.minD - d);
+    // bytes: [g, g_min, g_max, raw, raw_min, raw_max, -, -] of left (u) / right (v)
+    int acc = 0;
+#pragma unroll
+    for (int ch = 0; ch < 2; ch++) {
+        const uint32_t lw = ch == 0 ? L.x : (L.x >> 24) | (L.y << 8);
+        const uint32_t rw = ch == 0 ? R.x : (R.x >> 24) | (R.y << 8);
+        const int u = lw & 0xFF, u0 = (lw >> 8) & 0xFF, u1 = (lw >> 16) & 0xFF;
+        const int v = rw & 0xFF, v0 = (rw >> 8) & 0xFF, v1 = (rw >> 16) & 0xFF;
+        const int c0 = max(max(0, u - v1), v0 - u);
+        const int c1 = max(max(0, v - u1), u0 - v);
+        acc += min(c0, c1) >> (ch == 0 ? 0 : 2);
+    }
+    return acc;
+}
+
+__global__ void __launch_bounds__(256) k_sgbm_cost(SgbmCostArgs a)
+{
+    constexpr int HR = SC_TY + 2 * SC_MAXR, HC = SC_TX + 2 * SC_MAXR;
+    __shared__ __attribute__((aligned(16))) uint2 lpl[HR][HC];      // left planes of the halo tile
+    __shared__ __attribute__((aligned(16))) uint2 rpl[HR][HC + 8];  // right planes, shifted by the disparities
+    __shared__ __attribute__((aligned(16))) uint8_t pix[HR][HC][8];
+    __shared__ __attribute__((aligned(16))) uint16_t hs[HR][SC_TX][8];
+    const int x0 = blockIdx.x * SC_TX, y0 = blockIdx.y * SC_TY, d0 = blockIdx.z * 8;
+    const int SW2 = a.SW2, SH2 = a.SH2, W1 = a.width1, W = a.W;
+    const int rows_h = SC_TY + 2 * SH2, cols_h = SC_TX + 2 * SW2;
+    const size_t plane = (size_t)a.H * W;
+    const int xlo = max(x0 - SW2, 0), xhi = min(x0 + SC_TX + SW2 - 1, W1 - 1);  // clamped x1 range
+    const int rbase = xlo + a.minX1 - a.minD - d0 - 7;                           // right column of rpl[.][0]
+    const int rcols = xhi - xlo + 8;
+    auto gather = [&](int im, int y, int X) {
+        const uint8_t* b = a.planes + (size_t)(im * 6) * plane + (size_t)y * W + X;
+        uint2 w;
+        w.x = b[0] | (b[plane] << 8) | (b[2 * plane] << 16) | (b[3 * plane] << 24);
+        w.y = b[4 * plane] | (b[5 * plane] << 8);
+        return w;
+    };
+    for (int i = threadIdx.x; i < rows_h * cols_h; i += 256) {
+        const int r = i / cols_h, c = i % cols_h;
+        const int y = min(max(y0 - SH2 + r, 0), a.H - 1);
+        lpl[r][c] = gather(0, y, min(max(x0 - SW2 + c, 0), W1 - 1) + a.minX1);
+    }
+    for (int i = threadIdx.x; i < rows_h * rcols; i += 256) {
+        const int r = i / rcols, c = i % rcols;
+        const int y = min(max(y0 - SH2 + r, 0), a.H - 1);
+        rpl[r][c] = gather(1, y, rbase + c);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < rows_h * cols_h; i += 256) {
+        const int r = i / cols_h, c = i % cols_h;
+        const int x1 = min(max(x0 - SW2 + c, 0), W1 - 1);
+        const int ri = x1 - xlo + 7;  // right column index for disparity d0 (j = 0)
+        const uint2 L = lpl[r][c];
+        uint2 w;
+        uint8_t* pb = reinterpret_cast<uint8_t*>(&w);
+#pragma unroll
+        for (int j = 0; j < 8; j++) pb[j] = (uint8_t)bt_cost2(L, rpl[r][ri - j]);
+        *reinterpret_cast<uint2*>(&pix[r][c][0]) = w;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < rows_h * SC_TX; i += 256) {
+        const int r = i / SC_TX, c = i % SC_TX;
+        uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int j = 0; j <= 2 * SW2; j++) {
+            const uint2 w = *reinterpret_cast<const uint2*>(&pix[r][c + j][0]);
+            const uint8_t* pb = reinterpret_cast<const uint8_t*>(&w);
+#pragma unroll
+            for (int q = 0; q < 8; q++) acc[q] += pb[q];
         }
-        a.hsum[i] = (uint16_t)acc;
+        uint4 o;
+        o.x = acc[0] | (acc[1] << 16); o.y = acc[2] | (acc[3] << 16);
+        o.z = acc[4] | (acc[5] << 16); o.w = acc[6] | (acc[7] << 16);
+        *reinterpret_cast<uint4*>(&hs[r][c][0]) = o;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < SC_TY * SC_TX; i += 256) {
+        const int r = i / SC_TX, c = i % SC_TX;
+        const int y = y0 + r, x1 = x0 + c;
+        if (y >= a.Yc || x1 >= W1) continue;
+        uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int k = 0; k <= 2 * SH2; k++) {
+            const uint4 w = *reinterpret_cast<const uint4*>(&hs[r + k][c][0]);
+            acc[0] += w.x & 0xFFFF; acc[1] += w.x >> 16; acc[2] += w.y & 0xFFFF; acc[3] += w.y >> 16;
+            acc[4] += w.z & 0xFFFF; acc[5] += w.z >> 16; acc[6] += w.w & 0xFFFF; acc[7] += w.w >> 16;
+        }
+        uint4 o;  // int16 wrap == low 16 bits
+        o.x = (acc[0] & 0xFFFF) | (acc[1] << 16); o.y = (acc[2] & 0xFFFF) | (acc[3] << 16);
+        o.z = (acc[4] & 0xFFFF) | (acc[5] << 16); o.w = (acc[6] & 0xFFFF) | (acc[7] << 16);
+        *reinterpret_cast<uint4*>(a.C + ((size_t)y * W1 + x1) * a.D + d0) = o;
     }
 }
 
-// C_true[y] = wrap16(sum_{k=yc-SH2..yc+SH2} hsum[clamp(k)]), yc = clamp(y, 0, H-1-SH2);
-// MODE_HH leaves rows y >= 1, y > H-1-SH2 at the P2 seed (C_true = 0).
-struct VsumArgs {
-    const uint16_t* hsum;
-    uint16_t* C;
-    int H, width1, D, SH2, hh;
-};
-
-__global__ void __launch_bounds__(256) k_sgbm_vsum(VsumArgs a)
+// Rows y >= Yc: MODE_SGBM reuses one C row, so they stay equal to row Yc-1;
+// MODE_HH keeps one C row per y that is never updated (P2 seed only: C_true = 0).
+__global__ void __launch_bounds__(256) k_sgbm_cost_tail(uint16_t* C, int H, int Yc, size_t row_elems, int hh)
 {
-    const size_t row = (size_t)a.width1 * a.D;
-    const size_t n = (size_t)a.H * row;
-    const int last = a.H - 1 - a.SH2;
-    for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
-        int y = (int)(i / row);
-        size_t r = i % row;
-        if (a.hh && y >= 1 && y > last) {
-            a.C[i] = 0;
-            continue;
-        }
-        int yc = max(0, min(y, last));
-        int acc = 0;
-        for (int k = yc - a.SH2; k <= yc + a.SH2; k++) acc += a.hsum[(size_t)min(max(k, 0), a.H - 1) * row + r];
-        a.C[i] = (uint16_t)(int16_t)acc;
-    }
+    const size_t n = (size_t)(H - Yc) * row_elems / 8;
+    const uint4* src = reinterpret_cast<const uint4*>(C + (size_t)(Yc - 1) * row_elems);
+    uint4* dst = reinterpret_cast<uint4*>(C + (size_t)Yc * row_elems);
+    const size_t per_row = row_elems / 8;
+    for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+        dst[i] = hh ? make_uint4(0, 0, 0, 0) : src[i % per_row];
 }
 
 }  // namespace smk
