@@ -37,6 +37,8 @@ def parse():
     ap.add_argument("--mode", default="census8", choices=["census8", "sgbm5"])
     ap.add_argument("--pairs-per-gpu", type=int, default=8)
     ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--row", action="store_true",
+                    help="experimental fused row kernel (E/W paths + WTA) instead of k_wta (D %% 64 == 0)")
     ap.add_argument("--cpu-baseline-pairs", type=int, default=8,
                     help="KITTI pairs timed on the host C port (rank 0, N=1 only); 0 = skip")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
@@ -79,6 +81,8 @@ def main():
     eng = _lib.Engine(local_rank)
     stream = torch.cuda.current_stream(dev)
     eng.set_stream(stream.cuda_stream)
+    if args.row:
+        eng.set_debug_flags(32)
 
     def step():
         eng.compute_batch_device(dL.data_ptr(), dR.data_ptr(), P, H * W, H, W, W, prm, dOut.data_ptr())
@@ -125,24 +129,34 @@ def main():
         vol = H * width1 * D
         P_dirs = 8 if args.mode == "census8" else 5
         eb = 1 if args.mode == "census8" else 2  # bytes per path element
-        paths_ms, paths_launches, paths_pairs = stages["paths"]
-        paths_avg_s = paths_ms / 1e3 / max(paths_launches, 1)
-        pairs_per_launch = paths_pairs / max(paths_launches, 1)
-        # dominant kernel = SGM path aggregation: per pair it must
-        # write one path volume per direction and read its cost source once —
-        # the two census images (census on the fly) or, in OpenCV-parity mode,
-        # the int16 cost volume once per direction.
-        src_bytes = 2 * H * W * 8 if args.mode == "census8" else P_dirs * vol * 2
-        alg_bytes_pair = P_dirs * vol * eb + src_bytes
-        alg_bytes_paths = alg_bytes_pair * pairs_per_launch
+        row_mode = args.row and D % 64 == 0  # both horizontal paths fused into the row/WTA kernel
+        census_b = 2 * H * W * 8 if args.mode == "census8" else 0
+        if row_mode:
+            # paths launch: vertical family only; row kernel: E (+W) paths + WTA
+            paths_bytes = (P_dirs - 2) * vol * eb + (census_b or (P_dirs - 2) * vol * 2)
+            wta_bytes = vol * eb + (P_dirs - 1) * vol * eb + (census_b or 2 * vol * 2) + 2 * H * W
+            wta_name = "k_row_wta (E/W paths + WTA + disp2/LR, one wave per row)"
+        else:
+            paths_bytes = P_dirs * vol * eb + (census_b or P_dirs * vol * 2)
+            wta_bytes = P_dirs * vol * eb + 2 * H * W
+            wta_name = "k_wta"
+        kern = {"paths": ("k_sgm_paths (vertical family)" if row_mode else "k_sgm_paths (all directions)",
+                          paths_bytes),
+                "wta": (wta_name, wta_bytes)}
+        # dominant kernel = the stage with the larger device time
+        dom = max(("paths", "wta"), key=lambda k: stages[k][0])
+        dom_ms, dom_launches, dom_pairs = stages[dom]
+        paths_avg_s = dom_ms / 1e3 / max(dom_launches, 1)
+        pairs_per_launch = dom_pairs / max(dom_launches, 1)
+        alg_bytes_paths = kern[dom][1] * pairs_per_launch
         achieved = alg_bytes_paths / paths_avg_s / 1e9 if paths_avg_s > 0 else None
         traffic = None
         if os.path.exists(args.traffic_file):
             try:
                 with open(args.traffic_file) as f:
                     tr = json.load(f)
-                if tr.get("config") == args.config and tr.get("mode") == args.mode:
-                    traffic = tr.get("paths_hbm_bytes_per_launch")
+                if tr.get("config") == args.config and tr.get("mode") == args.mode and tr.get("kernel_stage") == dom:
+                    traffic = tr.get("hbm_bytes_per_launch")
             except (OSError, ValueError):
                 traffic = None
         # SURVEY.md §8(d) whole-pipeline model: H·W·D·(1+P+4) + 2HW + 4HW per pair
@@ -170,7 +184,7 @@ def main():
             },
             "mpix_disp_per_s": value * cells / 1e6,
             "roofline": {
-                "kernel": "k_sgm_paths (all directions, one launch)",
+                "kernel": kern[dom][0],
                 "bound": "hbm",
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,

@@ -119,7 +119,13 @@ long long sm_debug_fetch(sm_ctx* ctx, int what, void* host, size_t bytes);
 /* Timing ablations ONLY (results become wrong): bit 0 skips the horizontal
  * path family, bit 1 the vertical/diagonal family, bit 2 drops every path
  * store; bit 3 (valid results) selects 16-lane instead of 8-lane vertical
- * lines at D = 128.  0 = normal operation. */
+ * lines at D = 128; bit 5 (valid results, D % 64 == 0) replaces the
+ * horizontal family + WTA with the experimental fused row kernel (W path
+ * kept on chip); bit 4 (valid results) makes that kernel store the W path
+ * volume too, so sm_debug_fetch(1) returns every direction; bit 6 (valid
+ * results) runs WTA + median on a second internal stream, overlapped with
+ * the next launch group's path aggregation (double-buffered volumes).
+ * 0 = normal operation. */
 int sm_set_debug_flags(sm_ctx* ctx, int flags);
 
 /* Last error text of ctx (or of the calling thread when ctx == NULL). */

@@ -3,6 +3,16 @@
 // Host side of the drop-in boundary for stereo_vision/stereo_vision.py:153-179
 // (cv2.StereoSGBM_create(...).compute).  Parameter normalisation mirrors
 // OpenCV computeDisparitySGBM (see oracle/sgm_np.py:normalize_params).
+//
+// Pipeline per launch group of G pairs:
+//   cost (census | SGBM BT+box) -> path aggregation -> WTA + disp2/LR -> median
+// all on the caller's stream (A).  Optional overlap (debug flag 64): WTA and
+// median of group g run on an internal stream B while group g+1 aggregates
+// paths on A, double-buffered over two buffer sets; A waits for B at the end
+// of every call, so callers only ever synchronise with their own stream.
+// Measured on MI355X the overlap is a net loss for the
+// headline config — the two kernels slow each other more than they overlap —
+// so it stays opt-in.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -17,8 +27,9 @@
 #include "sm_cost.hpp"
 #include "sm_paths.hpp"
 #include "sm_post.hpp"
+#include "sm_rowwta.hpp"
 
-#define SM_VERSION "stereo_match_amd 0.1.0 (gfx950)"
+#define SM_VERSION "stereo_match_amd 0.2.0 (gfx950)"
 
 namespace {
 
@@ -39,16 +50,29 @@ struct TimedEvent {
     hipEvent_t a, b;
 };
 
+// per-group device buffers (double-buffered across launch groups)
+struct BufSet {
+    DevBuf census[2], cost, L, raw;
+    hipEvent_t paths_done = nullptr, wta_done = nullptr;
+    bool pending = false;  // wta_done recorded and not yet waited for by stream A
+};
+
+// debug flags (sm_set_debug_flags); 1 skip horizontal, 2 skip vertical and 4 drop stores are read in-kernel
+constexpr int DBG_VL16 = 8, DBG_STORE_W = 16, DBG_ROW = 32, DBG_OVERLAP = 64;
+
 }  // namespace
 
 struct sm_ctx {
     int device = 0;
     hipStream_t own_stream = nullptr;
-    hipStream_t stream = nullptr;
-    DevBuf img[2], census[2], planes, hsum, cost, L, raw, out, dbg;
+    hipStream_t stream = nullptr;  // stream A
+    hipStream_t side = nullptr;    // stream B
+    DevBuf img[2], planes, out, dbg;
+    BufSet set[2];
+    int next_set = 0;
     // geometry of the last computation (for sm_debug_fetch): its last pair
     int lastH = 0, lastW = 0, last_width1 = 0, lastD = 0, last_ndirs = 0, last_cost = 0, last_minD = 0;
-    int last_minX1 = 0, last_index = 0;
+    int last_minX1 = 0, last_index = 0, last_set = 0;
     size_t last_L_pair = 0;
     bool timing = false;
     int dbg_flags = 0;
@@ -82,11 +106,12 @@ int fail(sm_ctx* ctx, int code, const char* fmt, ...)
                         __FILE__, __LINE__);                                                          \
     } while (0)
 
+// (re)allocate; callers make sure no queued work still uses the old buffer
 int ensure(sm_ctx* ctx, DevBuf& b, size_t bytes)
 {
     if (b.n >= bytes && b.p) return SM_OK;
     if (b.p) {
-        (void)hipStreamSynchronize(ctx->stream);
+        HIP_TRY(ctx, hipDeviceSynchronize());
         (void)hipFree(b.p);
         b.p = nullptr;
         b.n = 0;
@@ -157,20 +182,21 @@ hipEvent_t get_event(sm_ctx* ctx)
 
 struct StageTimer {
     sm_ctx* ctx;
+    hipStream_t s;
     int stage, pairs;
     hipEvent_t a = nullptr;
-    StageTimer(sm_ctx* c, int s, int np) : ctx(c), stage(s), pairs(np)
+    StageTimer(sm_ctx* c, hipStream_t st, int stg, int np) : ctx(c), s(st), stage(stg), pairs(np)
     {
         if (ctx->timing) {
             a = get_event(ctx);
-            (void)hipEventRecord(a, ctx->stream);
+            (void)hipEventRecord(a, s);
         }
     }
     ~StageTimer()
     {
         if (ctx->timing) {
             hipEvent_t b = get_event(ctx);
-            (void)hipEventRecord(b, ctx->stream);
+            (void)hipEventRecord(b, s);
             ctx->pending.push_back({stage, pairs, a, b});
         }
     }
@@ -191,107 +217,6 @@ void harvest_timing(sm_ctx* ctx)
     ctx->pending.clear();
 }
 
-// Output slots: 0 E, 1 W (horizontal family), 2 SE, 3 S, 4 SW (MODE_SGBM adds
-// these three), 5 NE, 6 N, 7 NW (MODE_HH / 8-path adds these three).
-const int kVdx[6] = {1, 0, -1, 1, 0, -1};
-const int kVdy[6] = {1, 1, 1, -1, -1, -1};
-
-constexpr size_t kGroupBudget = size_t(24) << 30;  // bytes of path volumes per launch group
-constexpr int kMaxGroup = 16;
-
-template <int DPLV, bool CENSUS, int VL = 16>
-int launch_paths_wta(sm_ctx* ctx, const Norm& n, int H, int W, int G, size_t L_pair, size_t slot_bytes,
-                     size_t census_pair, size_t cost_pair)
-{
-    // 8-lane vertical lines for D = 128 (ablation flag 8 selects 16-lane lines)
-    if constexpr (VL == 16 && DPLV == 8) {
-        if (!(ctx->dbg_flags & 8))
-            return launch_paths_wta<DPLV, CENSUS, 8>(ctx, n, H, W, G, L_pair, slot_bytes, census_pair, cost_pair);
-    }
-    using LT = typename std::conditional<CENSUS, uint8_t, uint16_t>::type;
-    constexpr int D = 16 * DPLV;
-    constexpr bool WIDE = D % 64 == 0;
-    constexpr int LANESH = WIDE ? 64 : 16;
-    constexpr int DPLH = D / LANESH;
-    smk::PathsArgs pa{};
-    pa.cl = (const uint64_t*)ctx->census[0].p;
-    pa.cr = (const uint64_t*)ctx->census[1].p;
-    pa.census_pair = census_pair;
-    pa.cost = (const uint16_t*)ctx->cost.p;
-    pa.cost_pair = cost_pair;
-    pa.L = (uint8_t*)ctx->L.p;
-    pa.slot_bytes = slot_bytes;
-    pa.L_pair_bytes = L_pair;
-    pa.H = H;
-    pa.W = W;
-    pa.width1 = n.width1;
-    pa.D = n.D;
-    pa.minD = n.minD;
-    pa.minX1 = n.minX1;
-    pa.P1 = n.P1;
-    pa.P2 = n.P2;
-    pa.dbg = ctx->dbg_flags;
-    const int lines_per_wg = 4 * (64 / LANESH);
-    pa.hblocks = (H + lines_per_wg - 1) / lines_per_wg;
-    pa.nv = n.ndirs - 2;
-    int blocks = 0;
-    for (int k = 0; k < pa.nv; k++) {
-        pa.v_dx[k] = kVdx[k];
-        pa.v_dy[k] = kVdy[k];
-        pa.v_slot[k] = 2 + k;
-        pa.v_line_lo[k] = kVdx[k] > 0 ? -(H - 1) : 0;
-        pa.v_nlines[k] = kVdx[k] == 0 ? n.width1 : n.width1 + H - 1;
-        pa.v_blk_start[k] = blocks;
-        // waves come in groups of 8 covering 8*LPW lines (lines w + 8*kl)
-        constexpr int LPWV = 64 / VL;
-        blocks += ((pa.v_nlines[k] + 8 * LPWV - 1) / (8 * LPWV)) * 2;
-    }
-    for (int k = pa.nv; k <= 6; k++) pa.v_blk_start[k] = blocks;
-    {
-        StageTimer t(ctx, SM_STAGE_PATHS, G);
-        hipLaunchKernelGGL((smk::k_sgm_paths<VL, DPLV * 16 / VL, LANESH, DPLH, CENSUS, LT>), dim3(2 * pa.hblocks + blocks, G),
-                           dim3(256), 0, ctx->stream, pa);
-        HIP_TRY(ctx, hipGetLastError());
-    }
-    smk::WtaArgs wa{};
-    wa.L = (const uint8_t*)ctx->L.p;
-    wa.slot_bytes = slot_bytes;
-    wa.L_pair_bytes = L_pair;
-    wa.nslots = n.ndirs;
-    wa.H = H;
-    wa.W = W;
-    wa.width1 = n.width1;
-    wa.D = n.D;
-    wa.minD = n.minD;
-    wa.minX1 = n.minX1;
-    wa.uniq = n.uniq;
-    wa.disp12 = n.disp12;
-    wa.disp = (int16_t*)ctx->raw.p;
-    {
-        StageTimer t(ctx, SM_STAGE_WTA, G);
-        const size_t smem = (size_t)W * 8;
-        hipLaunchKernelGGL((smk::k_wta<DPLV, LT, 1024>), dim3(H, G), dim3(1024), smem, ctx->stream, wa);
-        HIP_TRY(ctx, hipGetLastError());
-    }
-    return SM_OK;
-}
-
-int dispatch_dpl(sm_ctx* ctx, const Norm& n, int H, int W, int G, size_t L_pair, size_t slot_bytes,
-                 size_t census_pair, size_t cost_pair)
-{
-    const bool census = n.cost == SM_COST_CENSUS;
-    switch (n.dpl) {
-#define CASE(k)                                                                                          \
-    case k:                                                                                              \
-        return census ? launch_paths_wta<k, true>(ctx, n, H, W, G, L_pair, slot_bytes, census_pair, cost_pair) \
-                      : launch_paths_wta<k, false>(ctx, n, H, W, G, L_pair, slot_bytes, census_pair, cost_pair);
-        CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
-        CASE(9) CASE(10) CASE(11) CASE(12) CASE(13) CASE(14) CASE(15) CASE(16)
-#undef CASE
-    default: return fail(ctx, SM_E_UNSUPPORTED, "numDisparities %d not built", n.D);
-    }
-}
-
 int grid_for(size_t n)
 {
     size_t g = (n + 255) / 256;
@@ -300,58 +225,218 @@ int grid_for(size_t n)
 
 size_t elem_bytes(const Norm& n) { return n.cost == SM_COST_CENSUS ? 1 : 2; }
 
-int group_size(const Norm& n, int H, int npairs)
+// Output slots: 0 E, 1 W (horizontal family), 2 SE, 3 S, 4 SW (MODE_SGBM adds
+// these three), 5 NE, 6 N, 7 NW (MODE_HH / 8-path adds these three).
+const int kVdx[6] = {1, 0, -1, 1, 0, -1};
+const int kVdy[6] = {1, 1, 1, -1, -1, -1};
+
+constexpr size_t kSetBudget = size_t(12) << 30;  // bytes of path volumes per buffer set
+constexpr int kMaxGroup = 16;
+
+struct Geo {  // per-group geometry shared by the launches
+    int H, W, stride, G;
+    size_t vol, slot_bytes, L_pair, census_pair, cost_pair;
+};
+
+bool row_mode(const sm_ctx* ctx, const Norm& n) { return (ctx->dbg_flags & DBG_ROW) && n.D % 64 == 0; }
+bool overlap(const sm_ctx* ctx) { return (ctx->dbg_flags & DBG_OVERLAP) != 0; }
+hipStream_t stream_b(const sm_ctx* ctx) { return overlap(ctx) ? ctx->side : ctx->stream; }
+
+// ---- stream A: path aggregation -------------------------------------------
+template <int DPLV, bool CENSUS, int VL>
+int launch_paths_t(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs)
 {
-    const size_t per = (size_t)H * std::max(n.width1, 1) * n.D * elem_bytes(n) * n.ndirs;
-    size_t g = std::max<size_t>(1, kGroupBudget / std::max<size_t>(per, 1));
-    return (int)std::min<size_t>({g, (size_t)kMaxGroup, (size_t)std::max(npairs, 1)});
+    using LT = typename std::conditional<CENSUS, uint8_t, uint16_t>::type;
+    constexpr int D = 16 * DPLV;
+    constexpr bool WIDE = D % 64 == 0;
+    constexpr int LANESH = WIDE ? 64 : 16;
+    constexpr int DPLH = D / LANESH;
+    smk::PathsArgs pa{};
+    pa.cl = (const uint64_t*)bs.census[0].p;
+    pa.cr = (const uint64_t*)bs.census[1].p;
+    pa.census_pair = g.census_pair;
+    pa.cost = (const uint16_t*)bs.cost.p;
+    pa.cost_pair = g.cost_pair;
+    pa.L = (uint8_t*)bs.L.p;
+    pa.slot_bytes = g.slot_bytes;
+    pa.L_pair_bytes = g.L_pair;
+    pa.H = g.H;
+    pa.W = g.W;
+    pa.width1 = n.width1;
+    pa.D = n.D;
+    pa.minD = n.minD;
+    pa.minX1 = n.minX1;
+    pa.P1 = n.P1;
+    pa.P2 = n.P2;
+    pa.dbg = ctx->dbg_flags;
+    const int lines_per_wg = 4 * (64 / LANESH);
+    pa.hblocks = row_mode(ctx, n) ? 0 : (g.H + lines_per_wg - 1) / lines_per_wg;
+    pa.nv = n.ndirs - 2;
+    int blocks = 0;
+    constexpr int LPWV = 64 / VL;
+    for (int k = 0; k < pa.nv; k++) {
+        pa.v_dx[k] = kVdx[k];
+        pa.v_dy[k] = kVdy[k];
+        pa.v_slot[k] = 2 + k;
+        pa.v_line_lo[k] = kVdx[k] > 0 ? -(g.H - 1) : 0;
+        pa.v_nlines[k] = kVdx[k] == 0 ? n.width1 : n.width1 + g.H - 1;
+        pa.v_blk_start[k] = blocks;
+        // waves come in groups of 8 covering 8*LPW lines (lines w + 8*kl)
+        blocks += ((pa.v_nlines[k] + 8 * LPWV - 1) / (8 * LPWV)) * 2;
+    }
+    for (int k = pa.nv; k <= 6; k++) pa.v_blk_start[k] = blocks;
+    StageTimer t(ctx, ctx->stream, SM_STAGE_PATHS, g.G);
+    hipLaunchKernelGGL((smk::k_sgm_paths<VL, DPLV * 16 / VL, LANESH, DPLH, CENSUS, LT>),
+                       dim3(2 * pa.hblocks + blocks, g.G), dim3(256), 0, ctx->stream, pa);
+    HIP_TRY(ctx, hipGetLastError());
+    return SM_OK;
 }
 
-// G pairs (device pointers; pair i at dL + i*pair_stride), enqueued on ctx->stream.
-int run_group(sm_ctx* ctx, const uint8_t* dL, const uint8_t* dR, size_t pair_stride, int G, int H, int W,
-              int stride, const Norm& n, int16_t* d_out)
+// ---- stream B: WTA (or the fused horizontal + WTA row kernel) ----------------
+template <int DPLV, bool CENSUS>
+int launch_wta_t(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs)
 {
-    const int INVALID = (n.minD - 1) * 16;
-    StageTimer total(ctx, SM_STAGE_TOTAL, G);
+    using LT = typename std::conditional<CENSUS, uint8_t, uint16_t>::type;
+    constexpr int D = 16 * DPLV;
+    StageTimer t(ctx, stream_b(ctx), SM_STAGE_WTA, g.G);
+    if constexpr (D % 64 == 0) {
+        if (row_mode(ctx, n)) {
+            smk::RowArgs ra{};
+            ra.cl = (const uint64_t*)bs.census[0].p;
+            ra.cr = (const uint64_t*)bs.census[1].p;
+            ra.census_pair = g.census_pair;
+            ra.cost = (const uint16_t*)bs.cost.p;
+            ra.cost_pair = g.cost_pair;
+            ra.L = (uint8_t*)bs.L.p;
+            ra.slot_bytes = g.slot_bytes;
+            ra.L_pair_bytes = g.L_pair;
+            ra.H = g.H;
+            ra.W = g.W;
+            ra.width1 = n.width1;
+            ra.D = n.D;
+            ra.minD = n.minD;
+            ra.minX1 = n.minX1;
+            ra.P1 = n.P1;
+            ra.P2 = n.P2;
+            ra.uniq = n.uniq;
+            ra.disp12 = n.disp12;
+            ra.store_w = (ctx->dbg_flags & DBG_STORE_W) ? 1 : 0;
+            ra.disp = (int16_t*)bs.raw.p;
+            const size_t smem = (1024 + (size_t)g.W * 6 + 15) & ~size_t(15);
+            if (n.ndirs == 8)
+                hipLaunchKernelGGL((smk::k_row_wta<D / 64, 8, CENSUS, LT>), dim3(g.H, g.G), dim3(64), smem, stream_b(ctx), ra);
+            else
+                hipLaunchKernelGGL((smk::k_row_wta<D / 64, 5, CENSUS, LT>), dim3(g.H, g.G), dim3(64), smem, stream_b(ctx), ra);
+            HIP_TRY(ctx, hipGetLastError());
+            return SM_OK;
+        }
+    }
+    smk::WtaArgs wa{};
+    wa.L = (const uint8_t*)bs.L.p;
+    wa.slot_bytes = g.slot_bytes;
+    wa.L_pair_bytes = g.L_pair;
+    wa.nslots = n.ndirs;
+    wa.H = g.H;
+    wa.W = g.W;
+    wa.width1 = n.width1;
+    wa.D = n.D;
+    wa.minD = n.minD;
+    wa.minX1 = n.minX1;
+    wa.uniq = n.uniq;
+    wa.disp12 = n.disp12;
+    wa.disp = (int16_t*)bs.raw.p;
+    hipLaunchKernelGGL((smk::k_wta<DPLV, LT, 1024>), dim3(g.H, g.G), dim3(1024), (size_t)g.W * 8, stream_b(ctx), wa);
+    HIP_TRY(ctx, hipGetLastError());
+    return SM_OK;
+}
+
+template <int DPLV, bool CENSUS>
+int launch_paths_dpl(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs)
+{
+    // 8-lane vertical lines at D = 128 (16-lane with the ablation flag)
+    if constexpr (DPLV == 8) {
+        if (!(ctx->dbg_flags & DBG_VL16)) return launch_paths_t<DPLV, CENSUS, 8>(ctx, n, g, bs);
+    }
+    return launch_paths_t<DPLV, CENSUS, 16>(ctx, n, g, bs);
+}
+
+int dispatch(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs, bool wta)
+{
+    const bool census = n.cost == SM_COST_CENSUS;
+    switch (n.dpl) {
+#define CASE(k)                                                                                           \
+    case k:                                                                                               \
+        if (wta) return census ? launch_wta_t<k, true>(ctx, n, g, bs) : launch_wta_t<k, false>(ctx, n, g, bs); \
+        return census ? launch_paths_dpl<k, true>(ctx, n, g, bs) : launch_paths_dpl<k, false>(ctx, n, g, bs);
+        CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
+        CASE(9) CASE(10) CASE(11) CASE(12) CASE(13) CASE(14) CASE(15) CASE(16)
+#undef CASE
+    default: return fail(ctx, SM_E_UNSUPPORTED, "numDisparities %d not built", n.D);
+    }
+}
+
+int group_size(const sm_ctx* ctx, const Norm& n, int H, int npairs)
+{
+    const size_t per = (size_t)H * std::max(n.width1, 1) * n.D * elem_bytes(n) * n.ndirs;
+    const size_t g = std::max<size_t>(1, kSetBudget / std::max<size_t>(per, 1));
+    // at least two groups per call when possible, so WTA(g) overlaps paths(g+1)
+    const size_t half = overlap(ctx) ? std::max(1, (npairs + 1) / 2) : kMaxGroup;
+    return (int)std::min<size_t>({g, (size_t)kMaxGroup, half});
+}
+
+int ensure_event(sm_ctx* ctx, hipEvent_t& e)
+{
+    if (!e) HIP_TRY(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    return SM_OK;
+}
+
+// G pairs (device pointers; pair i at dL + i*pair_stride).
+int run_group(sm_ctx* ctx, const uint8_t* dL, const uint8_t* dR, size_t pair_stride, const Geo& g, const Norm& n,
+              int16_t* d_out)
+{
+    const int H = g.H, W = g.W, G = g.G;
+    const int s = overlap(ctx) ? ctx->next_set : 0;  // one buffer set unless overlapping
+    ctx->next_set = s ^ 1;
+    BufSet& bs = ctx->set[s];
+    int rc;
+    if ((rc = ensure_event(ctx, bs.paths_done)) != SM_OK) return rc;
+    if ((rc = ensure_event(ctx, bs.wta_done)) != SM_OK) return rc;
+    // buffer set s is free once stream B finished its previous group
+    if (bs.pending) HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, bs.wta_done, 0));
     if (n.width1 <= 0) {
+        const int INVALID = (n.minD - 1) * 16;
         for (int i = 0; i < G; i++) {
             hipLaunchKernelGGL(smk::k_fill16, dim3(grid_for((size_t)H * W)), dim3(256), 0, ctx->stream,
                                d_out + (size_t)i * H * W, (size_t)H * W, (int16_t)INVALID);
             HIP_TRY(ctx, hipGetLastError());
         }
+        bs.pending = false;
         ctx->last_width1 = 0;
         return SM_OK;
     }
-    const size_t vol = (size_t)H * n.width1 * n.D;
-    const size_t eb = elem_bytes(n);
-    const size_t slot_bytes = (vol * eb + 255) & ~size_t(255);
-    const size_t L_pair = slot_bytes * n.ndirs;
-    const size_t census_pair = (size_t)H * W;
-    const size_t cost_pair = n.cost == SM_COST_CENSUS ? 0 : vol;
-    int rc;
-    if ((rc = ensure(ctx, ctx->L, L_pair * G)) != SM_OK) return rc;
-    if ((rc = ensure(ctx, ctx->raw, (size_t)G * H * W * 2)) != SM_OK) return rc;
+    if ((rc = ensure(ctx, bs.L, g.L_pair * G)) != SM_OK) return rc;
+    if ((rc = ensure(ctx, bs.raw, (size_t)G * H * W * 2)) != SM_OK) return rc;
     {
-        StageTimer t(ctx, SM_STAGE_COST, G);
+        StageTimer t(ctx, ctx->stream, SM_STAGE_COST, G);
         if (n.cost == SM_COST_CENSUS) {
             for (int i = 0; i < 2; i++)
-                if ((rc = ensure(ctx, ctx->census[i], (size_t)G * census_pair * 8)) != SM_OK) return rc;
+                if ((rc = ensure(ctx, bs.census[i], (size_t)G * g.census_pair * 8)) != SM_OK) return rc;
             smk::CensusArgs ca{};
             ca.img[0] = dL;
             ca.img[1] = dR;
-            ca.out[0] = (uint64_t*)ctx->census[0].p;
-            ca.out[1] = (uint64_t*)ctx->census[1].p;
+            ca.out[0] = (uint64_t*)bs.census[0].p;
+            ca.out[1] = (uint64_t*)bs.census[1].p;
             ca.in_pair = pair_stride;
             ca.H = H;
             ca.W = W;
-            ca.stride = stride;
+            ca.stride = g.stride;
             hipLaunchKernelGGL(smk::k_census9x7,
                                dim3((W + smk::CT_W - 1) / smk::CT_W, (H + smk::CT_H - 1) / smk::CT_H, 2 * G),
                                dim3(256), 0, ctx->stream, ca);
             HIP_TRY(ctx, hipGetLastError());
         } else {
             if ((rc = ensure(ctx, ctx->planes, (size_t)H * W * 12)) != SM_OK) return rc;
-            if ((rc = ensure(ctx, ctx->cost, (size_t)G * vol * 2)) != SM_OK) return rc;
+            if ((rc = ensure(ctx, bs.cost, (size_t)G * g.vol * 2)) != SM_OK) return rc;
             for (int i = 0; i < G; i++) {
                 smk::PrefilterArgs pf{};
                 pf.img[0] = dL + (size_t)i * pair_stride;
@@ -359,13 +444,13 @@ int run_group(sm_ctx* ctx, const uint8_t* dL, const uint8_t* dR, size_t pair_str
                 pf.planes = (uint8_t*)ctx->planes.p;
                 pf.H = H;
                 pf.W = W;
-                pf.stride = stride;
+                pf.stride = g.stride;
                 pf.ftzero = n.ftzero;
                 hipLaunchKernelGGL(smk::k_sgbm_prefilter, dim3((W + 255) / 256, H, 2), dim3(256), 0, ctx->stream, pf);
                 HIP_TRY(ctx, hipGetLastError());
                 smk::SgbmCostArgs sc{};
                 sc.planes = pf.planes;
-                sc.C = (uint16_t*)ctx->cost.p + (size_t)i * vol;
+                sc.C = (uint16_t*)bs.cost.p + (size_t)i * g.vol;
                 sc.H = H;
                 sc.W = W;
                 sc.width1 = n.width1;
@@ -384,21 +469,32 @@ int run_group(sm_ctx* ctx, const uint8_t* dL, const uint8_t* dR, size_t pair_str
                     const size_t row = (size_t)n.width1 * n.D;
                     hipLaunchKernelGGL(smk::k_sgbm_cost_tail, dim3(grid_for((size_t)(H - sc.Yc) * row / 8)), dim3(256), 0,
                                        ctx->stream, sc.C, H, sc.Yc, row, (int)(n.mode == SM_MODE_HH));
+                    HIP_TRY(ctx, hipGetLastError());
                 }
-                HIP_TRY(ctx, hipGetLastError());
             }
         }
     }
-    if ((rc = dispatch_dpl(ctx, n, H, W, G, L_pair, slot_bytes, census_pair, cost_pair)) != SM_OK) return rc;
+    if ((rc = dispatch(ctx, n, g, bs, false)) != SM_OK) return rc;
+    const hipStream_t sb = stream_b(ctx);
+    if (sb != ctx->stream) {
+        HIP_TRY(ctx, hipEventRecord(bs.paths_done, ctx->stream));
+        HIP_TRY(ctx, hipStreamWaitEvent(sb, bs.paths_done, 0));
+    }
+    if ((rc = dispatch(ctx, n, g, bs, true)) != SM_OK) return rc;
     {
-        StageTimer t(ctx, SM_STAGE_MEDIAN, G);
-        hipLaunchKernelGGL(smk::k_median3, dim3((W + 255) / 256, H, G), dim3(256), 0, ctx->stream,
-                           (const int16_t*)ctx->raw.p, d_out, H, W, (size_t)H * W);
+        StageTimer t(ctx, sb, SM_STAGE_MEDIAN, G);
+        hipLaunchKernelGGL(smk::k_median3, dim3((W + 255) / 256, H, G), dim3(256), 0, sb,
+                           (const int16_t*)bs.raw.p, d_out, H, W, (size_t)H * W);
         HIP_TRY(ctx, hipGetLastError());
+    }
+    if (sb != ctx->stream) {
+        HIP_TRY(ctx, hipEventRecord(bs.wta_done, sb));
+        bs.pending = true;
     }
     ctx->last_width1 = n.width1;
     ctx->last_index = G - 1;
-    ctx->last_L_pair = L_pair;
+    ctx->last_L_pair = g.L_pair;
+    ctx->last_set = s;
     return SM_OK;
 }
 
@@ -412,15 +508,34 @@ int run_pairs(sm_ctx* ctx, const uint8_t* dL, const uint8_t* dR, size_t pair_str
     ctx->last_cost = n.cost;
     ctx->last_minD = n.minD;
     ctx->last_minX1 = n.minX1;
-    const int G = group_size(n, H, npairs);
-    for (int i = 0; i < npairs; i += G) {
-        const int g = std::min(G, npairs - i);
-        int rc = run_group(ctx, dL + (size_t)i * pair_stride, dR + (size_t)i * pair_stride, pair_stride, g, H, W,
-                           stride, n, d_out + (size_t)i * H * W);
-        if (rc != SM_OK) return rc;
+    Geo g{};
+    g.H = H;
+    g.W = W;
+    g.stride = stride;
+    g.vol = (size_t)H * std::max(n.width1, 0) * n.D;
+    g.slot_bytes = (g.vol * elem_bytes(n) + 255) & ~size_t(255);
+    g.L_pair = g.slot_bytes * n.ndirs;
+    g.census_pair = (size_t)H * W;
+    g.cost_pair = n.cost == SM_COST_CENSUS ? 0 : g.vol;
+    const int G = group_size(ctx, n, H, npairs);
+    int rc = SM_OK;
+    {
+        StageTimer total(ctx, ctx->stream, SM_STAGE_TOTAL, npairs);
+        for (int i = 0; i < npairs && rc == SM_OK; i += G) {
+            g.G = std::min(G, npairs - i);
+            rc = run_group(ctx, dL + (size_t)i * pair_stride, dR + (size_t)i * pair_stride, pair_stride, g, n,
+                           d_out + (size_t)i * H * W);
+        }
+        // join stream B back into the caller's stream
+        for (auto& bs : ctx->set)
+            if (bs.pending) {
+                HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, bs.wta_done, 0));
+                bs.pending = false;
+            }
     }
-    return SM_OK;
+    return rc;
 }
+
 }  // namespace
 
 extern "C" {
@@ -439,6 +554,7 @@ int sm_create(int device, sm_ctx** out)
     ctx->device = device;
     e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete ctx;
         return fail(nullptr, SM_E_HIP, "context creation failed: %s", hipGetErrorString(e));
@@ -452,16 +568,23 @@ void sm_destroy(sm_ctx* ctx)
 {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
-    (void)hipStreamSynchronize(ctx->stream);
-    DevBuf* bufs[] = {&ctx->img[0], &ctx->img[1], &ctx->census[0], &ctx->census[1], &ctx->planes, &ctx->hsum,
-                      &ctx->cost, &ctx->L, &ctx->raw, &ctx->out, &ctx->dbg};
+    (void)hipDeviceSynchronize();
+    DevBuf* bufs[] = {&ctx->img[0], &ctx->img[1], &ctx->planes, &ctx->out, &ctx->dbg};
     for (DevBuf* b : bufs)
         if (b->p) (void)hipFree(b->p);
+    for (auto& bs : ctx->set) {
+        DevBuf* sb[] = {&bs.census[0], &bs.census[1], &bs.cost, &bs.L, &bs.raw};
+        for (DevBuf* b : sb)
+            if (b->p) (void)hipFree(b->p);
+        if (bs.paths_done) (void)hipEventDestroy(bs.paths_done);
+        if (bs.wta_done) (void)hipEventDestroy(bs.wta_done);
+    }
     for (auto& t : ctx->pending) {
         (void)hipEventDestroy(t.a);
         (void)hipEventDestroy(t.b);
     }
     for (auto e : ctx->free_events) (void)hipEventDestroy(e);
+    if (ctx->side) (void)hipStreamDestroy(ctx->side);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
     delete ctx;
 }
@@ -546,6 +669,7 @@ int sm_synchronize(sm_ctx* ctx)
 {
     if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->side));
     return SM_OK;
 }
 
@@ -594,6 +718,7 @@ long long sm_debug_fetch(sm_ctx* ctx, int what, void* host, size_t bytes)
     const size_t slot_bytes = (vol * et + 255) & ~size_t(255);
     const size_t img = (size_t)ctx->lastH * ctx->lastW;
     const int li = ctx->last_index;
+    BufSet& bs = ctx->set[ctx->last_set];
     size_t need;
     switch (what) {
     case 0: need = vol * et; break;
@@ -606,12 +731,13 @@ long long sm_debug_fetch(sm_ctx* ctx, int what, void* host, size_t bytes)
     if (bytes < need) return fail(ctx, SM_E_ARG, "host buffer too small (%zu < %zu)", bytes, need);
     if (need == 0) return 0;
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->side));
     if (what == 0 && ctx->last_cost == SM_COST_CENSUS) {
         int rc = ensure(ctx, ctx->dbg, need);
         if (rc != SM_OK) return rc;
         smk::CensusCostArgs cc{};
-        cc.cl = (const uint64_t*)ctx->census[0].p + (size_t)li * img;
-        cc.cr = (const uint64_t*)ctx->census[1].p + (size_t)li * img;
+        cc.cl = (const uint64_t*)bs.census[0].p + (size_t)li * img;
+        cc.cr = (const uint64_t*)bs.census[1].p + (size_t)li * img;
         cc.C = (uint8_t*)ctx->dbg.p;
         cc.H = ctx->lastH;
         cc.W = ctx->lastW;
@@ -626,17 +752,17 @@ long long sm_debug_fetch(sm_ctx* ctx, int what, void* host, size_t bytes)
         return (long long)need;
     }
     switch (what) {
-    case 0: HIP_TRY(ctx, hipMemcpy(host, (uint8_t*)ctx->cost.p + (size_t)li * vol * et, need, hipMemcpyDeviceToHost)); break;
+    case 0: HIP_TRY(ctx, hipMemcpy(host, (uint8_t*)bs.cost.p + (size_t)li * vol * et, need, hipMemcpyDeviceToHost)); break;
     case 1:
         for (int k = 0; k < ctx->last_ndirs; k++)
             HIP_TRY(ctx, hipMemcpy((uint8_t*)host + k * vol * et,
-                                   (uint8_t*)ctx->L.p + (size_t)li * ctx->last_L_pair + k * slot_bytes, vol * et,
+                                   (uint8_t*)bs.L.p + (size_t)li * ctx->last_L_pair + k * slot_bytes, vol * et,
                                    hipMemcpyDeviceToHost));
         break;
-    case 2: HIP_TRY(ctx, hipMemcpy(host, (int16_t*)ctx->raw.p + (size_t)li * img, need, hipMemcpyDeviceToHost)); break;
+    case 2: HIP_TRY(ctx, hipMemcpy(host, (int16_t*)bs.raw.p + (size_t)li * img, need, hipMemcpyDeviceToHost)); break;
     case 3:
-        HIP_TRY(ctx, hipMemcpy(host, (uint64_t*)ctx->census[0].p + (size_t)li * img, img * 8, hipMemcpyDeviceToHost));
-        HIP_TRY(ctx, hipMemcpy((uint8_t*)host + img * 8, (uint64_t*)ctx->census[1].p + (size_t)li * img, img * 8,
+        HIP_TRY(ctx, hipMemcpy(host, (uint64_t*)bs.census[0].p + (size_t)li * img, img * 8, hipMemcpyDeviceToHost));
+        HIP_TRY(ctx, hipMemcpy((uint8_t*)host + img * 8, (uint64_t*)bs.census[1].p + (size_t)li * img, img * 8,
                                hipMemcpyDeviceToHost));
         break;
     }

@@ -52,11 +52,17 @@ def test_census_images_match_oracle(eng):
     assert np.array_equal(got[1], sgm_np.census9x7(right))
 
 
-@pytest.mark.parametrize("cost,mode", [(1, 8), (0, 5), (0, 8)])
-def test_path_volumes_match_oracle(eng, cost, mode):
-    left, right, _ = synthetic.random_dot_pair(33, 101, 32, seed=8)
-    p = dict(synthetic.headline_params(32) if cost else synthetic.parity_params(32), mode=mode)
-    run(eng, left, right, p)
+@pytest.mark.parametrize("cost,mode,D,flags", [(1, 8, 32, 0), (0, 5, 32, 0), (0, 8, 32, 0), (1, 8, 64, 0),
+                                                (0, 5, 64, 0), (1, 5, 128, 0), (1, 8, 64, 48), (0, 5, 128, 48)])
+def test_path_volumes_match_oracle(eng, cost, mode, D, flags):
+    left, right, _ = synthetic.random_dot_pair(33, 101 + D, D, seed=8)
+    p = dict(synthetic.headline_params(D) if cost else synthetic.parity_params(D), mode=mode)
+    # flags 48 = fused row kernel (32) + keep its W volume (16), which it normally never writes
+    eng.set_debug_flags(flags)
+    try:
+        run(eng, left, right, p)
+    finally:
+        eng.set_debug_flags(0)
     prm = sgm_np.normalize_params(p)
     C = sgm_np.cost_volume(left, right, prm)
     dt = np.uint8 if cost else np.uint16
@@ -95,13 +101,17 @@ def test_random_shapes_vs_c_oracle(eng, c):
     assert np.array_equal(out, expected), f"{np.sum(out != expected)} px differ"
 
 
-@pytest.mark.parametrize("name,cost,mode", [("kitti", 1, 8), ("kitti", 0, 5), ("kitti", 0, 8),
-                                            ("kitti", 1, 5), ("mccnn", 1, 8)])
-def test_full_size_bit_exact(eng, name, cost, mode):
+@pytest.mark.parametrize("name,cost,mode,flags", [("kitti", 1, 8, 0), ("kitti", 0, 5, 0), ("kitti", 0, 8, 0),
+                                                  ("kitti", 1, 5, 0), ("mccnn", 1, 8, 0), ("kitti", 1, 8, 32)])
+def test_full_size_bit_exact(eng, name, cost, mode, flags):
     H, W, D = synthetic.CONFIGS[name]
     left, right, gt = synthetic.random_dot_pair(H, W, D, seed=42)
     p = dict(synthetic.headline_params(D) if cost else synthetic.parity_params(D), mode=mode)
-    out = run(eng, left, right, p)
+    eng.set_debug_flags(flags)
+    try:
+        out = run(eng, left, right, p)
+    finally:
+        eng.set_debug_flags(0)
     expected = ref_c.compute(left, right, p)
     assert np.array_equal(out, expected), f"{np.sum(out != expected)} px differ"
     valid = out >= 0
@@ -151,6 +161,33 @@ def test_batch_device_matches_single(eng):
     got = out.cpu().numpy()
     for i, (a, b) in enumerate(pairs):
         assert np.array_equal(got[i], ref_c.compute(a, b, q))
+
+
+@pytest.mark.parametrize("flags", [0, 32, 64, 96])
+def test_batch_pipeline_groups(eng, flags):
+    """Batches through the normal pipeline, the fused row kernel (32) and the
+    two-stream overlap (64: 7 pairs -> launch groups of 4 + 3 on alternating
+    buffer sets, WTA of group g on the second stream beside paths of group
+    g+1); then a call with a different geometry reuses (and regrows) the sets."""
+    import torch
+
+    eng.set_debug_flags(flags)
+    try:
+        for (H, W, D, n) in [(70, 260, 64, 7), (90, 330, 128, 5)]:
+            pairs = [synthetic.random_dot_pair(H, W, D, seed=100 + s)[:2] for s in range(n)]
+            L = torch.tensor(np.stack([a for a, _ in pairs]), device="cuda")
+            R = torch.tensor(np.stack([b for _, b in pairs]), device="cuda")
+            out = torch.full((n, H, W), 12345, dtype=torch.int16, device="cuda")
+            for p in (synthetic.headline_params(D), synthetic.parity_params(D)):
+                eng.set_stream(torch.cuda.current_stream().cuda_stream)
+                eng.compute_batch_device(L.data_ptr(), R.data_ptr(), n, H * W, H, W, W,
+                                         synthetic.to_sm_params(p), out.data_ptr())
+                got = out.cpu().numpy()  # same stream: ordered after both internal streams
+                eng.set_stream(None)
+                for i, (a, b) in enumerate(pairs):
+                    assert np.array_equal(got[i], ref_c.compute(a, b, p)), (H, W, D, i, p.get("cost"))
+    finally:
+        eng.set_debug_flags(0)
 
 
 def test_torch_tensor_interface():
