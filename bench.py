@@ -33,20 +33,26 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="kitti", choices=["kitti", "middlebury", "tsukuba", "mccnn"])
-    ap.add_argument("--mode", default="census8", choices=["census8", "sgbm5"])
+    ap.add_argument("--config", default=None, choices=["kitti", "middlebury", "tsukuba", "mccnn"],
+                    help="default: kitti (mccnn for --mode volume8)")
+    ap.add_argument("--mode", default="census8", choices=["census8", "sgbm5", "volume8"],
+                    help="census8 = headline; sgbm5 = OpenCV parity mode; volume8 = mc-cnn f32 cost volume")
     ap.add_argument("--pairs-per-gpu", type=int, default=8)
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--row", action="store_true",
                     help="experimental fused row kernel (E/W paths + WTA) instead of k_wta (D %% 64 == 0)")
     ap.add_argument("--cpu-baseline-pairs", type=int, default=8,
-                    help="KITTI pairs timed on the host C port (rank 0, N=1 only); 0 = skip")
+                    help="pairs timed on the host C port per thread (rank 0, N=1 only); 0 = skip")
+    ap.add_argument("--cpu-threads", type=int, default=16,
+                    help="host threads for the multi-core CPU baseline (the box's CPU share is 16)")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
     return ap.parse_args()
 
 
 def main():
     args = parse()
+    if args.config is None:
+        args.config = "mccnn" if args.mode == "volume8" else "kitti"
     import torch
     import torch.distributed as dist
 
@@ -63,7 +69,13 @@ def main():
     torch.cuda.set_device(dev)
 
     H, W, D = synthetic.CONFIGS[args.config]
-    p = synthetic.headline_params(D) if args.mode == "census8" else synthetic.parity_params(D)
+    volume = args.mode == "volume8"
+    if args.mode == "census8":
+        p = synthetic.headline_params(D)
+    elif volume:
+        p = synthetic.cost_volume_params(D)
+    else:
+        p = synthetic.parity_params(D)
     prm = synthetic.to_sm_params(p)
     P = args.pairs_per_gpu
     gpairs = P * world
@@ -77,6 +89,11 @@ def main():
     dL = torch.tensor(np.stack(lefts), device=dev)
     dR = torch.tensor(np.stack(rights), device=dev)
     dOut = torch.empty((P, H, W), dtype=torch.int16, device=dev)
+    vols = None
+    if volume:  # config C: (1, D, H, W) float32 cost per pair, resident in HBM
+        vols = torch.empty((P, D, H, W), dtype=torch.float32, device=dev)
+        for i in range(P):
+            vols[i].copy_(torch.from_numpy(synthetic.absdiff_volume(lefts[i], rights[i], D)[0]))
 
     eng = _lib.Engine(local_rank)
     stream = torch.cuda.current_stream(dev)
@@ -85,7 +102,11 @@ def main():
         eng.set_debug_flags(32)
 
     def step():
-        eng.compute_batch_device(dL.data_ptr(), dR.data_ptr(), P, H * W, H, W, W, prm, dOut.data_ptr())
+        if volume:
+            eng.aggregate_cost_f32_device(vols.data_ptr(), P, D * H * W, D, H, W, prm, 0.0, synthetic.VOLUME_SCALE,
+                                          dOut.data_ptr())
+        else:
+            eng.compute_batch_device(dL.data_ptr(), dR.data_ptr(), P, H * W, H, W, W, prm, dOut.data_ptr())
         if world > 1 and not args.no_gather:
             gather_to_root(dOut, gpairs)
 
@@ -127,7 +148,7 @@ def main():
         cells = H * W * D
         width1 = W - D
         vol = H * width1 * D
-        P_dirs = 8 if args.mode == "census8" else 5
+        P_dirs = 5 if args.mode == "sgbm5" else 8
         eb = 1 if args.mode == "census8" else 2  # bytes per path element
         row_mode = args.row and D % 64 == 0  # both horizontal paths fused into the row/WTA kernel
         census_b = 2 * H * W * 8 if args.mode == "census8" else 0
@@ -160,7 +181,11 @@ def main():
             except (OSError, ValueError):
                 traffic = None
         # SURVEY.md §8(d) whole-pipeline model: H·W·D·(1+P+4) + 2HW + 4HW per pair
-        survey_bytes = cells * (1 + P_dirs + 4) + 2 * H * W + 4 * H * W
+        # (mc-cnn f32 volume: H·W·D·(4·P + 8))
+        if volume:
+            survey_bytes = cells * (4 * P_dirs + 8)
+        else:
+            survey_bytes = cells * (1 + P_dirs + 4) + 2 * H * W + 4 * H * W
         tot_ms, _, tot_pairs = stages["total"]
         pair_s = tot_ms / 1e3 / max(tot_pairs, 1)
         line = {
@@ -174,11 +199,13 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "u8" if args.mode == "census8" else "i16",
-            "data": "synthetic random-dot pairs (no dataset in the image)",
+            "dtype": {"census8": "u8", "sgbm5": "i16", "volume8": "f32->u16"}[args.mode],
+            "data": "synthetic random-dot pairs (no dataset in the image)"
+                    + ("; f32 cost = 3x3-smoothed |L-R|/255 volume per pair" if volume else ""),
             "config": {
                 "workload": f"{args.config} {W}x{H} D={D} "
-                            + ("census9x7 + 8-path SGM" if args.mode == "census8" else "OpenCV-SGBM 5-path"),
+                            + {"census8": "census9x7 + 8-path SGM", "sgbm5": "OpenCV-SGBM 5-path",
+                               "volume8": "f32 cost volume (mc-cnn) + 8-path SGM"}[args.mode],
                 "pairs_per_gpu": P, "global_batch": gpairs, "H": H, "W": W, "D": D,
                 "gather": world > 1 and not args.no_gather, "parallelism": f"pairs/dp{world}",
             },
@@ -196,7 +223,7 @@ def main():
                 "avg_launch_us": paths_avg_s * 1e6,
             },
             "pipeline_roofline": {
-                "model": "SURVEY §8d H·W·D·(1+P+4)+I/O per pair",
+                "model": "SURVEY §8d " + ("H·W·D·(4P+8)" if volume else "H·W·D·(1+P+4)+I/O") + " per pair",
                 "bytes_per_pair": survey_bytes,
                 "device_us_per_pair": pair_s * 1e6,
                 "achieved_GBs": survey_bytes / pair_s / 1e9 if pair_s > 0 else None,
@@ -206,32 +233,64 @@ def main():
             "valid_frac_pair0": valid_frac,
         }
         if world == 1 and args.cpu_baseline_pairs > 0:
-            line["cpu_baseline"] = cpu_baseline(args, H, W, D, p, lefts, rights, out0)
+            line["cpu_baseline"] = cpu_baseline(args, H, W, D, p, lefts, rights, out0, volume)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
-def cpu_baseline(args, H, W, D, p, lefts, rights, out0):
-    """The C restatement (oracle/sgm_ref.c, -O3, one thread) on a bounded
-    sample of the same workload; also re-checks pair 0 bit for bit."""
+def cpu_baseline(args, H, W, D, p, lefts, rights, out0, volume):
+    """The C restatement (oracle/sgm_ref.c, -O3) on a bounded sample of the
+    same workload: ``--cpu-threads`` host threads each running
+    ``--cpu-baseline-pairs`` pairs concurrently (ctypes releases the GIL; the
+    port is single-threaded per pair, the pairs are independent), plus the
+    one-thread rate.  Also re-checks pair 0 bit for bit."""
+    import threading
+
     from oracle import ref_c
+    from stereo_match_amd import synthetic
 
     n = args.cpu_baseline_pairs
+    T = max(1, args.cpu_threads)
+    if volume:
+        n = max(1, n // 4)  # ~4x the work per pair (D=192, u16 volume, cost quantisation)
+        vol0 = synthetic.absdiff_volume(lefts[0], rights[0], D)[0]
+
+        def one(i):
+            return ref_c.compute_volume(vol0, p, 0.0, synthetic.VOLUME_SCALE)
+    else:
+        def one(i):
+            return ref_c.compute(lefts[i % len(lefts)], rights[i % len(rights)], p)
+    ref_c.load()
+    # one thread
+    n1 = max(1, n // 2)
     t0 = time.perf_counter()
-    first = None
-    for i in range(n):
-        o = ref_c.compute(lefts[i % len(lefts)], rights[i % len(rights)], p)
-        if i == 0:
-            first = o
-    dt = time.perf_counter() - t0
+    first = one(0)
+    for i in range(1, n1):
+        one(i)
+    dt1 = time.perf_counter() - t0
+
+    def worker(k):
+        for i in range(n):
+            one(k * n + i)
+
+    threads = [threading.Thread(target=worker, args=(k,)) for k in range(T)]
+    t0 = time.perf_counter()
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    dtT = time.perf_counter() - t0
+    what = "f32 cost volumes" if volume else "pairs"
     return {
-        "value": n / dt,
+        "value": T * n / dtT,
         "unit": "pairs/s",
-        "cores": 1,
+        "cores": T,
         "kind": "port",
-        "sample": f"{n} {W}x{H} D={D} pairs, oracle/sgm_ref.c single-threaded, {dt:.1f} s",
-        "mpix_disp_per_s": n * H * W * D / dt / 1e6,
+        "sample": f"{T} threads x {n} {W}x{H} D={D} {what}, oracle/sgm_ref.c -O3 (one pair per thread at a "
+                  f"time), {dtT:.1f} s wall",
+        "single_thread": {"value": n1 / dt1, "unit": "pairs/s", "cores": 1, "sample": f"{n1} {what}, {dt1:.1f} s"},
+        "mpix_disp_per_s": T * n * H * W * D / dtT / 1e6,
         "host_cpus_visible": os.cpu_count(),
         "gpu_matches_port_pair0": bool(np.array_equal(first, out0)),
     }

@@ -33,6 +33,7 @@ extern "C" {
 
 #define SM_COST_SGBM 0   /* OpenCV StereoSGBM cost: BT(Sobel-x clip) + BT(raw)>>2, blockSize^2 box */
 #define SM_COST_CENSUS 1 /* north-star cost: 9x7 census + Hamming (no reference counterpart) */
+#define SM_COST_VOLUME 2 /* external float32 cost volume (mc-cnn), set by sm_aggregate_cost_f32* */
 
 #define SM_MODE_SGBM 5 /* cv2.STEREO_SGBM_MODE_SGBM: 5 paths (reference default) */
 #define SM_MODE_HH 8   /* cv2.STEREO_SGBM_MODE_HH: 8 paths */
@@ -87,6 +88,22 @@ int sm_compute_batch_device(sm_ctx* ctx, const uint8_t* d_left, const uint8_t* d
                             size_t pair_stride_bytes, int H, int W, int stride, const sm_params* p,
                             int16_t* d_disp_out);
 
+/* SGM over an external matching-cost volume (mc-cnn; the reference memmaps
+ * one as float32 (1, D, H, W) at mapTo3D_mc_cnn.py:71 and feeds its
+ * disparities to the WLS filter, :81-100).  cost: float32 [D][H][W], d-major,
+ * plane d = cost of left x against right x - (min_disparity + d); D must equal
+ * p->num_disparities.  Costs are quantised q = rint((c + offset) * scale)
+ * (float32), clamped to [0, 4095], NaN -> 4095, then aggregated with the
+ * path recurrence / WTA / uniqueness / sub-pixel / LR / median of
+ * sm_compute (p->mode paths; block_size and pre_filter_cap unused;
+ * P2 <= 12288).  Output as sm_compute.  Host version is synchronous. */
+int sm_aggregate_cost_f32(sm_ctx* ctx, const float* cost, int D, int H, int W, const sm_params* p, float offset,
+                          float scale, int16_t* disp_out);
+/* Batch on device pointers: pair i's volume at d_cost + i*pair_stride_elems
+ * (elements, >= D*H*W), output d_disp_out + i*H*W.  Asynchronous. */
+int sm_aggregate_cost_f32_device(sm_ctx* ctx, const float* d_cost, int npairs, size_t pair_stride_elems, int D,
+                                 int H, int W, const sm_params* p, float offset, float scale, int16_t* d_disp_out);
+
 /* ximgproc::createRightMatcher(StereoSGBM) parameter derivation
  * (reference call: stereo_vision/stereo_vision.py:171). */
 int sm_right_matcher_params(const sm_params* left, sm_params* right_out);
@@ -108,7 +125,7 @@ int sm_get_timing(sm_ctx* ctx, int stage, double* total_ms, long long* launches,
 int sm_reset_timing(sm_ctx* ctx);
 
 /* Debug / parity: copy an intermediate of the LAST pair computed to host.
- * what: 0 cost volume C[H][width1][D] (uint8 census / uint16 SGBM),
+ * what: 0 cost volume C[H][width1][D] (uint8 census / uint16 SGBM, volume),
  *       1 path volumes L[P][H][width1][D] (uint8 census / uint16 SGBM),
  *         direction order E, W, SE, S, SW, NE, N, NW,
  *       2 pre-median disparity int16[H][W],

@@ -32,13 +32,16 @@ def build():
 def load():
     global _lib
     if _lib is None:
-        if not os.path.exists(_LIB):
-            build()
+        build()  # make: no-op when libsgm_ref.so is up to date
         lib = ctypes.CDLL(_LIB)
         lib.sgm_ref_compute.restype = ctypes.c_int
         lib.sgm_ref_compute.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                         ctypes.c_int, ctypes.POINTER(SgmRefParams), ctypes.c_void_p,
                                         ctypes.c_int]
+        lib.sgm_ref_compute_volume.restype = ctypes.c_int
+        lib.sgm_ref_compute_volume.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                               ctypes.POINTER(SgmRefParams), ctypes.c_float, ctypes.c_float,
+                                               ctypes.c_void_p, ctypes.c_int]
         lib.sgm_ref_census9x7.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                           ctypes.c_void_p]
         lib.sgm_ref_median3.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
@@ -66,6 +69,25 @@ def compute(left: np.ndarray, right: np.ndarray, params: dict, median: bool = Tr
                              out.ctypes.data, int(bool(median)))
     if rc != 0:
         raise ValueError(f"sgm_ref_compute failed ({rc})")
+    return out
+
+
+def compute_volume(vol: np.ndarray, params: dict, offset: float = 0.0, scale: float = 1.0,
+                   median: bool = True) -> np.ndarray:
+    """SGM over a d-major float32 cost volume [D][H][W] (or [1][D][H][W])."""
+    lib = load()
+    v = np.ascontiguousarray(vol, np.float32)
+    if v.ndim == 4:
+        v = v[0]
+    D, H, W = v.shape
+    if D != int(params.get("numDisparities", 16)):
+        raise ValueError("volume planes != numDisparities")
+    out = np.empty((H, W), np.int16)
+    prm = make_params(dict(params, cost=2))
+    rc = lib.sgm_ref_compute_volume(v.ctypes.data, H, W, ctypes.byref(prm), float(offset), float(scale),
+                                    out.ctypes.data, int(bool(median)))
+    if rc != 0:
+        raise ValueError(f"sgm_ref_compute_volume failed ({rc})")
     return out
 
 

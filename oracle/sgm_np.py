@@ -55,6 +55,8 @@ DIRS_8 = (DIR_E, DIR_SE, DIR_S, DIR_SW, DIR_W, DIR_N, DIR_NW, DIR_NE)
 
 COST_SGBM = 0
 COST_CENSUS = 1
+COST_VOLUME = 2  # external f32 cost volume (mc-cnn)
+VOLUME_CMAX = 4095  # quantised external costs live in [0, 4095]
 
 
 # --------------------------------------------------------------------------
@@ -241,6 +243,32 @@ def cost_volume(left, right, prm) -> np.ndarray:
     return box_cost_sgbm(pix, prm["bs"], prm["mode"])
 
 
+def quantize_volume(vol: np.ndarray, prm, offset: float, scale: float) -> np.ndarray:
+    """External matching cost (mc-cnn ``(1, D, H, W)`` / ``(D, H, W)`` float32,
+    d-major — the layout ``mapTo3D_mc_cnn.py:71`` memmaps) → C[y, x1, d].
+
+    Own definition (no reference arithmetic exists: the reference only loads
+    the volume): ``q = rint((c + offset) * scale)`` in float32 (two IEEE
+    roundings, round-half-even), clamped to [0, VOLUME_CMAX]; NaN → CMAX.
+    Volume plane d holds the cost of left pixel x against right pixel
+    x − (minD + d); columns follow the matcher geometry [minX1, maxX1)."""
+    v = np.asarray(vol, np.float32)
+    if v.ndim == 4:
+        v = v[0]
+    D = prm["D"]
+    if v.shape[0] != D:
+        raise ValueError("volume has %d planes, numDisparities is %d" % (v.shape[0], D))
+    H, W = v.shape[1:]
+    minX1, maxX1 = geometry(W, prm["minD"], D)
+    sub = v[:, :, minX1:maxX1]
+    with np.errstate(invalid="ignore", over="ignore"):
+        t = (sub + np.float32(offset)) * np.float32(scale)
+        q = np.rint(t)
+        q = np.where(np.isnan(q), np.float32(VOLUME_CMAX), q)
+        q = np.clip(q, 0, VOLUME_CMAX)
+    return q.astype(np.int64).transpose(1, 2, 0)
+
+
 # --------------------------------------------------------------------------
 # Path aggregation
 # --------------------------------------------------------------------------
@@ -403,6 +431,32 @@ def compute(left: np.ndarray, right: np.ndarray, params: dict, *, median=True,
         out = np.full((H, W), (prm["minD"] - 1) * DISP_SCALE, np.int16)
         return (out, {}) if return_stages else out
     C = cost_volume(left, right, prm)
+    S = aggregate(C, prm)
+    raw = wta(S, H, W, prm)
+    out = median3(raw) if median else raw
+    if prm["speckle_ws"] > 0:
+        out = filter_speckles(out, (prm["minD"] - 1) * DISP_SCALE, prm["speckle_ws"],
+                              DISP_SCALE * prm["speckle_range"])
+    if return_stages:
+        return out, dict(C=C, S=S, raw=raw)
+    return out
+
+
+def compute_volume(vol: np.ndarray, params: dict, offset: float = 0.0, scale: float = 1.0, *,
+                   median=True, return_stages=False):
+    """SGM over an external f32 cost volume (mc-cnn): the
+    quantised cost (``quantize_volume``) feeds the same path recurrence,
+    WTA / uniqueness / sub-pixel / LR and 3×3 median as ``compute``."""
+    prm = normalize_params(dict(params, cost=COST_VOLUME))
+    v = np.asarray(vol, np.float32)
+    H, W = v.shape[-2:]
+    if prm["P2"] > 16383 - VOLUME_CMAX:
+        raise ValueError("volume mode needs P2 <= %d" % (16383 - VOLUME_CMAX))
+    minX1, maxX1 = geometry(W, prm["minD"], prm["D"])
+    if minX1 >= maxX1:
+        out = np.full((H, W), (prm["minD"] - 1) * DISP_SCALE, np.int16)
+        return (out, {}) if return_stages else out
+    C = quantize_volume(v, prm, offset, scale)
     S = aggregate(C, prm)
     raw = wta(S, H, W, prm)
     out = median3(raw) if median else raw

@@ -25,6 +25,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <math.h>
 
 typedef int16_t CostType;
 #define MAX_COST 32767
@@ -187,10 +188,24 @@ void sgm_ref_filter_speckles(int16_t* img, int H, int W, int newVal, int maxSpec
 /* -------------------------------------------------- computeDisparitySGBM */
 #define NR2 4
 
-int sgm_ref_compute(const uint8_t* img1, const uint8_t* img2, int H, int W, int stride,
-                    const sgm_ref_params* prm, int16_t* disp1, int apply_median)
+/* External f32 cost (mc-cnn volume, own definition — see sgm_np.quantize_volume):
+ * q = rint((c + offset) * scale) in float32, clamped to [0, 4095], NaN -> 4095. */
+#define VOLUME_CMAX 4095
+static inline int quant_cost(float c, float offset, float scale)
 {
-    if (!img1 || !img2 || !disp1 || !prm || H <= 0 || W <= 0 || stride < W) return -1;
+    if (c != c) return VOLUME_CMAX;
+    float t = (c + offset) * scale;
+    float v = rintf(t);
+    if (!(v > 0.f)) return 0;
+    if (v > (float)VOLUME_CMAX) return VOLUME_CMAX;
+    return (int)v;
+}
+
+static int compute_core(const uint8_t* img1, const uint8_t* img2, int H, int W, int stride, const float* vol,
+                        float vol_offset, float vol_scale, const sgm_ref_params* prm, int16_t* disp1,
+                        int apply_median)
+{
+    if ((!vol && (!img1 || !img2 || stride < W)) || !disp1 || !prm || H <= 0 || W <= 0) return -1;
     int minD = prm->min_disparity, D = prm->num_disparities, maxD = minD + D;
     if (D <= 0 || D % 16) return -1;
     int bs = prm->block_size > 0 ? prm->block_size : 5;
@@ -200,6 +215,7 @@ int sgm_ref_compute(const uint8_t* img1, const uint8_t* img2, int H, int W, int 
     int P1 = prm->P1 > 0 ? prm->P1 : 2;
     int P2 = imax(prm->P2 > 0 ? prm->P2 : 5, P1 + 1);
     int census = prm->cost_kind == 1;
+    if (vol && P2 > 16383 - VOLUME_CMAX) return -1;
     int minX1 = imax(maxD, 0), maxX1 = W + imin(minD, 0), width1 = maxX1 - minX1;
     int INVALID = (minD - 1) * DISP_SCALE;
     int SW2 = bs / 2, SH2 = bs / 2;
@@ -260,7 +276,12 @@ int sgm_ref_compute(const uint8_t* img1, const uint8_t* img2, int H, int W, int 
                 CostType* C = Cbuf + (fullDP ? (size_t)y * costBufSize : 0);
                 CostType* S = Sbuf + (fullDP ? (size_t)y * costBufSize : 0);
                 if (pass == 1) {
-                    if (census) {
+                    if (vol) {
+                        for (int x = 0; x < width1; x++)
+                            for (int d = 0; d < D; d++)
+                                C[(size_t)x * D + d] = (CostType)(
+                                    P2 + quant_cost(vol[((size_t)d * H + y) * W + x + minX1], vol_offset, vol_scale));
+                    } else if (census) {
                         const uint64_t* l = cl + (size_t)y * W;
                         const uint64_t* r = cr + (size_t)y * W;
                         for (int x = 0; x < width1; x++)
@@ -432,4 +453,18 @@ done:
         sgm_ref_filter_speckles(disp1, H, W, INVALID, prm->speckle_window_size,
                                 DISP_SCALE * prm->speckle_range);
     return 0;
+}
+
+int sgm_ref_compute(const uint8_t* img1, const uint8_t* img2, int H, int W, int stride,
+                    const sgm_ref_params* prm, int16_t* disp1, int apply_median)
+{
+    return compute_core(img1, img2, H, W, stride, NULL, 0.f, 1.f, prm, disp1, apply_median);
+}
+
+/* SGM over an external d-major float32 cost volume vol[D][H][W] (mc-cnn). */
+int sgm_ref_compute_volume(const float* vol, int H, int W, const sgm_ref_params* prm, float offset, float scale,
+                           int16_t* disp1, int apply_median)
+{
+    if (!vol) return -1;
+    return compute_core(NULL, NULL, H, W, W, vol, offset, scale, prm, disp1, apply_median);
 }

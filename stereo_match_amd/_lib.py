@@ -18,7 +18,7 @@ LIB_PATH = os.path.join(_HERE, "libstereo_match_amd.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "stereo_match_amd.h")
 
 SM_OK, SM_E_ARG, SM_E_HIP, SM_E_UNSUPPORTED = 0, -1, -2, -4
-SM_COST_SGBM, SM_COST_CENSUS = 0, 1
+SM_COST_SGBM, SM_COST_CENSUS, SM_COST_VOLUME = 0, 1, 2
 SM_MODE_SGBM, SM_MODE_HH = 5, 8
 STAGES = ("cost", "paths", "wta", "median", "total")
 
@@ -47,6 +47,11 @@ _SIGS = {
                                      _c.POINTER(SmParams), _c.c_void_p]),
     "sm_compute_batch_device": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_int, _c.c_size_t,
                                            _c.c_int, _c.c_int, _c.c_int, _c.POINTER(SmParams), _c.c_void_p]),
+    "sm_aggregate_cost_f32": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_int, _c.c_int, _c.c_int,
+                                         _c.POINTER(SmParams), _c.c_float, _c.c_float, _c.c_void_p]),
+    "sm_aggregate_cost_f32_device": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_int, _c.c_size_t, _c.c_int,
+                                                _c.c_int, _c.c_int, _c.POINTER(SmParams), _c.c_float,
+                                                _c.c_float, _c.c_void_p]),
     "sm_right_matcher_params": (_c.c_int, [_c.POINTER(SmParams), _c.POINTER(SmParams)]),
     "sm_synchronize": (_c.c_int, [_c.c_void_p]),
     "sm_set_timing": (_c.c_int, [_c.c_void_p, _c.c_int]),
@@ -163,6 +168,29 @@ class Engine:
         self._check(self._lib.sm_compute_batch_device(
             self.ctx, ctypes.c_void_p(d_left), ctypes.c_void_p(d_right), npairs, pair_stride, H, W, stride,
             ctypes.byref(params), ctypes.c_void_p(d_out)))
+
+    # -- external cost volume (mc-cnn) ----------------------------------------
+    def aggregate_cost_f32(self, vol: np.ndarray, params: SmParams, offset: float = 0.0,
+                           scale: float = 1.0) -> np.ndarray:
+        """SGM over a float32 d-major cost volume [D][H][W] (or [1][D][H][W])."""
+        v = np.ascontiguousarray(vol, np.float32)
+        if v.ndim == 4:
+            if v.shape[0] != 1:
+                raise ValueError("expected a (1, D, H, W) volume")
+            v = v[0]
+        if v.ndim != 3:
+            raise ValueError("expected a (D, H, W) float32 volume")
+        D, H, W = v.shape
+        out = np.empty((H, W), np.int16)
+        self._check(self._lib.sm_aggregate_cost_f32(self.ctx, v.ctypes.data, D, H, W, ctypes.byref(params),
+                                                    float(offset), float(scale), out.ctypes.data))
+        return out
+
+    def aggregate_cost_f32_device(self, d_cost: int, npairs: int, pair_stride_elems: int, D: int, H: int,
+                                  W: int, params: SmParams, offset: float, scale: float, d_out: int):
+        self._check(self._lib.sm_aggregate_cost_f32_device(
+            self.ctx, ctypes.c_void_p(d_cost), npairs, pair_stride_elems, D, H, W, ctypes.byref(params),
+            float(offset), float(scale), ctypes.c_void_p(d_out)))
 
     def synchronize(self):
         self._check(self._lib.sm_synchronize(self.ctx))

@@ -67,7 +67,7 @@ struct sm_ctx {
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;  // stream A
     hipStream_t side = nullptr;    // stream B
-    DevBuf img[2], planes, out, dbg;
+    DevBuf img[2], planes, out, dbg, volbuf;
     BufSet set[2];
     int next_set = 0;
     // geometry of the last computation (for sm_debug_fetch): its last pair
@@ -143,7 +143,7 @@ int normalize(sm_ctx* ctx, const sm_params* p, int H, int W, Norm& n)
     n.speckle_range = p->speckle_range;
     n.cost = p->cost_kind;
     n.mode = p->mode;
-    if (n.cost != SM_COST_SGBM && n.cost != SM_COST_CENSUS)
+    if (n.cost != SM_COST_SGBM && n.cost != SM_COST_CENSUS && n.cost != SM_COST_VOLUME)
         return fail(ctx, SM_E_ARG, "cost_kind %d unknown", n.cost);
     if (n.mode != SM_MODE_SGBM && n.mode != SM_MODE_HH)
         return fail(ctx, SM_E_UNSUPPORTED, "mode %d not supported (5 = MODE_SGBM, 8 = MODE_HH)", n.mode);
@@ -156,8 +156,11 @@ int normalize(sm_ctx* ctx, const sm_params* p, int H, int W, Norm& n)
             return fail(ctx, SM_E_UNSUPPORTED,
                         "blockSize=%d/preFilterCap/P2=%d outside the int16-exact range (bs^2*(2*ftzero+63)+P2 <= 16383)",
                         n.bs, n.P2);
-    } else {
+    } else if (n.cost == SM_COST_CENSUS) {
         if (62 + n.P2 > 255) return fail(ctx, SM_E_UNSUPPORTED, "census mode needs P2 <= 193 (8-bit path values)");
+    } else {
+        if (smk::VOL_CMAX + n.P2 > 16383)
+            return fail(ctx, SM_E_UNSUPPORTED, "cost-volume mode needs P2 <= %d", 16383 - smk::VOL_CMAX);
     }
     if (n.P1 > 16383 || n.P2 > 16383) return fail(ctx, SM_E_UNSUPPORTED, "P1/P2 too large");
     n.minX1 = std::max(n.maxD, 0);
@@ -223,7 +226,7 @@ int grid_for(size_t n)
     return (int)std::min<size_t>(std::max<size_t>(g, 1), 8192);
 }
 
-size_t elem_bytes(const Norm& n) { return n.cost == SM_COST_CENSUS ? 1 : 2; }
+size_t elem_bytes(const Norm& n) { return n.cost == SM_COST_CENSUS ? 1 : 2; }  // path values: u8 census, else u16
 
 // Output slots: 0 E, 1 W (horizontal family), 2 SE, 3 S, 4 SW (MODE_SGBM adds
 // these three), 5 NE, 6 N, 7 NW (MODE_HH / 8-path adds these three).
@@ -232,6 +235,23 @@ const int kVdy[6] = {1, 1, 1, -1, -1, -1};
 
 constexpr size_t kSetBudget = size_t(12) << 30;  // bytes of path volumes per buffer set
 constexpr int kMaxGroup = 16;
+
+struct Src {  // where a launch group's pairs come from (device pointers)
+    const uint8_t* L = nullptr;  // census / SGBM: images, pair i at L + i*pair_stride
+    const uint8_t* R = nullptr;
+    size_t pair_stride = 0;
+    const float* vol = nullptr;  // external cost: vol + i*vol_pair, [D][H][W] float32
+    size_t vol_pair = 0;
+    float offset = 0.f, scale = 1.f;
+    Src advance(int i) const
+    {
+        Src s = *this;
+        if (L) s.L += (size_t)i * pair_stride;
+        if (R) s.R += (size_t)i * pair_stride;
+        if (vol) s.vol += (size_t)i * vol_pair;
+        return s;
+    }
+};
 
 struct Geo {  // per-group geometry shared by the launches
     int H, W, stride, G;
@@ -391,9 +411,10 @@ int ensure_event(sm_ctx* ctx, hipEvent_t& e)
 }
 
 // G pairs (device pointers; pair i at dL + i*pair_stride).
-int run_group(sm_ctx* ctx, const uint8_t* dL, const uint8_t* dR, size_t pair_stride, const Geo& g, const Norm& n,
-              int16_t* d_out)
+int run_group(sm_ctx* ctx, const Src& src, const Geo& g, const Norm& n, int16_t* d_out)
 {
+    const uint8_t *dL = src.L, *dR = src.R;
+    const size_t pair_stride = src.pair_stride;
     const int H = g.H, W = g.W, G = g.G;
     const int s = overlap(ctx) ? ctx->next_set : 0;  // one buffer set unless overlapping
     ctx->next_set = s ^ 1;
@@ -433,6 +454,24 @@ int run_group(sm_ctx* ctx, const uint8_t* dL, const uint8_t* dR, size_t pair_str
             hipLaunchKernelGGL(smk::k_census9x7,
                                dim3((W + smk::CT_W - 1) / smk::CT_W, (H + smk::CT_H - 1) / smk::CT_H, 2 * G),
                                dim3(256), 0, ctx->stream, ca);
+            HIP_TRY(ctx, hipGetLastError());
+        } else if (n.cost == SM_COST_VOLUME) {
+            if ((rc = ensure(ctx, bs.cost, (size_t)G * g.vol * 2)) != SM_OK) return rc;
+            smk::VolArgs va{};
+            va.vol = src.vol;
+            va.vol_pair = src.vol_pair;
+            va.C = (uint16_t*)bs.cost.p;
+            va.C_pair = g.vol;
+            va.H = H;
+            va.W = W;
+            va.width1 = n.width1;
+            va.D = n.D;
+            va.minX1 = n.minX1;
+            va.offset = src.offset;
+            va.scale = src.scale;
+            const size_t smem = (size_t)smk::VT_X * (n.D / 2 + 1) * 4;
+            hipLaunchKernelGGL(smk::k_cost_volume_f32, dim3((n.width1 + smk::VT_X - 1) / smk::VT_X, H, G), dim3(256),
+                               smem, ctx->stream, va);
             HIP_TRY(ctx, hipGetLastError());
         } else {
             if ((rc = ensure(ctx, ctx->planes, (size_t)H * W * 12)) != SM_OK) return rc;
@@ -498,8 +537,7 @@ int run_group(sm_ctx* ctx, const uint8_t* dL, const uint8_t* dR, size_t pair_str
     return SM_OK;
 }
 
-int run_pairs(sm_ctx* ctx, const uint8_t* dL, const uint8_t* dR, size_t pair_stride, int npairs, int H, int W,
-              int stride, const Norm& n, int16_t* d_out)
+int run_pairs(sm_ctx* ctx, const Src& src, int npairs, int H, int W, int stride, const Norm& n, int16_t* d_out)
 {
     ctx->lastH = H;
     ctx->lastW = W;
@@ -523,8 +561,7 @@ int run_pairs(sm_ctx* ctx, const uint8_t* dL, const uint8_t* dR, size_t pair_str
         StageTimer total(ctx, ctx->stream, SM_STAGE_TOTAL, npairs);
         for (int i = 0; i < npairs && rc == SM_OK; i += G) {
             g.G = std::min(G, npairs - i);
-            rc = run_group(ctx, dL + (size_t)i * pair_stride, dR + (size_t)i * pair_stride, pair_stride, g, n,
-                           d_out + (size_t)i * H * W);
+            rc = run_group(ctx, src.advance(i), g, n, d_out + (size_t)i * H * W);
         }
         // join stream B back into the caller's stream
         for (auto& bs : ctx->set)
@@ -569,7 +606,7 @@ void sm_destroy(sm_ctx* ctx)
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     (void)hipDeviceSynchronize();
-    DevBuf* bufs[] = {&ctx->img[0], &ctx->img[1], &ctx->planes, &ctx->out, &ctx->dbg};
+    DevBuf* bufs[] = {&ctx->img[0], &ctx->img[1], &ctx->planes, &ctx->out, &ctx->dbg, &ctx->volbuf};
     for (DevBuf* b : bufs)
         if (b->p) (void)hipFree(b->p);
     for (auto& bs : ctx->set) {
@@ -624,7 +661,10 @@ int sm_compute_device(sm_ctx* ctx, const uint8_t* dL, const uint8_t* dR, int H, 
     int rc = normalize(ctx, p, H, W, n);
     if (rc != SM_OK) return rc;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    return run_pairs(ctx, dL, dR, 0, 1, H, W, stride, n, d_out);
+    Src src;
+    src.L = dL;
+    src.R = dR;
+    return run_pairs(ctx, src, 1, H, W, stride, n, d_out);
 }
 
 int sm_compute_batch_device(sm_ctx* ctx, const uint8_t* dL, const uint8_t* dR, int npairs, size_t pair_stride,
@@ -638,7 +678,11 @@ int sm_compute_batch_device(sm_ctx* ctx, const uint8_t* dL, const uint8_t* dR, i
     int rc = normalize(ctx, p, H, W, n);
     if (rc != SM_OK) return rc;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    return run_pairs(ctx, dL, dR, pair_stride, npairs, H, W, stride, n, d_out);
+    Src src;
+    src.L = dL;
+    src.R = dR;
+    src.pair_stride = pair_stride;
+    return run_pairs(ctx, src, npairs, H, W, stride, n, d_out);
 }
 
 int sm_compute(sm_ctx* ctx, const uint8_t* L, const uint8_t* R, int H, int W, int stride, const sm_params* p,
@@ -657,8 +701,53 @@ int sm_compute(sm_ctx* ctx, const uint8_t* L, const uint8_t* R, int H, int W, in
     if ((rc = ensure(ctx, ctx->out, img * 2)) != SM_OK) return rc;
     HIP_TRY(ctx, hipMemcpy2DAsync(ctx->img[0].p, W, L, stride, W, H, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipMemcpy2DAsync(ctx->img[1].p, W, R, stride, W, H, hipMemcpyHostToDevice, ctx->stream));
-    rc = run_pairs(ctx, (const uint8_t*)ctx->img[0].p, (const uint8_t*)ctx->img[1].p, 0, 1, H, W, W, n,
-                   (int16_t*)ctx->out.p);
+    Src src;
+    src.L = (const uint8_t*)ctx->img[0].p;
+    src.R = (const uint8_t*)ctx->img[1].p;
+    rc = run_pairs(ctx, src, 1, H, W, W, n, (int16_t*)ctx->out.p);
+    if (rc != SM_OK) return rc;
+    HIP_TRY(ctx, hipMemcpyAsync(disp_out, ctx->out.p, img * 2, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return SM_OK;
+}
+
+int sm_aggregate_cost_f32_device(sm_ctx* ctx, const float* d_cost, int npairs, size_t pair_stride_elems, int D,
+                                 int H, int W, const sm_params* p, float offset, float scale, int16_t* d_out)
+{
+    if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
+    if (npairs < 0) return fail(ctx, SM_E_ARG, "npairs < 0");
+    if (!d_cost || !d_out || !p) return fail(ctx, SM_E_ARG, "NULL cost/output/params pointer");
+    if (D != p->num_disparities)
+        return fail(ctx, SM_E_ARG, "cost volume has %d planes but numDisparities = %d", D, p->num_disparities);
+    if (npairs > 1 && pair_stride_elems < (size_t)D * H * W) return fail(ctx, SM_E_ARG, "pair stride too small");
+    sm_params q = *p;
+    q.cost_kind = SM_COST_VOLUME;
+    Norm n;
+    int rc = normalize(ctx, &q, H, W, n);
+    if (rc != SM_OK) return rc;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    Src src;
+    src.vol = d_cost;
+    src.vol_pair = pair_stride_elems;
+    src.offset = offset;
+    src.scale = scale;
+    return run_pairs(ctx, src, npairs, H, W, W, n, d_out);
+}
+
+int sm_aggregate_cost_f32(sm_ctx* ctx, const float* cost, int D, int H, int W, const sm_params* p, float offset,
+                          float scale, int16_t* disp_out)
+{
+    if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
+    if (!cost || !disp_out) return fail(ctx, SM_E_ARG, "NULL cost/output pointer");
+    if (H <= 0 || W <= 0 || D <= 0) return fail(ctx, SM_E_ARG, "empty volume (%dx%dx%d)", D, H, W);
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    const size_t img = (size_t)H * W;
+    int rc;
+    if ((rc = ensure(ctx, ctx->volbuf, img * D * 4)) != SM_OK) return rc;
+    if ((rc = ensure(ctx, ctx->out, img * 2)) != SM_OK) return rc;
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->volbuf.p, cost, img * D * 4, hipMemcpyHostToDevice, ctx->stream));
+    rc = sm_aggregate_cost_f32_device(ctx, (const float*)ctx->volbuf.p, 1, img * D, D, H, W, p, offset, scale,
+                                      (int16_t*)ctx->out.p);
     if (rc != SM_OK) return rc;
     HIP_TRY(ctx, hipMemcpyAsync(disp_out, ctx->out.p, img * 2, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));

@@ -261,4 +261,58 @@ __global__ void __launch_bounds__(256) k_sgbm_cost_tail(uint16_t* C, int H, int 
         dst[i] = hh ? make_uint4(0, 0, 0, 0) : src[i % per_row];
 }
 
+// ---------------------------------------------------------------------------
+// External float32 cost volume (mc-cnn; the reference memmaps
+// it at mapTo3D_mc_cnn.py:71) -> quantised u16 C[H][width1][D].
+// d-major [D][H][W] in, d-minor out: an LDS-tiled transpose, HBM-bound
+// (4 B read + 2 B written per cell).  q = rint((c + offset) * scale) in
+// float32 clamped to [0, VOL_CMAX], NaN -> VOL_CMAX (oracle:
+// sgm_np.quantize_volume).  (c + offset) * scale cannot be contracted into an
+// FMA, so the two IEEE roundings match the oracle's.
+constexpr int VOL_CMAX = 4095;
+constexpr int VT_X = 64;  // columns per tile
+
+struct VolArgs {
+    const float* vol;
+    size_t vol_pair;  // elements between pairs
+    uint16_t* C;
+    size_t C_pair;  // elements between pairs
+    int H, W, width1, D, minX1;
+    float offset, scale;
+};
+
+__device__ inline uint32_t quant_cost(float c, float off, float sc)
+{
+    if (c != c) return VOL_CMAX;
+    const float v = __builtin_rintf((c + off) * sc);
+    if (!(v > 0.f)) return 0;
+    if (v > (float)VOL_CMAX) return VOL_CMAX;
+    return (uint32_t)v;
+}
+
+__global__ void __launch_bounds__(256) k_cost_volume_f32(VolArgs a)
+{
+    extern __shared__ uint32_t tile[];  // [VT_X][D/2 + 1] packed u16 pairs (d even | d odd << 16)
+    const int half = a.D >> 1, rowdw = half + 1;
+    const int x0 = blockIdx.x * VT_X, y = blockIdx.y, pair = blockIdx.z;
+    const int nx = min(VT_X, a.width1 - x0);
+    const size_t plane = (size_t)a.H * a.W;
+    const float* v = a.vol + pair * a.vol_pair + (size_t)y * a.W + a.minX1 + x0;
+    for (int i = threadIdx.x; i < VT_X * half; i += 256) {
+        const int xl = i & (VT_X - 1), dp = i >> 6;
+        if (xl < nx) {
+            const float c0 = __builtin_nontemporal_load(v + (size_t)(2 * dp) * plane + xl);
+            const float c1 = __builtin_nontemporal_load(v + (size_t)(2 * dp + 1) * plane + xl);
+            tile[xl * rowdw + dp] = quant_cost(c0, a.offset, a.scale) | (quant_cost(c1, a.offset, a.scale) << 16);
+        }
+    }
+    __syncthreads();
+    uint32_t* out = reinterpret_cast<uint32_t*>(a.C + pair * a.C_pair + ((size_t)y * a.width1 + x0) * a.D);
+    const int total = nx * half;
+    for (int i = threadIdx.x; i < total; i += 256) {
+        const int xl = i / half, j = i - xl * half;
+        out[i] = tile[xl * rowdw + j];
+    }
+}
+
 }  // namespace smk

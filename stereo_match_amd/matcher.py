@@ -111,6 +111,39 @@ class StereoSGBM:
             return disparity
         return out
 
+    def computeFromCost(self, cost, offset: float = 0.0, scale: float = 1.0):
+        """SGM over an external matching-cost volume (mc-cnn).
+
+        ``cost``: float32 ``(1, D, H, W)`` or ``(D, H, W)``, d-major — the
+        memmap ``mapTo3D_mc_cnn.py:71`` opens (``np.memmap`` works as is) —
+        with ``D == numDisparities``; plane d is the cost of left x against
+        right x − (minDisparity + d).  Costs are quantised
+        ``rint((c + offset) * scale)`` to [0, 4095] (NaN → 4095), then the
+        same paths / WTA / LR / median as :meth:`compute` run (``mode`` picks
+        5 or 8 paths; ``blockSize``/``preFilterCap`` are unused).  numpy in →
+        int16 numpy out; a torch CUDA float32 tensor in → int16 CUDA tensor
+        (torch's current stream)."""
+        prm = self.params()
+        prm.cost_kind = _lib.SM_COST_VOLUME
+        if _is_torch_cuda(cost):
+            import torch
+
+            if cost.dtype != torch.float32:
+                raise ValueError("cost volume must be float32")
+            v = cost.contiguous()
+            if v.dim() == 4:
+                v = v[0]
+            D, H, W = v.shape
+            out = torch.empty((H, W), dtype=torch.int16, device=v.device)
+            eng = _lib.engine(v.device.index or 0)
+            eng.set_stream(torch.cuda.current_stream(v.device).cuda_stream)
+            eng.aggregate_cost_f32_device(v.data_ptr(), 1, D * H * W, D, H, W, prm, offset, scale, out.data_ptr())
+            return out
+        v = np.asarray(cost)
+        if v.dtype != np.float32:
+            raise ValueError("cost volume must be float32")
+        return _lib.engine(self.device).aggregate_cost_f32(v, prm, offset, scale)
+
 
 def _check_pair(left, right):
     if left.shape != right.shape or left.dtype != right.dtype:

@@ -75,6 +75,34 @@ def parity_params(D: int = 128, window_size: int = 5) -> dict:
                 speckleWindowSize=0, speckleRange=2, mode=5, cost=0)
 
 
+def cost_volume_params(D: int = 192) -> dict:
+    """mc-cnn volume mode (config C): 8 paths; P1/P2 in quantised cost units
+    (costs scaled by VOLUME_SCALE, so P1 ~ 0.05 and P2 ~ 0.5 of the [0,1] cost
+    range), uniqueness 15, disp12MaxDiff 1."""
+    return dict(minDisparity=0, numDisparities=D, blockSize=5, P1=200, P2=2000, disp12MaxDiff=1,
+                uniquenessRatio=15, preFilterCap=63, speckleWindowSize=0, speckleRange=2, mode=8, cost=2)
+
+
+VOLUME_SCALE = 4000.0  # [0,1] costs -> [0, 4000] of the 12-bit quantised range
+
+
+def absdiff_volume(left: np.ndarray, right: np.ndarray, D: int, minD: int = 0) -> np.ndarray:
+    """Config C stand-in for an mc-cnn output: float32 (1, D, H, W),
+    d-major, plane d = |L(x) − R(x − minD − d)| / 255 averaged over a 3×3
+    window; NaN where x − minD − d falls outside the right image (mc-cnn leaves
+    those undefined too)."""
+    L = _smooth3(left.astype(np.float64)).astype(np.float32)
+    R = _smooth3(right.astype(np.float64)).astype(np.float32)
+    H, W = left.shape
+    vol = np.full((1, D, H, W), np.nan, np.float32)
+    for d in range(D):
+        s = minD + d
+        lo, hi = max(s, 0), min(W, W + s)
+        if lo < hi:
+            vol[0, d, :, lo:hi] = np.abs(L[:, lo:hi] - R[:, lo - s:hi - s]) / np.float32(255.0)
+    return vol
+
+
 def to_sm_params(p: dict):
     """Oracle-style dict -> C-ABI SmParams (mode 5/8, cost 0/1)."""
     from ._lib import SmParams

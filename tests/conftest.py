@@ -24,8 +24,27 @@ def golden_cases():
 
     out = []
     for path in sorted(glob.glob(os.path.join(GOLDEN, "*.npz"))):
+        if os.path.basename(path).startswith("vol_"):
+            continue
         z = np.load(path, allow_pickle=False)
         out.append((os.path.basename(path)[:-4], z["left"], z["right"], json.loads(str(z["params"])),
                     z["expected"], z["raw"]))
     assert out, "no golden fixtures (run tests/golden/make_golden.py)"
+    return out
+
+
+@pytest.fixture(scope="session")
+def golden_volume_cases():
+    """(name, vol f32 [D,H,W], params, offset, scale, expected, raw) — mc-cnn mode."""
+    import glob
+    import json
+
+    import numpy as np
+
+    out = []
+    for path in sorted(glob.glob(os.path.join(GOLDEN, "vol_*.npz"))):
+        z = np.load(path, allow_pickle=False)
+        out.append((os.path.basename(path)[:-4], z["vol"], json.loads(str(z["params"])), float(z["offset"]),
+                    float(z["scale"]), z["expected"], z["raw"]))
+    assert out, "no volume fixtures (run tests/golden/make_golden.py)"
     return out

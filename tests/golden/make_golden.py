@@ -54,7 +54,33 @@ def cases():
     yield "sgbm5_one_row", l32[:1].copy(), r32[:1].copy(), synthetic.parity_params(16)
 
 
+def volume_cases():
+    """External f32 cost volumes (mc-cnn mode): vol_<name>.npz
+    holds ``vol`` float32 [D,H,W], ``params``, ``offset``, ``scale``,
+    ``expected`` and ``raw``."""
+    l16, r16, _ = synthetic.random_dot_pair(40, 90, 16, seed=11)
+    l32, r32, _ = synthetic.random_dot_pair(36, 100, 32, seed=12)
+    v16 = synthetic.absdiff_volume(l16, r16, 16)[0]
+    v32 = synthetic.absdiff_volume(l32, r32, 32)[0]
+    rng = np.random.default_rng(13)
+    vr = (rng.standard_normal((16, 30, 70)) * 0.5).astype(np.float32)
+    vr[rng.random(vr.shape) < 0.02] = np.nan
+    vr[0, 0, :4] = [np.inf, -np.inf, 0.5, 1.5]  # clamp, clamp, half-even ties
+    yield "vol_absdiff_d16_p8", v16, dict(synthetic.cost_volume_params(16)), 0.0, synthetic.VOLUME_SCALE
+    yield "vol_absdiff_d32_p5", v32, dict(synthetic.cost_volume_params(32), mode=5), 0.0, synthetic.VOLUME_SCALE
+    yield "vol_signed_nan_d16", vr, dict(synthetic.cost_volume_params(16), P1=3, P2=40), 1.0, 1.0
+    yield "vol_minD_neg3_d16", v16, dict(synthetic.cost_volume_params(16), minDisparity=-3), 0.0, 1000.0
+
+
 def main():
+    for name, vol, p, off, sc in volume_cases():
+        out, st = sgm_np.compute_volume(vol, p, off, sc, return_stages=True)
+        c = ref_c.compute_volume(vol, p, off, sc)
+        if not np.array_equal(out, c):
+            raise SystemExit(f"{name}: numpy and C restatements disagree")
+        np.savez_compressed(os.path.join(HERE, name + ".npz"), vol=vol, params=np.array(json.dumps(p)),
+                            offset=np.float32(off), scale=np.float32(sc), expected=out, raw=st["raw"])
+        print(f"{name}: {vol.shape} valid={np.mean(out > (p.get('minDisparity', 0) - 1) * 16):.3f}")
     for name, left, right, p in cases():
         out, st = sgm_np.compute(left, right, p, return_stages=True)
         raw = st.get("raw", out)

@@ -244,3 +244,88 @@ def test_timing_counters(eng):
     eng.set_timing(False)
     assert t["paths"][1] == 3 and t["total"][1] == 3
     assert 0 < t["paths"][0] <= t["total"][0]
+
+
+# ---------------------------------------------------------------- mc-cnn cost volume
+def test_golden_volume_fixtures(eng, golden_volume_cases):
+    for name, vol, p, off, sc, expected, raw in golden_volume_cases:
+        out = eng.aggregate_cost_f32(vol, synthetic.to_sm_params(p), off, sc)
+        assert np.array_equal(out, expected), f"{name}: {np.sum(out != expected)} px differ"
+        got_raw = np.frombuffer(eng.debug_fetch(2), np.int16).reshape(expected.shape)
+        assert np.array_equal(got_raw, raw), name
+
+
+def test_volume_quantised_cost_matches_oracle(eng):
+    rng = np.random.default_rng(21)
+    vol = rng.standard_normal((48, 23, 130)).astype(np.float32)
+    vol[rng.random(vol.shape) < 0.03] = np.nan
+    p = dict(synthetic.cost_volume_params(48), minDisparity=2)
+    eng.aggregate_cost_f32(vol, synthetic.to_sm_params(p), 0.1, 900.0)
+    prm = sgm_np.normalize_params(dict(p, cost=2))
+    C = sgm_np.quantize_volume(vol, prm, 0.1, 900.0)
+    got = np.frombuffer(eng.debug_fetch(0), np.uint16).reshape(C.shape)
+    assert np.array_equal(got, C)
+
+
+_VCASES = [dict(H=int(_rng.integers(1, 70)), W=int(_rng.integers(20, 300)), D=16 * int(_rng.integers(1, 9)),
+                minD=int(_rng.integers(-8, 8)), mode=int(_rng.choice([5, 8])), seed=int(_rng.integers(0, 1 << 30)))
+           for _ in range(12)]
+
+
+@pytest.mark.parametrize("c", _VCASES, ids=lambda c: "H{H}W{W}D{D}m{minD}p{mode}".format(**c))
+def test_volume_random_shapes_vs_c_oracle(eng, c):
+    rng = np.random.default_rng(c["seed"])
+    vol = rng.random((c["D"], c["H"], c["W"]), dtype=np.float32)
+    p = dict(synthetic.cost_volume_params(c["D"]), minDisparity=c["minD"], mode=c["mode"])
+    out = eng.aggregate_cost_f32(vol, synthetic.to_sm_params(p), 0.0, synthetic.VOLUME_SCALE)
+    assert np.array_equal(out, ref_c.compute_volume(vol, p, 0.0, synthetic.VOLUME_SCALE))
+
+
+@pytest.mark.parametrize("mode", [8, 5])
+def test_volume_full_size_mccnn(eng, mode):
+    """Config C: (1, 192, 375, 1242) float32 |L-R| volume of the KITTI-size pair."""
+    H, W, D = synthetic.CONFIGS["mccnn"]
+    left, right, gt = synthetic.random_dot_pair(H, W, D, seed=7)
+    vol = synthetic.absdiff_volume(left, right, D)
+    p = dict(synthetic.cost_volume_params(D), mode=mode)
+    out = eng.aggregate_cost_f32(vol, synthetic.to_sm_params(p), 0.0, synthetic.VOLUME_SCALE)
+    assert np.array_equal(out, ref_c.compute_volume(vol, p, 0.0, synthetic.VOLUME_SCALE))
+    valid = out >= 0
+    assert valid.mean() > 0.7
+    assert np.mean(np.abs(((out.astype(np.int64) + 8) >> 4) - gt)[valid] <= 1) > 0.97
+
+
+def test_volume_torch_batch_and_matcher():
+    import torch
+
+    import stereo_match_amd as sm
+
+    H, W, D, n = 50, 180, 32, 3
+    vols = []
+    for s in range(n):
+        l, r, _ = synthetic.random_dot_pair(H, W, D, seed=30 + s)
+        vols.append(synthetic.absdiff_volume(l, r, D)[0])
+    p = synthetic.cost_volume_params(D)
+    m = sm.StereoSGBM_create(numDisparities=D, P1=p["P1"], P2=p["P2"], disp12MaxDiff=1, uniquenessRatio=15,
+                             mode=sm.STEREO_SGBM_MODE_HH)
+    a = m.computeFromCost(vols[0][None], 0.0, synthetic.VOLUME_SCALE)
+    assert np.array_equal(a, ref_c.compute_volume(vols[0], p, 0.0, synthetic.VOLUME_SCALE))
+    t = m.computeFromCost(torch.tensor(vols[0], device="cuda"), 0.0, synthetic.VOLUME_SCALE)
+    assert np.array_equal(t.cpu().numpy(), a)
+    V = torch.tensor(np.stack(vols), device="cuda")
+    out = torch.empty((n, H, W), dtype=torch.int16, device="cuda")
+    eng = _lib.engine(0)
+    eng.set_stream(torch.cuda.current_stream().cuda_stream)
+    eng.aggregate_cost_f32_device(V.data_ptr(), n, D * H * W, D, H, W, synthetic.to_sm_params(p), 0.0,
+                                  synthetic.VOLUME_SCALE, out.data_ptr())
+    got = out.cpu().numpy()
+    for i in range(n):
+        assert np.array_equal(got[i], ref_c.compute_volume(vols[i], p, 0.0, synthetic.VOLUME_SCALE)), i
+
+
+def test_volume_bad_args(eng):
+    vol = np.zeros((16, 8, 40), np.float32)
+    with pytest.raises(ValueError):  # planes != numDisparities
+        eng.aggregate_cost_f32(vol, synthetic.to_sm_params(synthetic.cost_volume_params(32)))
+    with pytest.raises(_lib.SmError):  # P2 beyond the exact range
+        eng.aggregate_cost_f32(vol, synthetic.to_sm_params(dict(synthetic.cost_volume_params(16), P2=13000)))

@@ -160,3 +160,62 @@ def test_speckle_filter_matches_c():
     lib.sgm_ref_filter_speckles.argtypes = [ref_c.ctypes.c_void_p] + [ref_c.ctypes.c_int] * 5
     lib.sgm_ref_filter_speckles(b.ctypes.data, 20, 30, -16, 3, 32)
     assert np.array_equal(a, b)
+
+
+# ---------------------------------------------------------------- mc-cnn volume mode
+def test_volume_quantisation_kat():
+    """q = rint((c + offset) * scale) (float32, half-even), clamp [0, 4095], NaN -> 4095."""
+    prm = sgm_np.normalize_params(dict(numDisparities=16, cost=2))
+    c = np.array([0.5, 1.5, 2.5, -0.4, -7, 4095.4, 4095.6, 1e9, np.inf, -np.inf, np.nan, 3.0],
+                 np.float32)
+    W = c.size + 16  # minX1 = 16: the samples sit at x = 16..
+    vol = np.zeros((16, 1, W), np.float32)
+    vol[0, 0, 16:] = c
+    q = sgm_np.quantize_volume(vol, prm, 0.0, 1.0)[0, :, 0]
+    assert q.tolist() == [0, 2, 2, 0, 0, 4095, 4095, 4095, 4095, 0, 4095, 3]
+    q2 = sgm_np.quantize_volume(vol, prm, 0.5, 2.0)[0, :, 0]  # (c + .5) * 2
+    assert q2[:3].tolist() == [2, 4, 6]
+
+
+def test_volume_constant_shift_recovered():
+    """KAT: a volume that is 0 at d = 7 and 1 elsewhere → raw WTA = 7·16 wherever LR holds."""
+    H, W, D = 20, 90, 16
+    vol = np.ones((D, H, W), np.float32)
+    vol[7] = 0
+    p = dict(synthetic.cost_volume_params(D))
+    out, st = sgm_np.compute_volume(vol, p, 0.0, 1000.0, return_stages=True)
+    raw = st["raw"]
+    assert np.all(raw[:, D:] == 7 * 16)
+    assert np.all(raw[:, :D] == -16)
+    assert np.array_equal(out, ref_c.compute_volume(vol, p, 0.0, 1000.0))
+
+
+def test_golden_volume_fixtures_reproduce(golden_volume_cases):
+    for name, vol, p, off, sc, expected, raw in golden_volume_cases:
+        out, st = sgm_np.compute_volume(vol, p, off, sc, return_stages=True)
+        assert np.array_equal(out, expected), name
+        assert np.array_equal(st["raw"], raw), name
+        assert np.array_equal(ref_c.compute_volume(vol, p, off, sc), expected), name
+
+
+@settings(max_examples=25, deadline=None)
+@given(H=st.integers(1, 24), W=st.integers(17, 80), Dk=st.integers(1, 2), minD=st.integers(-4, 4),
+       mode=st.sampled_from([5, 8]), scale=st.sampled_from([1.0, 37.5, 4000.0]),
+       nan_frac=st.sampled_from([0.0, 0.05]), seed=st.integers(0, 2**31 - 1))
+def test_volume_numpy_c_bit_exact(H, W, Dk, minD, mode, scale, nan_frac, seed):
+    D = 16 * Dk
+    rng = np.random.default_rng(seed)
+    vol = rng.standard_normal((D, H, W)).astype(np.float32)
+    vol[rng.random(vol.shape) < nan_frac] = np.nan
+    p = dict(synthetic.cost_volume_params(D), minDisparity=minD, mode=mode, P1=int(rng.integers(1, 60)),
+             P2=int(rng.integers(60, 600)))
+    assert np.array_equal(sgm_np.compute_volume(vol, p, 0.25, scale), ref_c.compute_volume(vol, p, 0.25, scale))
+
+
+def test_volume_rejects_bad_shapes():
+    with pytest.raises(ValueError):
+        sgm_np.compute_volume(np.zeros((16, 4, 40), np.float32), dict(numDisparities=32))
+    with pytest.raises(ValueError):
+        ref_c.compute_volume(np.zeros((16, 4, 40), np.float32), dict(numDisparities=32))
+    with pytest.raises(ValueError):  # P2 outside the int16-exact range
+        sgm_np.compute_volume(np.zeros((16, 4, 40), np.float32), dict(numDisparities=16, P2=20000))
