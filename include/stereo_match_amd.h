@@ -104,6 +104,52 @@ int sm_aggregate_cost_f32(sm_ctx* ctx, const float* cost, int D, int H, int W, c
 int sm_aggregate_cost_f32_device(sm_ctx* ctx, const float* d_cost, int npairs, size_t pair_stride_elems, int D,
                                  int H, int W, const sm_params* p, float offset, float scale, int16_t* d_disp_out);
 
+/* ---- WLS post-filter: cv2.ximgproc.createDisparityWLSFilter(left_matcher)
+ * + setLambda/setSigmaColor + filter(displ, gray_l, None, dispr)
+ * (reference: stereo_vision/stereo_vision.py:172-175,182).  Fields mirror
+ * DisparityWLSFilter's setters / the filter's construction parameters. */
+typedef struct sm_wls_params {
+    double lambda;                  /* setLambda (default 8000; settings.ini lmbda 80000) */
+    double sigma_color;             /* setSigmaColor (default 1.0; settings.ini sigma 1.2) */
+    int lrc_thresh;                 /* setLRCthresh (24, in 1/16 px) */
+    int depth_discontinuity_radius; /* setDepthDiscontinuityRadius (ceil(0.5*blockSize) for SGBM) */
+    int use_confidence;             /* 1: LR-confidence WLS (needs dispr); 0: plain FGS (Generic(false)) */
+    int min_disp;                   /* fill outside the ROI: 16*(min_disp-1) */
+    int left_offset, right_offset, top_offset, bottom_offset; /* valid ROI of the left map */
+    int num_iter;                   /* fast global smoother iterations (3) */
+    float lambda_attenuation;       /* per-iteration lambda factor (0.25) */
+    float roll_off;                 /* depth-discontinuity roll-off (0.001) */
+} sm_wls_params;
+
+/* The filter createDisparityWLSFilter(matcher with params `left`) builds. */
+int sm_wls_default_params(const sm_params* left, sm_wls_params* out);
+
+/* DisparityWLSFilter::filter on host buffers: displ/dispr int16[H*W] x16
+ * (dispr may be NULL when !use_confidence), guide = left gray view uint8
+ * (row stride guide_stride).  out int16[H*W].  Synchronous. */
+int sm_wls_filter(sm_ctx* ctx, const int16_t* displ, const int16_t* dispr, const uint8_t* guide, int guide_stride,
+                  int H, int W, const sm_wls_params* p, int16_t* out);
+/* Batch on device pointers (maps at +i*H*W, guides at +i*guide_pair_stride). */
+int sm_wls_filter_batch_device(sm_ctx* ctx, const int16_t* d_displ, const int16_t* d_dispr, const uint8_t* d_guide,
+                               int npairs, size_t guide_pair_stride, int guide_stride, int H, int W,
+                               const sm_wls_params* p, int16_t* d_out);
+
+/* compute_disparity (stereo_vision/stereo_vision.py:132-184) in one call:
+ * `left` = the matcher as created from the settings (:153-163); the
+ * createDisparityWLSFilter mutation (uniqueness 0, disp12MaxDiff 1e6,
+ * speckle 0) is applied to it, the right matcher is derived as
+ * createRightMatcher does and runs on the swapped pair, and `wls` (see
+ * sm_wls_default_params, then lambda/sigma from the settings) filters.
+ * Outputs displ and filtered int16[H*W] x16.  Synchronous. */
+int sm_compute_disparity(sm_ctx* ctx, const uint8_t* left_img, const uint8_t* right_img, int H, int W, int stride,
+                         const sm_params* left, const sm_wls_params* wls, int16_t* displ, int16_t* filtered);
+/* Same over a device batch (pair i at +i*pair_stride bytes; maps at +i*H*W;
+ * d_dispr receives the right matcher's maps). Asynchronous. */
+int sm_compute_disparity_batch_device(sm_ctx* ctx, const uint8_t* d_left, const uint8_t* d_right, int npairs,
+                                      size_t pair_stride, int H, int W, int stride, const sm_params* left,
+                                      const sm_wls_params* wls, int16_t* d_displ, int16_t* d_dispr,
+                                      int16_t* d_filtered);
+
 /* ximgproc::createRightMatcher(StereoSGBM) parameter derivation
  * (reference call: stereo_vision/stereo_vision.py:171). */
 int sm_right_matcher_params(const sm_params* left, sm_params* right_out);

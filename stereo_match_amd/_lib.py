@@ -34,6 +34,18 @@ class SmParams(ctypes.Structure):
         return {n: getattr(self, n) for n, _ in self._fields_}
 
 
+class SmWlsParams(ctypes.Structure):
+    """Mirror of ``struct sm_wls_params``."""
+    _fields_ = [("lambda_", ctypes.c_double), ("sigma_color", ctypes.c_double)] + [
+        (n, ctypes.c_int) for n in (
+            "lrc_thresh", "depth_discontinuity_radius", "use_confidence", "min_disp", "left_offset",
+            "right_offset", "top_offset", "bottom_offset", "num_iter")] + [
+        ("lambda_attenuation", ctypes.c_float), ("roll_off", ctypes.c_float)]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
 _c = ctypes
 _SIGS = {
     "sm_version": (_c.c_char_p, []),
@@ -52,6 +64,18 @@ _SIGS = {
     "sm_aggregate_cost_f32_device": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_int, _c.c_size_t, _c.c_int,
                                                 _c.c_int, _c.c_int, _c.POINTER(SmParams), _c.c_float,
                                                 _c.c_float, _c.c_void_p]),
+    "sm_wls_default_params": (_c.c_int, [_c.POINTER(SmParams), _c.POINTER(SmWlsParams)]),
+    "sm_wls_filter": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_int, _c.c_int, _c.c_int,
+                                 _c.POINTER(SmWlsParams), _c.c_void_p]),
+    "sm_wls_filter_batch_device": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_int,
+                                              _c.c_size_t, _c.c_int, _c.c_int, _c.c_int, _c.POINTER(SmWlsParams),
+                                              _c.c_void_p]),
+    "sm_compute_disparity": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_int, _c.c_int, _c.c_int,
+                                        _c.POINTER(SmParams), _c.POINTER(SmWlsParams), _c.c_void_p, _c.c_void_p]),
+    "sm_compute_disparity_batch_device": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_int, _c.c_size_t,
+                                                     _c.c_int, _c.c_int, _c.c_int, _c.POINTER(SmParams),
+                                                     _c.POINTER(SmWlsParams), _c.c_void_p, _c.c_void_p,
+                                                     _c.c_void_p]),
     "sm_right_matcher_params": (_c.c_int, [_c.POINTER(SmParams), _c.POINTER(SmParams)]),
     "sm_synchronize": (_c.c_int, [_c.c_void_p]),
     "sm_set_timing": (_c.c_int, [_c.c_void_p, _c.c_int]),
@@ -65,6 +89,15 @@ _SIGS = {
 
 _lib = None
 _lock = threading.Lock()
+
+
+def wls_default_params(left: SmParams) -> SmWlsParams:
+    """sm_wls_default_params: the filter createDisparityWLSFilter(left) builds."""
+    out = SmWlsParams()
+    rc = load().sm_wls_default_params(ctypes.byref(left), ctypes.byref(out))
+    if rc != SM_OK:
+        _raise(rc, None)
+    return out
 
 
 def header_symbols(path: str = HEADER_PATH):
@@ -191,6 +224,50 @@ class Engine:
         self._check(self._lib.sm_aggregate_cost_f32_device(
             self.ctx, ctypes.c_void_p(d_cost), npairs, pair_stride_elems, D, H, W, ctypes.byref(params),
             float(offset), float(scale), ctypes.c_void_p(d_out)))
+
+    # -- WLS post-filter --------------------------------------------------------
+    def wls_filter(self, displ: np.ndarray, guide: np.ndarray, dispr, params: "SmWlsParams") -> np.ndarray:
+        displ = np.ascontiguousarray(displ, np.int16)
+        guide = np.ascontiguousarray(guide, np.uint8)
+        H, W = displ.shape
+        if guide.shape != (H, W):
+            raise ValueError("guide must be a gray (uint8) image of the disparity map's size")
+        ptr_r = None
+        if dispr is not None:
+            dispr = np.ascontiguousarray(dispr, np.int16)
+            if dispr.shape != (H, W):
+                raise ValueError("right disparity map must match the left one")
+            ptr_r = dispr.ctypes.data
+        out = np.empty((H, W), np.int16)
+        self._check(self._lib.sm_wls_filter(self.ctx, displ.ctypes.data, ptr_r, guide.ctypes.data, W, H, W,
+                                            ctypes.byref(params), out.ctypes.data))
+        return out
+
+    def wls_filter_batch_device(self, d_displ: int, d_dispr, d_guide: int, npairs: int, guide_pair_stride: int,
+                                guide_stride: int, H: int, W: int, params: "SmWlsParams", d_out: int):
+        self._check(self._lib.sm_wls_filter_batch_device(
+            self.ctx, ctypes.c_void_p(d_displ), ctypes.c_void_p(d_dispr or 0) if d_dispr else None,
+            ctypes.c_void_p(d_guide), npairs, guide_pair_stride, guide_stride, H, W, ctypes.byref(params),
+            ctypes.c_void_p(d_out)))
+
+    def compute_disparity(self, left: np.ndarray, right: np.ndarray, params: SmParams, wls: "SmWlsParams"):
+        left = np.ascontiguousarray(left, np.uint8)
+        right = np.ascontiguousarray(right, np.uint8)
+        H, W = left.shape
+        displ = np.empty((H, W), np.int16)
+        filt = np.empty((H, W), np.int16)
+        self._check(self._lib.sm_compute_disparity(self.ctx, left.ctypes.data, right.ctypes.data, H, W, W,
+                                                   ctypes.byref(params), ctypes.byref(wls), displ.ctypes.data,
+                                                   filt.ctypes.data))
+        return displ, filt
+
+    def compute_disparity_batch_device(self, d_left: int, d_right: int, npairs: int, pair_stride: int, H: int,
+                                       W: int, stride: int, params: SmParams, wls: "SmWlsParams", d_displ: int,
+                                       d_dispr: int, d_filtered: int):
+        self._check(self._lib.sm_compute_disparity_batch_device(
+            self.ctx, ctypes.c_void_p(d_left), ctypes.c_void_p(d_right), npairs, pair_stride, H, W, stride,
+            ctypes.byref(params), ctypes.byref(wls), ctypes.c_void_p(d_displ), ctypes.c_void_p(d_dispr),
+            ctypes.c_void_p(d_filtered)))
 
     def synchronize(self):
         self._check(self._lib.sm_synchronize(self.ctx))

@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -28,6 +29,7 @@
 #include "sm_paths.hpp"
 #include "sm_post.hpp"
 #include "sm_rowwta.hpp"
+#include "sm_wls.hpp"
 
 #define SM_VERSION "stereo_match_amd 0.2.0 (gfx950)"
 
@@ -68,6 +70,7 @@ struct sm_ctx {
     hipStream_t stream = nullptr;  // stream A
     hipStream_t side = nullptr;    // stream B
     DevBuf img[2], planes, out, dbg, volbuf;
+    DevBuf wls_num, wls_den, wls_inter, wls_disp[2], wls_out;  // WLS scratch
     BufSet set[2];
     int next_set = 0;
     // geometry of the last computation (for sm_debug_fetch): its last pair
@@ -573,6 +576,126 @@ int run_pairs(sm_ctx* ctx, const Src& src, int npairs, int H, int W, int stride,
     return rc;
 }
 
+
+// ---- WLS post-filter (sm_wls.hpp) ---------------------------------------------
+struct WlsNorm {
+    int x0, y0, w, h, rx0;
+    int radius, lrc, use_conf, fill, num_iter;
+    float lam, att, roll_off;
+    float tab[256];
+};
+
+int normalize_wls(sm_ctx* ctx, const sm_wls_params* p, int H, int W, WlsNorm& n)
+{
+    if (!p) return fail(ctx, SM_E_ARG, "wls params is NULL");
+    if (H <= 0 || W <= 0) return fail(ctx, SM_E_ARG, "empty disparity map (%dx%d)", W, H);
+    if (!(p->lambda >= 0) || !(p->sigma_color > 0)) return fail(ctx, SM_E_ARG, "lambda must be >= 0, sigma > 0");
+    if (p->num_iter < 1) return fail(ctx, SM_E_ARG, "num_iter must be >= 1");
+    if (p->depth_discontinuity_radius < 0 || p->depth_discontinuity_radius > 64)
+        return fail(ctx, SM_E_ARG, "depth_discontinuity_radius %d outside [0, 64]", p->depth_discontinuity_radius);
+    if (p->left_offset < 0 || p->right_offset < 0 || p->top_offset < 0 || p->bottom_offset < 0)
+        return fail(ctx, SM_E_ARG, "negative ROI offset");
+    n.x0 = p->left_offset;
+    n.y0 = p->top_offset;
+    n.w = W - p->left_offset - p->right_offset;
+    n.h = H - p->top_offset - p->bottom_offset;
+    n.rx0 = W - (n.x0 + n.w);  // right_view_valid_disp_ROI
+    n.radius = p->depth_discontinuity_radius;
+    n.lrc = p->lrc_thresh;
+    n.use_conf = p->use_confidence != 0;
+    n.fill = 16 * (p->min_disp - 1);
+    n.num_iter = p->num_iter;
+    n.lam = (float)p->lambda;
+    n.att = p->lambda_attenuation;
+    n.roll_off = p->roll_off;
+    const double sg = (double)(float)p->sigma_color;
+    for (int k = 0; k < 256; k++) n.tab[k] = (float)(-std::exp(-std::sqrt((double)k * k) / sg));
+    return SM_OK;
+}
+
+// npairs maps; pair i: displ/dispr at +i*disp_pair elements, guide at +i*guide_pair bytes.
+int run_wls(sm_ctx* ctx, const int16_t* dl, const int16_t* dr, size_t disp_pair, const uint8_t* guide,
+            size_t guide_pair, int guide_stride, int npairs, int H, int W, const WlsNorm& n, int16_t* d_out)
+{
+    if (npairs <= 0) return SM_OK;
+    const bool roi = n.w > 0 && n.h > 0;
+    const size_t roi_elems = roi ? (size_t)n.w * n.h : 0;
+    // scratch: num, den, inter floats per pair
+    const int G = (int)std::max<size_t>(1, std::min<size_t>(npairs, (size_t(6) << 30) / std::max<size_t>(roi_elems * 12, 1)));
+    int rc;
+    if (roi) {
+        if ((rc = ensure(ctx, ctx->wls_num, (size_t)G * roi_elems * 4)) != SM_OK) return rc;
+        if ((rc = ensure(ctx, ctx->wls_den, (size_t)G * roi_elems * 4)) != SM_OK) return rc;
+        if ((rc = ensure(ctx, ctx->wls_inter, (size_t)G * roi_elems * 4)) != SM_OK) return rc;
+    }
+    for (int p0 = 0; p0 < npairs; p0 += G) {
+        const int g = std::min(G, npairs - p0);
+        if (roi) {
+            smk::WlsConfArgs ca{};
+            ca.dl = dl + (size_t)p0 * disp_pair;
+            ca.dr = dr ? dr + (size_t)p0 * disp_pair : nullptr;
+            ca.disp_pair = disp_pair;
+            ca.num = (float*)ctx->wls_num.p;
+            ca.den = (float*)ctx->wls_den.p;
+            ca.roi_pair = roi_elems;
+            ca.H = H;
+            ca.W = W;
+            ca.x0 = n.x0;
+            ca.y0 = n.y0;
+            ca.w = n.w;
+            ca.h = n.h;
+            ca.rx0 = n.rx0;
+            ca.radius = n.radius;
+            ca.lrc_thresh = n.lrc;
+            ca.roll_off = n.roll_off;
+            ca.use_confidence = n.use_conf;
+            hipLaunchKernelGGL(smk::k_wls_conf, dim3(n.h, g), dim3(256), (size_t)n.w * 4, ctx->stream, ca);
+            HIP_TRY(ctx, hipGetLastError());
+            smk::FgsArgs fa{};
+            fa.u[0] = (float*)ctx->wls_num.p;
+            fa.u[1] = (float*)ctx->wls_den.p;
+            fa.inter = (float*)ctx->wls_inter.p;
+            fa.roi_pair = roi_elems;
+            fa.guide = guide + (size_t)p0 * guide_pair + (size_t)n.y0 * guide_stride + n.x0;
+            fa.guide_pair = guide_pair;
+            fa.guide_stride = guide_stride;
+            fa.w = n.w;
+            fa.h = n.h;
+            std::memcpy(fa.tab, n.tab, sizeof fa.tab);
+            float lam = n.lam;
+            for (int it = 0; it < n.num_iter; it++) {
+                fa.lam = lam;
+                if (n.use_conf) {
+                    hipLaunchKernelGGL((smk::k_fgs<2, true>), dim3((n.h + 63) / 64, g), dim3(64), 0, ctx->stream, fa);
+                    hipLaunchKernelGGL((smk::k_fgs<2, false>), dim3((n.w + 63) / 64, g), dim3(64), 0, ctx->stream, fa);
+                } else {
+                    hipLaunchKernelGGL((smk::k_fgs<1, true>), dim3((n.h + 63) / 64, g), dim3(64), 0, ctx->stream, fa);
+                    hipLaunchKernelGGL((smk::k_fgs<1, false>), dim3((n.w + 63) / 64, g), dim3(64), 0, ctx->stream, fa);
+                }
+                HIP_TRY(ctx, hipGetLastError());
+                lam = lam * n.att;
+            }
+        }
+        smk::WlsFinalArgs wa{};
+        wa.num = (const float*)ctx->wls_num.p;
+        wa.den = (const float*)ctx->wls_den.p;
+        wa.roi_pair = roi_elems;
+        wa.out = d_out + (size_t)p0 * H * W;
+        wa.out_pair = (size_t)H * W;
+        wa.H = H;
+        wa.W = W;
+        wa.x0 = n.x0;
+        wa.y0 = n.y0;
+        wa.w = roi ? n.w : 0;
+        wa.h = roi ? n.h : 0;
+        wa.fill = n.fill;
+        wa.use_confidence = n.use_conf;
+        hipLaunchKernelGGL(smk::k_wls_final, dim3((W + 255) / 256, H, g), dim3(256), 0, ctx->stream, wa);
+        HIP_TRY(ctx, hipGetLastError());
+    }
+    return SM_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -606,7 +729,9 @@ void sm_destroy(sm_ctx* ctx)
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     (void)hipDeviceSynchronize();
-    DevBuf* bufs[] = {&ctx->img[0], &ctx->img[1], &ctx->planes, &ctx->out, &ctx->dbg, &ctx->volbuf};
+    DevBuf* bufs[] = {&ctx->img[0],  &ctx->img[1],  &ctx->planes,    &ctx->out,         &ctx->dbg,
+                      &ctx->volbuf,  &ctx->wls_num, &ctx->wls_den,   &ctx->wls_inter,   &ctx->wls_disp[0],
+                      &ctx->wls_disp[1], &ctx->wls_out};
     for (DevBuf* b : bufs)
         if (b->p) (void)hipFree(b->p);
     for (auto& bs : ctx->set) {
@@ -750,6 +875,120 @@ int sm_aggregate_cost_f32(sm_ctx* ctx, const float* cost, int D, int H, int W, c
                                       (int16_t*)ctx->out.p);
     if (rc != SM_OK) return rc;
     HIP_TRY(ctx, hipMemcpyAsync(disp_out, ctx->out.p, img * 2, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return SM_OK;
+}
+
+int sm_wls_default_params(const sm_params* left, sm_wls_params* out)
+{
+    if (!left || !out) return fail(nullptr, SM_E_ARG, "NULL params");
+    const int minD = left->min_disparity, D = left->num_disparities, ws = left->block_size;
+    out->lambda = 8000.0;
+    out->sigma_color = 1.0;
+    out->lrc_thresh = 24;
+    out->depth_discontinuity_radius = (int)std::ceil(0.5 * ws);
+    out->use_confidence = 1;
+    out->min_disp = minD;
+    out->left_offset = std::max(0, minD + D);
+    out->right_offset = std::max(0, -minD);
+    out->top_offset = 0;
+    out->bottom_offset = 0;
+    out->num_iter = 3;
+    out->lambda_attenuation = 0.25f;
+    out->roll_off = 0.001f;
+    return SM_OK;
+}
+
+int sm_wls_filter_batch_device(sm_ctx* ctx, const int16_t* d_displ, const int16_t* d_dispr, const uint8_t* d_guide,
+                               int npairs, size_t guide_pair_stride, int guide_stride, int H, int W,
+                               const sm_wls_params* p, int16_t* d_out)
+{
+    if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
+    if (npairs < 0) return fail(ctx, SM_E_ARG, "npairs < 0");
+    if (!d_displ || !d_guide || !d_out) return fail(ctx, SM_E_ARG, "NULL disparity/guide/output pointer");
+    if (guide_stride < W) return fail(ctx, SM_E_ARG, "guide stride %d < width %d", guide_stride, W);
+    WlsNorm n;
+    int rc = normalize_wls(ctx, p, H, W, n);
+    if (rc != SM_OK) return rc;
+    if (n.use_conf && !d_dispr) return fail(ctx, SM_E_ARG, "use_confidence needs the right disparity map");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    return run_wls(ctx, d_displ, d_dispr, (size_t)H * W, d_guide, guide_pair_stride, guide_stride, npairs, H, W, n,
+                   d_out);
+}
+
+int sm_wls_filter(sm_ctx* ctx, const int16_t* displ, const int16_t* dispr, const uint8_t* guide, int guide_stride,
+                  int H, int W, const sm_wls_params* p, int16_t* out)
+{
+    if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
+    if (!displ || !guide || !out) return fail(ctx, SM_E_ARG, "NULL disparity/guide/output pointer");
+    if (guide_stride < W) return fail(ctx, SM_E_ARG, "guide stride %d < width %d", guide_stride, W);
+    WlsNorm n;
+    int rc = normalize_wls(ctx, p, H, W, n);
+    if (rc != SM_OK) return rc;
+    if (n.use_conf && !dispr) return fail(ctx, SM_E_ARG, "use_confidence needs the right disparity map");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    const size_t img = (size_t)H * W;
+    if ((rc = ensure(ctx, ctx->wls_disp[0], img * 2)) != SM_OK) return rc;
+    if ((rc = ensure(ctx, ctx->wls_disp[1], img * 2)) != SM_OK) return rc;
+    if ((rc = ensure(ctx, ctx->img[0], img)) != SM_OK) return rc;
+    if ((rc = ensure(ctx, ctx->wls_out, img * 2)) != SM_OK) return rc;
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->wls_disp[0].p, displ, img * 2, hipMemcpyHostToDevice, ctx->stream));
+    if (dispr) HIP_TRY(ctx, hipMemcpyAsync(ctx->wls_disp[1].p, dispr, img * 2, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpy2DAsync(ctx->img[0].p, W, guide, guide_stride, W, H, hipMemcpyHostToDevice, ctx->stream));
+    rc = run_wls(ctx, (const int16_t*)ctx->wls_disp[0].p, dispr ? (const int16_t*)ctx->wls_disp[1].p : nullptr, img,
+                 (const uint8_t*)ctx->img[0].p, img, W, 1, H, W, n, (int16_t*)ctx->wls_out.p);
+    if (rc != SM_OK) return rc;
+    HIP_TRY(ctx, hipMemcpyAsync(out, ctx->wls_out.p, img * 2, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return SM_OK;
+}
+
+// compute_disparity (stereo_vision/stereo_vision.py:132-184) in one call, on
+// device pointers: left matcher with the createDisparityWLSFilter mutation
+// (uniqueness 0, disp12MaxDiff 1e6, speckle 0), right matcher on the swapped
+// pair, WLS filter guided by the left view.
+int sm_compute_disparity_batch_device(sm_ctx* ctx, const uint8_t* dL, const uint8_t* dR, int npairs,
+                                      size_t pair_stride, int H, int W, int stride, const sm_params* left,
+                                      const sm_wls_params* wls, int16_t* d_displ, int16_t* d_dispr,
+                                      int16_t* d_filtered)
+{
+    if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
+    if (!left || !wls) return fail(ctx, SM_E_ARG, "NULL params");
+    if (!d_displ || !d_dispr || !d_filtered) return fail(ctx, SM_E_ARG, "NULL output pointer");
+    sm_params lm = *left, rm;
+    sm_right_matcher_params(left, &rm);  // createRightMatcher (:171) sees the unmutated matcher
+    lm.uniqueness_ratio = 0;             // createDisparityWLSFilter (:172) mutates the left one
+    lm.disp12_max_diff = 1000000;
+    lm.speckle_window_size = 0;
+    int rc = sm_compute_batch_device(ctx, dL, dR, npairs, pair_stride, H, W, stride, &lm, d_displ);
+    if (rc != SM_OK) return rc;
+    rc = sm_compute_batch_device(ctx, dR, dL, npairs, pair_stride, H, W, stride, &rm, d_dispr);
+    if (rc != SM_OK) return rc;
+    return sm_wls_filter_batch_device(ctx, d_displ, d_dispr, dL, npairs, pair_stride, stride, H, W, wls, d_filtered);
+}
+
+int sm_compute_disparity(sm_ctx* ctx, const uint8_t* L, const uint8_t* R, int H, int W, int stride,
+                         const sm_params* left, const sm_wls_params* wls, int16_t* displ, int16_t* filtered)
+{
+    if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
+    if (!L || !R || !displ || !filtered) return fail(ctx, SM_E_ARG, "NULL image/output pointer");
+    if (stride < W || H <= 0 || W <= 0) return fail(ctx, SM_E_ARG, "bad geometry %dx%d stride %d", W, H, stride);
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    const size_t img = (size_t)H * W;
+    int rc;
+    for (int i = 0; i < 2; i++)
+        if ((rc = ensure(ctx, ctx->img[i], img)) != SM_OK) return rc;
+    if ((rc = ensure(ctx, ctx->wls_disp[0], img * 2)) != SM_OK) return rc;
+    if ((rc = ensure(ctx, ctx->wls_disp[1], img * 2)) != SM_OK) return rc;
+    if ((rc = ensure(ctx, ctx->wls_out, img * 2)) != SM_OK) return rc;
+    HIP_TRY(ctx, hipMemcpy2DAsync(ctx->img[0].p, W, L, stride, W, H, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpy2DAsync(ctx->img[1].p, W, R, stride, W, H, hipMemcpyHostToDevice, ctx->stream));
+    rc = sm_compute_disparity_batch_device(ctx, (const uint8_t*)ctx->img[0].p, (const uint8_t*)ctx->img[1].p, 1, img,
+                                           H, W, W, left, wls, (int16_t*)ctx->wls_disp[0].p,
+                                           (int16_t*)ctx->wls_disp[1].p, (int16_t*)ctx->wls_out.p);
+    if (rc != SM_OK) return rc;
+    HIP_TRY(ctx, hipMemcpyAsync(displ, ctx->wls_disp[0].p, img * 2, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(filtered, ctx->wls_out.p, img * 2, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     return SM_OK;
 }

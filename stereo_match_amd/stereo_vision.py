@@ -7,9 +7,11 @@ Reference: ``stereo_vision/stereo_vision.py:132-184``::
 
 Same argument meaning, same P1/P2 derivation (``:148-149``), same
 ``RuntimeError('Method not supported')`` (``:167-168``).  The left and
-right SGBM matches run on the MI355X through the C-ABI; the WLS post-filter
-(``:172-175,182``) is the next row of the scope table and is
-provided by :mod:`stereo_match_amd.wls`.
+right SGBM matches and the WLS post-filter (``:172-175,182``,
+:mod:`stereo_match_amd.wls`) all run on the MI355X through the C-ABI, in
+the reference's call order (so ``createDisparityWLSFilter``'s mutation of
+the left matcher applies to ``displ`` exactly as in the reference).
+``sm_compute_disparity`` in the C-ABI is the same flow in one call.
 """
 from __future__ import annotations
 

@@ -24,7 +24,7 @@ def golden_cases():
 
     out = []
     for path in sorted(glob.glob(os.path.join(GOLDEN, "*.npz"))):
-        if os.path.basename(path).startswith("vol_"):
+        if os.path.basename(path).startswith(("vol_", "wls_")):
             continue
         z = np.load(path, allow_pickle=False)
         out.append((os.path.basename(path)[:-4], z["left"], z["right"], json.loads(str(z["params"])),
@@ -47,4 +47,21 @@ def golden_volume_cases():
         out.append((os.path.basename(path)[:-4], z["vol"], json.loads(str(z["params"])), float(z["offset"]),
                     float(z["scale"]), z["expected"], z["raw"]))
     assert out, "no volume fixtures (run tests/golden/make_golden.py)"
+    return out
+
+
+@pytest.fixture(scope="session")
+def golden_wls_cases():
+    """(name, displ, dispr or None, guide, wls params, expected) — WLS post-filter."""
+    import glob
+    import json
+
+    import numpy as np
+
+    out = []
+    for path in sorted(glob.glob(os.path.join(GOLDEN, "wls_*.npz"))):
+        z = np.load(path, allow_pickle=False)
+        out.append((os.path.basename(path)[:-4], z["displ"], z["dispr"] if "dispr" in z.files else None,
+                    z["guide"], json.loads(str(z["params"])), z["expected"]))
+    assert out, "no WLS fixtures (run tests/golden/make_golden.py)"
     return out

@@ -21,7 +21,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, ROOT)
 
-from oracle import ref_c, sgm_np  # noqa: E402
+from oracle import ref_c, sgm_np, wls_np  # noqa: E402
 from stereo_match_amd import synthetic  # noqa: E402
 
 
@@ -72,7 +72,31 @@ def volume_cases():
     yield "vol_minD_neg3_d16", v16, dict(synthetic.cost_volume_params(16), minDisparity=-3), 0.0, 1000.0
 
 
+def wls_cases():
+    """WLS post-filter: wls_<name>.npz holds ``displ``, ``dispr``
+    (int16, from the SGBM oracle as compute_disparity runs them), ``guide``
+    (uint8), ``params`` (JSON of the wls_np params) and ``expected``."""
+    for name, (H, W, D, seed, ws) in dict(d16=(40, 96, 16, 21, 5), d32_ws3=(48, 120, 32, 22, 3)).items():
+        left, right, _ = synthetic.random_dot_pair(H, W, D, seed=seed)
+        settings = synthetic.parity_params(D, window_size=ws)
+        lp = dict(settings, uniquenessRatio=0, disp12MaxDiff=1000000)  # createDisparityWLSFilter mutation
+        displ = ref_c.compute(left, right, lp)
+        dispr = ref_c.compute(right, left, sgm_np.right_matcher_params(settings))
+        wp = dict(lmbda=80000.0, sigma=1.2, radius=(5 + 1) // 2, min_disp=0, left_offset=D, right_offset=0)
+        yield "wls_" + name, displ, dispr, left, wp
+    left, right, _ = synthetic.random_dot_pair(30, 70, 16, seed=23)
+    d = ref_c.compute(left, right, synthetic.parity_params(16))
+    yield "wls_generic_noconf", d, None, left, dict(lmbda=8000.0, sigma=1.5, use_confidence=False)
+
+
 def main():
+    for name, displ, dispr, guide, wp in wls_cases():
+        out = wls_np.wls_filter(displ, guide, dispr, wp)
+        arrs = dict(displ=displ, guide=guide, params=np.array(json.dumps(wp)), expected=out)
+        if dispr is not None:
+            arrs["dispr"] = dispr
+        np.savez_compressed(os.path.join(HERE, name + ".npz"), **arrs)
+        print(f"{name}: {displ.shape} filled={np.mean(out >= 0):.3f}")
     for name, vol, p, off, sc in volume_cases():
         out, st = sgm_np.compute_volume(vol, p, off, sc, return_stages=True)
         c = ref_c.compute_volume(vol, p, off, sc)

@@ -1,0 +1,146 @@
+"""GPU parity of the WLS post-filter and of the whole compute_disparity
+(left SGBM + right SGBM + WLS) against the CPU restatements.  Bar:
+bit-exact int16 (the kernels run the oracle's float32 operation order with
+FP contraction off).  Parity with ximgproc itself is unpinned."""
+import numpy as np
+import pytest
+
+from oracle import ref_c, sgm_np, wls_np
+from stereo_match_amd import _lib, synthetic
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    e = _lib.Engine(0)
+    yield e
+    e.close()
+
+
+def wls_params(p: dict, H, W) -> _lib.SmWlsParams:
+    q = wls_np.normalize_wls(p, H, W)
+    return _lib.SmWlsParams(q["lmbda"], q["sigma"], q["lrc_thresh"], q["radius"], int(q["use_confidence"]),
+                            q["min_disp"], q["left_offset"], q["right_offset"], q["top_offset"],
+                            q["bottom_offset"], q["num_iter"], q["attenuation"], q["roll_off"])
+
+
+def test_golden_wls_fixtures(eng, golden_wls_cases):
+    for name, displ, dispr, guide, p, expected in golden_wls_cases:
+        out = eng.wls_filter(displ, guide, dispr, wls_params(p, *displ.shape))
+        assert np.array_equal(out, expected), f"{name}: {np.sum(out != expected)} px differ"
+
+
+def _pair_maps(H, W, D, seed, ws=5, minD=0):
+    left, right, gt = synthetic.random_dot_pair(H, W, D, seed=seed)
+    settings = dict(synthetic.parity_params(D, window_size=ws), minDisparity=minD)
+    lp = dict(settings, uniquenessRatio=0, disp12MaxDiff=1000000)
+    displ = ref_c.compute(left, right, lp)
+    dispr = ref_c.compute(right, left, sgm_np.right_matcher_params(settings))
+    return left, right, gt, settings, displ, dispr
+
+
+_rng = np.random.default_rng(77)
+_CASES = [dict(H=int(_rng.integers(2, 80)), W=int(_rng.integers(40, 260)), D=16 * int(_rng.integers(1, 3)),
+               minD=int(_rng.integers(-4, 4)), r=int(_rng.integers(0, 5)), lam=float(_rng.choice([10.0, 8000.0, 80000.0])),
+               sigma=float(_rng.choice([0.7, 1.2, 3.0])), top=int(_rng.integers(0, 3)), seed=int(_rng.integers(0, 1 << 30)))
+          for _ in range(10)]
+
+
+@pytest.mark.parametrize("c", _CASES, ids=lambda c: "H{H}W{W}D{D}m{minD}r{r}".format(**c))
+def test_wls_random_vs_oracle(eng, c):
+    left, _, _, _, displ, dispr = _pair_maps(c["H"], c["W"], c["D"], c["seed"], minD=c["minD"])
+    H, W = displ.shape
+    p = dict(lmbda=c["lam"], sigma=c["sigma"], radius=c["r"], min_disp=c["minD"],
+             left_offset=max(0, c["minD"] + c["D"]), right_offset=max(0, -c["minD"]),
+             top_offset=min(c["top"], H - 1), bottom_offset=0)
+    out = eng.wls_filter(displ, left, dispr, wls_params(p, H, W))
+    assert np.array_equal(out, wls_np.wls_filter(displ, left, dispr, p))
+
+
+def test_wls_no_confidence(eng):
+    left, _, _, _, displ, _ = _pair_maps(50, 160, 32, 5)
+    p = dict(lmbda=8000.0, sigma=1.5, use_confidence=False)
+    out = eng.wls_filter(displ, left, None, wls_params(p, *displ.shape))
+    assert np.array_equal(out, wls_np.wls_filter(displ, left, None, p))
+
+
+def test_wls_full_size_kitti(eng):
+    H, W, D = synthetic.CONFIGS["kitti"]
+    left, _, gt, _, displ, dispr = _pair_maps(H, W, D, 42)
+    p = dict(lmbda=80000.0, sigma=1.2, radius=3, left_offset=D)
+    out = eng.wls_filter(displ, left, dispr, wls_params(p, H, W))
+    exp = wls_np.wls_filter(displ, left, dispr, p)
+    assert np.array_equal(out, exp), f"{np.sum(out != exp)} px differ"
+    roi = out[:, D:]
+    assert np.all(roi >= 0)
+    assert np.mean(np.abs(((roi.astype(np.int64) + 8) >> 4) - gt[:, D:]) <= 1) > 0.97
+
+
+def test_compute_disparity_end_to_end():
+    """stereo_vision.compute_disparity drop-in: (displ, filtered) vs the
+    oracle chain run in the reference's order."""
+    import stereo_match_amd as sm
+
+    H, W, D = 96, 300, 64
+    left, right, _ = synthetic.random_dot_pair(H, W, D, seed=8)
+    s = dict(sm.DEFAULT_SETTINGS, window_size=5, num_disparities=D, lmbda=80000, sigma=1.2)
+    displ, filt = sm.compute_disparity(left, right, s)
+    lp = dict(synthetic.parity_params(D), blockSize=s["block_size"], uniquenessRatio=0, disp12MaxDiff=1000000,
+              minDisparity=s["min_disparity"], preFilterCap=s["pre_filter_cap"], speckleRange=s["speckle_range"])
+    settings = dict(lp, uniquenessRatio=s["uniqueness_ratio"], disp12MaxDiff=s["disp12_max_diff"])
+    exp_l = ref_c.compute(left, right, lp)
+    exp_r = ref_c.compute(right, left, sgm_np.right_matcher_params(settings))
+    assert np.array_equal(displ, exp_l)
+    wp = dict(lmbda=80000.0, sigma=1.2, radius=-(-s["block_size"] // 2), min_disp=s["min_disparity"],
+              left_offset=max(0, s["min_disparity"] + D), right_offset=max(0, -s["min_disparity"]))
+    assert np.array_equal(filt, wls_np.wls_filter(exp_l, left, exp_r, wp))
+    # the one-call C-ABI flow gives the same maps
+    eng = _lib.engine(0)
+    sp = synthetic.to_sm_params(settings)
+    d2, f2 = eng.compute_disparity(left, right, sp, wls_params(dict(wp), H, W))
+    assert np.array_equal(d2, displ) and np.array_equal(f2, filt)
+    dw = _lib.wls_default_params(sp)
+    assert (dw.left_offset, dw.right_offset, dw.depth_discontinuity_radius, dw.min_disp) == (D, 0, 3, 0)
+
+
+def test_compute_disparity_batch_device_and_torch():
+    import torch
+
+    import stereo_match_amd as sm
+    from stereo_match_amd import wls
+
+    H, W, D, n = 64, 220, 32, 3
+    pairs = [synthetic.random_dot_pair(H, W, D, seed=50 + i)[:2] for i in range(n)]
+    L = torch.tensor(np.stack([a for a, _ in pairs]), device="cuda")
+    R = torch.tensor(np.stack([b for _, b in pairs]), device="cuda")
+    settings = synthetic.parity_params(D)
+    sp = synthetic.to_sm_params(settings)
+    wp = _lib.wls_default_params(sp)
+    wp.lambda_, wp.sigma_color = 80000.0, 1.2
+    outs = [torch.empty((n, H, W), dtype=torch.int16, device="cuda") for _ in range(3)]
+    eng = _lib.engine(0)
+    eng.set_stream(torch.cuda.current_stream().cuda_stream)
+    eng.compute_disparity_batch_device(L.data_ptr(), R.data_ptr(), n, H * W, H, W, W, sp, wp,
+                                       *(o.data_ptr() for o in outs))
+    got = [o.cpu().numpy() for o in outs]
+    for i, (a, b) in enumerate(pairs):
+        d2, f2 = eng.compute_disparity(a, b, sp, wp)
+        assert np.array_equal(got[0][i], d2) and np.array_equal(got[2][i], f2), i
+    # torch tensors through the Python filter object
+    m = sm.StereoSGBM_create(numDisparities=D, blockSize=5, P1=600, P2=2400, disp12MaxDiff=1, uniquenessRatio=15,
+                             preFilterCap=63)
+    f = wls.createDisparityWLSFilter(m)
+    f.setLambda(80000.0)
+    f.setSigmaColor(1.2)
+    t = f.filter(outs[0][0], L[0], None, outs[1][0])
+    assert np.array_equal(t.cpu().numpy(), got[2][0])
+
+
+def test_wls_bad_args(eng):
+    d = np.zeros((10, 40), np.int16)
+    g = np.zeros((10, 40), np.uint8)
+    with pytest.raises(ValueError):
+        eng.wls_filter(d, g, None, wls_params(dict(), 10, 40))  # confidence needs dispr
+    with pytest.raises(ValueError):
+        eng.wls_filter(d, g, d, wls_params(dict(left_offset=-1), 10, 40))

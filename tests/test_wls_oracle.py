@@ -1,0 +1,90 @@
+"""WLS post-filter oracle (oracle/wls_np.py): known-answer tests and a check
+that the Thomas restatement solves the fast-global-smoother system.
+Parity with ximgproc itself is unpinned (not in the image)."""
+import numpy as np
+import pytest
+
+from oracle import wls_np
+from stereo_match_amd import synthetic
+
+
+def _laplacian_solve(f, C, lam):
+    """Dense float64 solve of (I + lam*L_w) u = f along axis 1 (C = -w)."""
+    h, w = f.shape
+    out = np.empty((h, w))
+    for i in range(h):
+        A = np.eye(w)
+        for j in range(w - 1):
+            wt = -float(C[i, j])
+            A[j, j] += lam * wt
+            A[j + 1, j + 1] += lam * wt
+            A[j, j + 1] -= lam * wt
+            A[j + 1, j] -= lam * wt
+        out[i] = np.linalg.solve(A, f[i].astype(np.float64))
+    return out
+
+
+def test_thomas_solves_fgs_system():
+    rng = np.random.default_rng(0)
+    g = rng.integers(0, 256, (6, 40))
+    tab = wls_np.weight_table(2.0)
+    C = np.zeros(g.shape, np.float32)
+    C[:, :-1] = tab[np.abs(np.diff(g, axis=1))]
+    f = rng.standard_normal(g.shape).astype(np.float32) * 100
+    u = f.copy()
+    wls_np._solve_rows([u], C, 50.0)
+    ref = _laplacian_solve(f, C, 50.0)
+    assert np.allclose(u, ref, rtol=1e-4, atol=1e-3)
+
+
+def test_weight_table():
+    t = wls_np.weight_table(1.2)
+    assert t.dtype == np.float32 and t[0] == -1.0
+    assert np.all(np.diff(t) >= 0) and np.all(np.diff(t[:80]) > 0) and t[-1] == 0
+
+
+@pytest.mark.parametrize("conf", [True, False])
+def test_constant_disparity_is_fixed_point(conf):
+    H, W, D = 30, 80, 16
+    displ = np.full((H, W), 5 * 16 + 3, np.int16)
+    displ[:, :D] = -16
+    dispr = np.full((H, W), -(5 * 16 + 3), np.int16)
+    guide = synthetic.random_dot_pair(H, W, D, seed=1)[0]
+    p = dict(lmbda=80000.0, sigma=1.2, radius=3, left_offset=D, use_confidence=conf)
+    out = wls_np.wls_filter(displ, guide, dispr if conf else None, p)
+    assert np.all(out[:, D:] == 5 * 16 + 3)
+    assert np.all(out[:, :D] == -16)
+
+
+def test_confidence_drops_at_discontinuities_and_lr_failures():
+    H, W = 20, 60
+    displ = np.full((H, W), 160, np.int16)
+    displ[:, 40:] = 480  # depth step
+    dispr = np.full((H, W), -160, np.int16)
+    p = wls_np.normalize_wls(dict(radius=2, left_offset=16), H, W)
+    conf = wls_np.confidence_map(displ, dispr, p)
+    assert conf[5, 20] == 255.0  # flat and LR-consistent
+    assert conf[5, 40] == 0.0  # variance of the step window >> 1/roll_off
+    # where dl = 480 the right view says -160: LR check fails → 0
+    assert np.all(conf[:, 43:] == 0.0)
+
+
+def test_fills_holes_inside_roi():
+    H, W, D = 24, 70, 16
+    displ = np.full((H, W), 8 * 16, np.int16)
+    displ[10:14, 30:36] = -16  # invalid hole
+    dispr = np.full((H, W), -8 * 16, np.int16)
+    guide = np.full((H, W), 100, np.uint8)
+    out = wls_np.wls_filter(displ, guide, dispr, dict(lmbda=8000.0, sigma=1.0, radius=3, left_offset=D))
+    assert np.all(np.abs(out[10:14, 30:36].astype(int) - 128) <= 2)
+
+
+def test_empty_roi_is_fill_only():
+    d = np.zeros((5, 20), np.int16)
+    out = wls_np.wls_filter(d, np.zeros((5, 20), np.uint8), d, dict(left_offset=20, min_disp=-3))
+    assert np.all(out == 16 * (-3 - 1))
+
+
+def test_golden_wls_fixtures_reproduce(golden_wls_cases):
+    for name, displ, dispr, guide, p, expected in golden_wls_cases:
+        assert np.array_equal(wls_np.wls_filter(displ, guide, dispr, p), expected), name
