@@ -35,8 +35,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default=None, choices=["kitti", "middlebury", "tsukuba", "mccnn"],
                     help="default: kitti (mccnn for --mode volume8)")
-    ap.add_argument("--mode", default="census8", choices=["census8", "sgbm5", "volume8"],
-                    help="census8 = headline; sgbm5 = OpenCV parity mode; volume8 = mc-cnn f32 cost volume")
+    ap.add_argument("--mode", default="census8", choices=["census8", "sgbm5", "volume8", "disparity5"],
+                    help="census8 = headline; sgbm5 = OpenCV parity mode; volume8 = mc-cnn f32 cost volume; "
+                         "disparity5 = the reference's whole compute_disparity (left + right SGBM + WLS)")
     ap.add_argument("--pairs-per-gpu", type=int, default=8)
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--row", action="store_true",
@@ -70,6 +71,7 @@ def main():
 
     H, W, D = synthetic.CONFIGS[args.config]
     volume = args.mode == "volume8"
+    full = args.mode == "disparity5"
     if args.mode == "census8":
         p = synthetic.headline_params(D)
     elif volume:
@@ -89,6 +91,12 @@ def main():
     dL = torch.tensor(np.stack(lefts), device=dev)
     dR = torch.tensor(np.stack(rights), device=dev)
     dOut = torch.empty((P, H, W), dtype=torch.int16, device=dev)
+    dOutR = dFilt = wprm = None
+    if full:  # compute_disparity: settings.ini lambda/sigma, createDisparityWLSFilter defaults
+        dOutR = torch.empty_like(dOut)
+        dFilt = torch.empty_like(dOut)
+        wprm = _lib.wls_default_params(prm)
+        wprm.lambda_, wprm.sigma_color = 80000.0, 1.2
     vols = None
     if volume:  # config C: (1, D, H, W) float32 cost per pair, resident in HBM
         vols = torch.empty((P, D, H, W), dtype=torch.float32, device=dev)
@@ -102,7 +110,10 @@ def main():
         eng.set_debug_flags(32)
 
     def step():
-        if volume:
+        if full:
+            eng.compute_disparity_batch_device(dL.data_ptr(), dR.data_ptr(), P, H * W, H, W, W, prm, wprm,
+                                               dOut.data_ptr(), dOutR.data_ptr(), dFilt.data_ptr())
+        elif volume:
             eng.aggregate_cost_f32_device(vols.data_ptr(), P, D * H * W, D, H, W, prm, 0.0, synthetic.VOLUME_SCALE,
                                           dOut.data_ptr())
         else:
@@ -148,7 +159,7 @@ def main():
         cells = H * W * D
         width1 = W - D
         vol = H * width1 * D
-        P_dirs = 5 if args.mode == "sgbm5" else 8
+        P_dirs = 5 if args.mode in ("sgbm5", "disparity5") else 8
         eb = 1 if args.mode == "census8" else 2  # bytes per path element
         row_mode = args.row and D % 64 == 0  # both horizontal paths fused into the row/WTA kernel
         census_b = 2 * H * W * 8 if args.mode == "census8" else 0
@@ -184,10 +195,14 @@ def main():
         # (mc-cnn f32 volume: H·W·D·(4·P + 8))
         if volume:
             survey_bytes = cells * (4 * P_dirs + 8)
+        elif full:  # two matcher runs (left, right) per pair; WLS traffic is O(H·W)
+            survey_bytes = 2 * (cells * (1 + P_dirs + 4) + 2 * H * W + 4 * H * W)
         else:
             survey_bytes = cells * (1 + P_dirs + 4) + 2 * H * W + 4 * H * W
         tot_ms, _, tot_pairs = stages["total"]
         pair_s = tot_ms / 1e3 / max(tot_pairs, 1)
+        if full:  # per reference pair: two matcher calls + the WLS filter
+            pair_s = (tot_ms + stages["wls"][0]) / 1e3 / max(stages["wls"][2], 1)
         line = {
             "metric": "stereo pairs/sec + Mpix·disp/sec, KITTI 1242×375 D=128 SGM, 1/2/4/8 GPU",
             "value": value,
@@ -199,13 +214,14 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": {"census8": "u8", "sgbm5": "i16", "volume8": "f32->u16"}[args.mode],
+            "dtype": {"census8": "u8", "sgbm5": "i16", "volume8": "f32->u16", "disparity5": "i16+f32"}[args.mode],
             "data": "synthetic random-dot pairs (no dataset in the image)"
                     + ("; f32 cost = 3x3-smoothed |L-R|/255 volume per pair" if volume else ""),
             "config": {
                 "workload": f"{args.config} {W}x{H} D={D} "
                             + {"census8": "census9x7 + 8-path SGM", "sgbm5": "OpenCV-SGBM 5-path",
-                               "volume8": "f32 cost volume (mc-cnn) + 8-path SGM"}[args.mode],
+                               "volume8": "f32 cost volume (mc-cnn) + 8-path SGM",
+                               "disparity5": "compute_disparity: left+right OpenCV-SGBM 5-path + WLS"}[args.mode],
                 "pairs_per_gpu": P, "global_batch": gpairs, "H": H, "W": W, "D": D,
                 "gather": world > 1 and not args.no_gather, "parallelism": f"pairs/dp{world}",
             },
@@ -223,7 +239,8 @@ def main():
                 "avg_launch_us": paths_avg_s * 1e6,
             },
             "pipeline_roofline": {
-                "model": "SURVEY §8d " + ("H·W·D·(4P+8)" if volume else "H·W·D·(1+P+4)+I/O") + " per pair",
+                "model": "SURVEY §8d " + ("H·W·D·(4P+8)" if volume else "H·W·D·(1+P+4)+I/O")
+                         + (" x2 matchers" if full else "") + " per pair",
                 "bytes_per_pair": survey_bytes,
                 "device_us_per_pair": pair_s * 1e6,
                 "achieved_GBs": survey_bytes / pair_s / 1e9 if pair_s > 0 else None,
@@ -233,13 +250,13 @@ def main():
             "valid_frac_pair0": valid_frac,
         }
         if world == 1 and args.cpu_baseline_pairs > 0:
-            line["cpu_baseline"] = cpu_baseline(args, H, W, D, p, lefts, rights, out0, volume)
+            line["cpu_baseline"] = cpu_baseline(args, H, W, D, p, lefts, rights, out0, volume, full)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
-def cpu_baseline(args, H, W, D, p, lefts, rights, out0, volume):
+def cpu_baseline(args, H, W, D, p, lefts, rights, out0, volume, full=False):
     """The C restatement (oracle/sgm_ref.c, -O3) on a bounded sample of the
     same workload: ``--cpu-threads`` host threads each running
     ``--cpu-baseline-pairs`` pairs concurrently (ctypes releases the GIL; the
@@ -258,6 +275,19 @@ def cpu_baseline(args, H, W, D, p, lefts, rights, out0, volume):
 
         def one(i):
             return ref_c.compute_volume(vol0, p, 0.0, synthetic.VOLUME_SCALE)
+    elif full:  # compute_disparity: C port for both matchers + the numpy WLS restatement
+        from oracle import sgm_np, wls_np
+        lp = dict(p, uniquenessRatio=0, disp12MaxDiff=1000000)
+        rp = sgm_np.right_matcher_params(p)
+        wp = dict(lmbda=80000.0, sigma=1.2, radius=(p["blockSize"] + 1) // 2, min_disp=p["minDisparity"],
+                  left_offset=max(0, p["minDisparity"] + D), right_offset=max(0, -p["minDisparity"]))
+        n = max(1, n // 4)
+
+        def one(i):
+            a, b = lefts[i % len(lefts)], rights[i % len(rights)]
+            dl = ref_c.compute(a, b, lp)
+            wls_np.wls_filter(dl, a, ref_c.compute(b, a, rp), wp)
+            return dl
     else:
         def one(i):
             return ref_c.compute(lefts[i % len(lefts)], rights[i % len(rights)], p)
@@ -281,7 +311,7 @@ def cpu_baseline(args, H, W, D, p, lefts, rights, out0, volume):
     for t in threads:
         t.join()
     dtT = time.perf_counter() - t0
-    what = "f32 cost volumes" if volume else "pairs"
+    what = "f32 cost volumes" if volume else ("pairs (left+right C port + numpy WLS)" if full else "pairs")
     return {
         "value": T * n / dtT,
         "unit": "pairs/s",

@@ -158,14 +158,16 @@ int sm_right_matcher_params(const sm_params* left, sm_params* right_out);
 int sm_synchronize(sm_ctx* ctx);
 
 /* Per-stage device timing with hipEvents on the context stream.
- * stage: 0 cost, 1 path aggregation, 2 WTA+LR, 3 median, 4 whole pipeline.
+ * stage: 0 cost, 1 path aggregation, 2 WTA+LR, 3 median, 4 whole matcher
+ * call, 5 WLS filter (confidence + smoother + final).
  * total_ms: summed duration; launches: timed launches; pairs: pairs they covered. */
 #define SM_STAGE_COST 0
 #define SM_STAGE_PATHS 1
 #define SM_STAGE_WTA 2
 #define SM_STAGE_MEDIAN 3
 #define SM_STAGE_TOTAL 4
-#define SM_NUM_STAGES 5
+#define SM_STAGE_WLS 5
+#define SM_NUM_STAGES 6
 int sm_set_timing(sm_ctx* ctx, int enable);
 int sm_get_timing(sm_ctx* ctx, int stage, double* total_ms, long long* launches, long long* pairs);
 int sm_reset_timing(sm_ctx* ctx);

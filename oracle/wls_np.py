@@ -26,8 +26,9 @@ published algorithm (version unpinned, OpenCV 3.3–3.4 era per SURVEY.md §8c):
 3. Fast global smoother (Min et al. 2014, ``fgs_filter.cpp``) over the ROI,
    guided by the left gray view: edge weights ``−exp(−|Δg|/σ)``, per
    iteration one horizontal and one vertical tridiagonal (Thomas) solve of
-   ``(I + λ·L_w) u = f``, ``λ *= 0.25`` per iteration, 3 iterations — run on
-   ``conf·disp`` and on ``conf``.
+   ``(I + λ·L_w) u = f`` (one reciprocal of the pivot per element, as
+   upstream's SIMD-friendly form), ``λ *= 0.25`` per iteration, 3 iterations
+   — run on ``conf·disp`` and on ``conf``.
 4. ``filtered = round_half_even(FGS(conf·disp) / FGS(conf))`` (0 where the
    denominator is 0, OpenCV 3.x ``divide``), saturated to int16, written
    into a map pre-filled with ``16·(minDisparity − 1)``.
@@ -112,21 +113,26 @@ def confidence_map(displ, dispr, p):
 
 def _solve_rows(u_list, C, lam):
     """Thomas solve along axis 1 for every row; C[:, j] couples j and j+1
-    (C[:, -1] == 0).  Fixed float32 op order (see module doc)."""
+    (C[:, -1] == 0).  Fixed float32 op order, one reciprocal per element:
+    r = 1/(1 − λ(C[j−1]+C[j]) − λC[j−1]·c'[j−1]); c'[j] = λC[j]·r;
+    d'[j] = (f[j] − λC[j−1]·d'[j−1])·r; x[j] = d'[j] − c'[j]·x[j+1]."""
     lam = f32(lam)
     h, w = C.shape
     inter = np.empty((h, w), np.float32)
-    denom = f32(1.0) - lam * C[:, 0]
-    inter[:, 0] = (lam * C[:, 0]) / denom
-    for u in u_list:
-        u[:, 0] = u[:, 0] / denom
-    for j in range(1, w):
-        cp, cj = C[:, j - 1], C[:, j]
+    ip = np.zeros(h, np.float32)
+    cp = np.zeros(h, np.float32)
+    prev = [np.zeros(h, np.float32) for _ in u_list]
+    for j in range(w):
+        cj = C[:, j]
         t = f32(1.0) - lam * (cp + cj)
-        denom = t - (lam * cp) * inter[:, j - 1]
-        inter[:, j] = (lam * cj) / denom
-        for u in u_list:
-            u[:, j] = (u[:, j] - (lam * cp) * u[:, j - 1]) / denom
+        lcp = lam * cp
+        r = f32(1.0) / (t - lcp * ip)
+        ip = (lam * cj) * r
+        inter[:, j] = ip
+        for k, u in enumerate(u_list):
+            prev[k] = (u[:, j] - lcp * prev[k]) * r
+            u[:, j] = prev[k]
+        cp = cj
     for j in range(w - 2, -1, -1):
         for u in u_list:
             u[:, j] = u[:, j] - inter[:, j] * u[:, j + 1]

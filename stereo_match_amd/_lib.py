@@ -20,7 +20,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "stereo_match_amd.
 SM_OK, SM_E_ARG, SM_E_HIP, SM_E_UNSUPPORTED = 0, -1, -2, -4
 SM_COST_SGBM, SM_COST_CENSUS, SM_COST_VOLUME = 0, 1, 2
 SM_MODE_SGBM, SM_MODE_HH = 5, 8
-STAGES = ("cost", "paths", "wta", "median", "total")
+STAGES = ("cost", "paths", "wta", "median", "total", "wls")
 
 
 class SmParams(ctypes.Structure):
@@ -108,6 +108,23 @@ def header_symbols(path: str = HEADER_PATH):
     return sorted(set(re.findall(r"^\s*(?:const\s+)?[\w\s\*]*?\b(sm_\w+)\s*\(", text, flags=re.M)))
 
 
+def _init_torch_hip_first():
+    """torch wheels bundle their own libamdhip64; our library links ROCm's.
+    Both runtimes can live in one process, but on the MI355X boxes torch's
+    reports "No HIP GPUs are available" if ROCm's was initialised first.  So
+    when torch is installed, bring its runtime up before ours (device
+    enumeration only; no context is created on any device)."""
+    try:
+        import torch
+    except Exception:  # torch absent: nothing to order
+        return
+    try:
+        if getattr(torch.version, "hip", None):
+            torch.cuda.is_available()
+    except Exception:
+        pass
+
+
 def load():
     """Load the HIP library (fails loudly if it has not been built)."""
     global _lib
@@ -119,6 +136,7 @@ def load():
                 f"{LIB_PATH} is missing: build it with `make -C stereo_match_amd/csrc` "
                 "(or python -c 'import __graft_entry__ as g; g.build()'). "
                 "There is no CPU fallback.")
+        _init_torch_hip_first()
         lib = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in _SIGS.items():
             fn = getattr(lib, name)

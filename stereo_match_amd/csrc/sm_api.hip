@@ -70,7 +70,7 @@ struct sm_ctx {
     hipStream_t stream = nullptr;  // stream A
     hipStream_t side = nullptr;    // stream B
     DevBuf img[2], planes, out, dbg, volbuf;
-    DevBuf wls_num, wls_den, wls_inter, wls_disp[2], wls_out;  // WLS scratch
+    DevBuf wls_num, wls_den, wls_inter, wls_w, wls_disp[2], wls_out;  // WLS scratch
     BufSet set[2];
     int next_set = 0;
     // geometry of the last computation (for sm_debug_fetch): its last pair
@@ -619,15 +619,20 @@ int run_wls(sm_ctx* ctx, const int16_t* dl, const int16_t* dr, size_t disp_pair,
 {
     if (npairs <= 0) return SM_OK;
     const bool roi = n.w > 0 && n.h > 0;
-    const size_t roi_elems = roi ? (size_t)n.w * n.h : 0;
-    // scratch: num, den, inter floats per pair
-    const int G = (int)std::max<size_t>(1, std::min<size_t>(npairs, (size_t(6) << 30) / std::max<size_t>(roi_elems * 12, 1)));
+    const int wp = roi ? (n.w + smk::FT - 1) / smk::FT * smk::FT : 0;
+    const int hp = roi ? (n.h + smk::FT - 1) / smk::FT * smk::FT : 0;
+    const size_t roi_elems = (size_t)wp * hp;
+    // scratch: num, den, inter, Ch, Cv floats per pair
+    const int G = (int)std::max<size_t>(
+        1, std::min<size_t>(npairs, (size_t(6) << 30) / std::max<size_t>(roi_elems * 20, 1)));
     int rc;
     if (roi) {
         if ((rc = ensure(ctx, ctx->wls_num, (size_t)G * roi_elems * 4)) != SM_OK) return rc;
         if ((rc = ensure(ctx, ctx->wls_den, (size_t)G * roi_elems * 4)) != SM_OK) return rc;
         if ((rc = ensure(ctx, ctx->wls_inter, (size_t)G * roi_elems * 4)) != SM_OK) return rc;
+        if ((rc = ensure(ctx, ctx->wls_w, (size_t)G * roi_elems * 8)) != SM_OK) return rc;
     }
+    StageTimer t(ctx, ctx->stream, SM_STAGE_WLS, npairs);
     for (int p0 = 0; p0 < npairs; p0 += G) {
         const int g = std::min(G, npairs - p0);
         if (roi) {
@@ -635,8 +640,13 @@ int run_wls(sm_ctx* ctx, const int16_t* dl, const int16_t* dr, size_t disp_pair,
             ca.dl = dl + (size_t)p0 * disp_pair;
             ca.dr = dr ? dr + (size_t)p0 * disp_pair : nullptr;
             ca.disp_pair = disp_pair;
+            ca.guide = guide + (size_t)p0 * guide_pair;
+            ca.guide_pair = guide_pair;
+            ca.guide_stride = guide_stride;
             ca.num = (float*)ctx->wls_num.p;
             ca.den = (float*)ctx->wls_den.p;
+            ca.Ch = (float*)ctx->wls_w.p;
+            ca.Cv = (float*)ctx->wls_w.p + (size_t)G * roi_elems;
             ca.roi_pair = roi_elems;
             ca.H = H;
             ca.W = W;
@@ -644,34 +654,37 @@ int run_wls(sm_ctx* ctx, const int16_t* dl, const int16_t* dr, size_t disp_pair,
             ca.y0 = n.y0;
             ca.w = n.w;
             ca.h = n.h;
+            ca.wp = wp;
             ca.rx0 = n.rx0;
             ca.radius = n.radius;
             ca.lrc_thresh = n.lrc;
             ca.roll_off = n.roll_off;
             ca.use_confidence = n.use_conf;
-            hipLaunchKernelGGL(smk::k_wls_conf, dim3(n.h, g), dim3(256), (size_t)n.w * 4, ctx->stream, ca);
+            std::memcpy(ca.tab, n.tab, sizeof ca.tab);
+            hipLaunchKernelGGL(smk::k_wls_conf, dim3(hp, g), dim3(256), (size_t)(256 + n.w) * 4, ctx->stream, ca);
             HIP_TRY(ctx, hipGetLastError());
             smk::FgsArgs fa{};
-            fa.u[0] = (float*)ctx->wls_num.p;
-            fa.u[1] = (float*)ctx->wls_den.p;
+            fa.u[0] = ca.num;
+            fa.u[1] = ca.den;
             fa.inter = (float*)ctx->wls_inter.p;
             fa.roi_pair = roi_elems;
-            fa.guide = guide + (size_t)p0 * guide_pair + (size_t)n.y0 * guide_stride + n.x0;
-            fa.guide_pair = guide_pair;
-            fa.guide_stride = guide_stride;
             fa.w = n.w;
             fa.h = n.h;
-            std::memcpy(fa.tab, n.tab, sizeof fa.tab);
+            fa.wp = wp;
+            fa.dbg = ctx->dbg_flags;
             float lam = n.lam;
             for (int it = 0; it < n.num_iter; it++) {
                 fa.lam = lam;
-                if (n.use_conf) {
-                    hipLaunchKernelGGL((smk::k_fgs<2, true>), dim3((n.h + 63) / 64, g), dim3(64), 0, ctx->stream, fa);
-                    hipLaunchKernelGGL((smk::k_fgs<2, false>), dim3((n.w + 63) / 64, g), dim3(64), 0, ctx->stream, fa);
-                } else {
-                    hipLaunchKernelGGL((smk::k_fgs<1, true>), dim3((n.h + 63) / 64, g), dim3(64), 0, ctx->stream, fa);
-                    hipLaunchKernelGGL((smk::k_fgs<1, false>), dim3((n.w + 63) / 64, g), dim3(64), 0, ctx->stream, fa);
-                }
+                fa.C = ca.Ch;
+                if (n.use_conf)
+                    hipLaunchKernelGGL((smk::k_fgs<2, true>), dim3(hp / smk::FT, g), dim3(64), 0, ctx->stream, fa);
+                else
+                    hipLaunchKernelGGL((smk::k_fgs<1, true>), dim3(hp / smk::FT, g), dim3(64), 0, ctx->stream, fa);
+                fa.C = ca.Cv;
+                if (n.use_conf)
+                    hipLaunchKernelGGL((smk::k_fgs<2, false>), dim3(wp / smk::FT, g), dim3(64), 0, ctx->stream, fa);
+                else
+                    hipLaunchKernelGGL((smk::k_fgs<1, false>), dim3(wp / smk::FT, g), dim3(64), 0, ctx->stream, fa);
                 HIP_TRY(ctx, hipGetLastError());
                 lam = lam * n.att;
             }
@@ -688,6 +701,7 @@ int run_wls(sm_ctx* ctx, const int16_t* dl, const int16_t* dr, size_t disp_pair,
         wa.y0 = n.y0;
         wa.w = roi ? n.w : 0;
         wa.h = roi ? n.h : 0;
+        wa.wp = wp;
         wa.fill = n.fill;
         wa.use_confidence = n.use_conf;
         hipLaunchKernelGGL(smk::k_wls_final, dim3((W + 255) / 256, H, g), dim3(256), 0, ctx->stream, wa);
@@ -730,7 +744,7 @@ void sm_destroy(sm_ctx* ctx)
     (void)hipSetDevice(ctx->device);
     (void)hipDeviceSynchronize();
     DevBuf* bufs[] = {&ctx->img[0],  &ctx->img[1],  &ctx->planes,    &ctx->out,         &ctx->dbg,
-                      &ctx->volbuf,  &ctx->wls_num, &ctx->wls_den,   &ctx->wls_inter,   &ctx->wls_disp[0],
+                      &ctx->volbuf,  &ctx->wls_num, &ctx->wls_den,   &ctx->wls_inter,   &ctx->wls_disp[0], &ctx->wls_w,
                       &ctx->wls_disp[1], &ctx->wls_out};
     for (DevBuf* b : bufs)
         if (b->p) (void)hipFree(b->p);

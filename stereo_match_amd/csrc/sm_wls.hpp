@@ -2,40 +2,54 @@
 // FastGlobalSmootherFilter) for gfx950.  SURVEY §8 f1; reference call:
 // stereo_vision/stereo_vision.py:172-182.  Semantics: oracle/wls_np.py.
 //
-// Per launch group of G pairs:
-//   k_wls_conf  one workgroup per (ROI row, pair): depth-discontinuity
+// Per launch group of G pairs (ROI arrays padded to hp x wp, multiples of 64,
+// so every 64x64 tile access below is in bounds and 16-byte aligned):
+//   k_wls_conf  one workgroup per (padded ROI row, pair): depth-discontinuity
 //               confidence of the right row into LDS, then the left ROI row:
 //               its own confidence, the discontinuity-aware LR check, x255,
-//               and the two FGS right-hand sides num = conf*disp, den = conf.
-//   k_fgs_rows  one lane per (ROI row, pair): Thomas solve along x for both
-//               right-hand sides (they share the elimination factors).
-//   k_fgs_cols  one lane per (ROI column, pair): the same along y
-//               (coalesced: neighbouring lanes = neighbouring columns).
+//               the two FGS right-hand sides num = conf*disp, den = conf, and
+//               the smoother's edge weights Ch (to x+1) and Cv (to y+1) from
+//               the guide.  Padding is written as zeros.
+//   k_fgs<ROWS> 64 lines per one-wave workgroup, one line per lane: Thomas
+//               solve along the line for both right-hand sides (they share
+//               the elimination factors).  ROWS: lines = ROI rows; else
+//               lines = ROI columns.
 //   k_wls_final num/den (0 where den == 0), round-half-even, saturate int16,
 //               fill 16*(min_disp-1) outside the ROI.
 // Everything is float32 in the oracle's operation order with FP contraction
-// off, so results are bit-identical to oracle/wls_np.py.  The sequential
-// solves are latency-bound (one dependent divide per element); their
-// parallelism is rows x pairs, which is why they run on whole launch groups.
+// off, so results are bit-identical to oracle/wls_np.py.  The solves are
+// latency-bound (a dependent reciprocal per element); their parallelism is
+// lines x pairs, which is why they run on whole launch groups and why the
+// tile traffic is prefetched a chunk ahead.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "sm_common.hpp"
+
 namespace smk {
+
+constexpr int FT = 64, FP = 65;  // tile edge, LDS pitch (conflict-free both ways)
 
 struct WlsConfArgs {
     const int16_t* dl;  // [pair][H][W]
     const int16_t* dr;
     size_t disp_pair;  // elements between pairs
-    float* num;        // [pair][h][w]
+    const uint8_t* guide;
+    size_t guide_pair;  // bytes between pairs
+    int guide_stride;
+    float* num;  // [pair][hp][wp]
     float* den;
-    size_t roi_pair;  // elements between pairs (h*w)
+    float* Ch;
+    float* Cv;
+    size_t roi_pair;  // hp*wp
     int H, W;
-    int x0, y0, w, h;  // left ROI
-    int rx0;           // right ROI x (same y0, w, h)
+    int x0, y0, w, h, wp;  // left ROI, padded pitch
+    int rx0;               // right ROI x (same y0, w, h)
     int radius, lrc_thresh;
     float roll_off;
     int use_confidence;
+    float tab[256];  // -exp(-k / sigma), k = |delta guide|
 };
 
 __device__ inline int reflect101(int i, int n)
@@ -71,16 +85,44 @@ __device__ inline float discontinuity_conf(const int16_t* __restrict__ d, int H,
 __global__ void __launch_bounds__(256) k_wls_conf(WlsConfArgs a)
 {
 #pragma clang fp contract(off)
-    extern __shared__ float confr[];  // right-view confidence of this row, [W]
+    extern __shared__ uint32_t smem[];  // tab[256], right-view confidence of this row [w]
+    float* tab = reinterpret_cast<float*>(smem);
+    float* confr = tab + 256;
+    for (int i = threadIdx.x; i < 256; i += 256) tab[i] = a.tab[i];
     const int yr = blockIdx.x, pair = blockIdx.y;
+    const size_t ro = pair * a.roi_pair + (size_t)yr * a.wp;
+    float* num = a.num + ro;
+    float* den = a.den + ro;
+    float* Ch = a.Ch + ro;
+    float* Cv = a.Cv + ro;
+    if (yr >= a.h) {  // padding row
+        for (int j = threadIdx.x; j < a.wp; j += 256) num[j] = den[j] = Ch[j] = Cv[j] = 0.f;
+        return;
+    }
     const int y = a.y0 + yr;
     const int16_t* dl = a.dl + pair * a.disp_pair;
     const int16_t* dr = a.dr + pair * a.disp_pair;
-    float* num = a.num + pair * a.roi_pair + (size_t)yr * a.w;
-    float* den = a.den + pair * a.roi_pair + (size_t)yr * a.w;
+    const uint8_t* g = a.guide + pair * a.guide_pair + (size_t)y * a.guide_stride + a.x0;
     const int16_t* dlrow = dl + (size_t)y * a.W;
+    __syncthreads();
+    for (int j = threadIdx.x; j < a.wp; j += 256) {  // smoother weights
+        float ch = 0.f, cv = 0.f;
+        if (j < a.w) {
+            const int g0 = g[j];
+            if (j < a.w - 1) {
+                const int d = (int)g[j + 1] - g0;
+                ch = tab[d < 0 ? -d : d];
+            }
+            if (yr < a.h - 1) {
+                const int d = (int)g[j + a.guide_stride] - g0;
+                cv = tab[d < 0 ? -d : d];
+            }
+        }
+        Ch[j] = ch;
+        Cv[j] = cv;
+    }
     if (!a.use_confidence) {
-        for (int j = threadIdx.x; j < a.w; j += 256) num[j] = (float)dlrow[a.x0 + j];
+        for (int j = threadIdx.x; j < a.wp; j += 256) num[j] = j < a.w ? (float)dlrow[a.x0 + j] : 0.f;
         return;
     }
     const double scale = 1.0 / (double)((2 * a.radius + 1) * (2 * a.radius + 1));
@@ -88,7 +130,11 @@ __global__ void __launch_bounds__(256) k_wls_conf(WlsConfArgs a)
         confr[j] = discontinuity_conf(dr, a.H, a.W, y, a.rx0 + j, a.radius, scale, a.roll_off);
     __syncthreads();
     const int16_t* drrow = dr + (size_t)y * a.W;
-    for (int j = threadIdx.x; j < a.w; j += 256) {
+    for (int j = threadIdx.x; j < a.wp; j += 256) {
+        if (j >= a.w) {
+            num[j] = den[j] = 0.f;
+            continue;
+        }
         const int X = a.x0 + j;
         float c = discontinuity_conf(dl, a.H, a.W, y, X, a.radius, scale, a.roll_off);
         const int d = dlrow[X];
@@ -104,82 +150,212 @@ __global__ void __launch_bounds__(256) k_wls_conf(WlsConfArgs a)
 }
 
 struct FgsArgs {
-    float* u[2];  // right-hand sides, [pair][h][w], solved in place
-    float* inter;  // elimination factors, [pair][h][w]
+    float* u[2];  // right-hand sides, [pair][hp][wp], solved in place
+    float* inter;  // elimination factors, [pair][hp][wp]
+    const float* C;  // edge weights along the solve direction (Ch or Cv)
     size_t roi_pair;
-    const uint8_t* guide;  // [pair] gray left view; ROI origin already applied
-    size_t guide_pair;
-    int guide_stride;
-    int w, h;
+    int w, h, wp;
     float lam;
-    float tab[256];  // -exp(-k / sigma), k = |delta guide|
+    int dbg;  // timing ablations: 128 skip the sweeps, 256 skip global loads/stores
 };
 
-// Thomas solve of (I + lam*L_w) u = f along one line of n samples.
-// P(i) = element offset of sample i, G(i) = guide offset of sample i.
-template <int NRHS>
-__device__ inline void fgs_line(const FgsArgs& a, const float* tab, float* __restrict__ u0, float* __restrict__ u1,
-                                float* __restrict__ inter, const uint8_t* __restrict__ g, size_t step, size_t gstep,
-                                int n)
+// Thomas solve of (I + lam*L_w) u = f along lines, 64 lines per workgroup
+// (one wave, one line per lane):
+//   forward   r = 1/(1 - lam(C[j-1]+C[j]) - lam C[j-1] c'[j-1]),
+//             c'[j] = lam C[j] r,  d'[j] = (f[j] - lam C[j-1] d'[j-1]) r
+//   backward  x[j] = d'[j] - c'[j] x[j+1]
+// The recurrence is serial along a line, so lines are staged through LDS in
+// 64x64 tiles.  Tile traffic uses float4 accesses on the padded arrays
+// (ROWS: 16 lanes cover one line's 64 positions; columns: 16 lanes cover 64
+// lines of one position), and the next chunk's tiles are loaded into
+// registers while the current chunk is swept, so the per-chunk memory latency
+// hides behind the dependent reciprocal chain.  Zero-initialised carries
+// reproduce the oracle's first-element formulas exactly (x - 0*0 == x).
+template <bool ROWS>
+struct TileMap {
+    // load k (0..15) of lane -> local (line, pos) of the float4's first element;
+    // the float4 runs along pos (ROWS) or along line (columns)
+    __device__ static void at(int k, int lane, int& ll, int& pl)
+    {
+        if (ROWS) {
+            ll = 4 * k + (lane >> 4);
+            pl = (lane & 15) * 4;
+        } else {
+            pl = 4 * k + (lane >> 4);
+            ll = (lane & 15) * 4;
+        }
+    }
+    __device__ static int tix(int ll, int pl) { return ROWS ? ll * FP + pl : pl * FP + ll; }
+    __device__ static int tix_e(int ll, int pl, int e) { return ROWS ? tix(ll, pl + e) : tix(ll + e, pl); }
+    __device__ static size_t eoff(int line, int pos, int wp)
+    {
+        return ROWS ? (size_t)line * wp + pos : (size_t)pos * wp + line;
+    }
+};
+
+// Tile I/O through raw buffer ops: the per-lane byte offset of load k = 0 is
+// in a VGPR; load k adds k*16*wp bytes (4 lines for ROWS, 4 positions for
+// columns — the same stride) as a scalar offset, so the 16 accesses of a
+// tile cost no extra address registers.
+template <bool ROWS>
+__device__ inline uint32_t tile_voff(int l0, int j0, int wp, int lane)
 {
-#pragma clang fp contract(off)
-    const float lam = a.lam;
-    auto C = [&](int i) -> float {
-        if (i >= n - 1) return 0.0f;
-        const int d = (int)g[(size_t)(i + 1) * gstep] - (int)g[(size_t)i * gstep];
-        return tab[d < 0 ? -d : d];
-    };
-    float cp = C(0);
-    float denom = 1.0f - lam * cp;
-    float ip = (lam * cp) / denom;
-    inter[0] = ip;
-    float p0 = u0[0] / denom, p1 = 0.f;
-    u0[0] = p0;
-    if (NRHS == 2) {
-        p1 = u1[0] / denom;
-        u1[0] = p1;
-    }
-    for (int i = 1; i < n; i++) {
-        const float cj = C(i);
-        const float t = 1.0f - lam * (cp + cj);
-        const float lcp = lam * cp;
-        denom = t - lcp * ip;
-        ip = (lam * cj) / denom;
-        inter[(size_t)i * step] = ip;
-        p0 = (u0[(size_t)i * step] - lcp * p0) / denom;
-        u0[(size_t)i * step] = p0;
-        if (NRHS == 2) {
-            p1 = (u1[(size_t)i * step] - lcp * p1) / denom;
-            u1[(size_t)i * step] = p1;
-        }
-        cp = cj;
-    }
-    for (int i = n - 2; i >= 0; i--) {
-        const float f = inter[(size_t)i * step];
-        p0 = u0[(size_t)i * step] - f * p0;
-        u0[(size_t)i * step] = p0;
-        if (NRHS == 2) {
-            p1 = u1[(size_t)i * step] - f * p1;
-            u1[(size_t)i * step] = p1;
-        }
+    int ll, pl;
+    TileMap<ROWS>::at(0, lane, ll, pl);
+    return (uint32_t)(TileMap<ROWS>::eoff(l0 + ll, j0 + pl, wp) * 4);
+}
+
+template <bool ROWS>
+__device__ inline void tile_load(float4 (&r)[16], rsrc_t rs, uint32_t voff, int wp)
+{
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, k * 16 * wp, 0);
+        r[k] = make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
     }
 }
 
-// ROWS: one lane per ROI row (solve along x); else one lane per ROI column.
+template <bool ROWS>
+__device__ inline void tile_to_lds(const float4 (&r)[16], float* T, int lane)
+{
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        int ll, pl;
+        TileMap<ROWS>::at(k, lane, ll, pl);
+        T[TileMap<ROWS>::tix_e(ll, pl, 0)] = r[k].x;
+        T[TileMap<ROWS>::tix_e(ll, pl, 1)] = r[k].y;
+        T[TileMap<ROWS>::tix_e(ll, pl, 2)] = r[k].z;
+        T[TileMap<ROWS>::tix_e(ll, pl, 3)] = r[k].w;
+    }
+}
+
+template <bool ROWS>
+__device__ inline void tile_store(rsrc_t rs, uint32_t voff, const float* T, int wp, int lane)
+{
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        int ll, pl;
+        TileMap<ROWS>::at(k, lane, ll, pl);
+        u32x4 v;
+        v[0] = __float_as_uint(T[TileMap<ROWS>::tix_e(ll, pl, 0)]);
+        v[1] = __float_as_uint(T[TileMap<ROWS>::tix_e(ll, pl, 1)]);
+        v[2] = __float_as_uint(T[TileMap<ROWS>::tix_e(ll, pl, 2)]);
+        v[3] = __float_as_uint(T[TileMap<ROWS>::tix_e(ll, pl, 3)]);
+        __builtin_amdgcn_raw_buffer_store_b128(v, rs, voff, k * 16 * wp, 0);
+    }
+}
+
 template <int NRHS, bool ROWS>
 __global__ void __launch_bounds__(64) k_fgs(FgsArgs a)
 {
-    __shared__ float tab[256];
-    for (int i = threadIdx.x; i < 256; i += 64) tab[i] = a.tab[i];
-    __syncthreads();
-    const int line = blockIdx.x * 64 + threadIdx.x, pair = blockIdx.y;
-    if (line >= (ROWS ? a.h : a.w)) return;
-    const size_t base = pair * a.roi_pair + (ROWS ? (size_t)line * a.w : (size_t)line);
-    const uint8_t* g = a.guide + pair * a.guide_pair + (ROWS ? (size_t)line * a.guide_stride : (size_t)line);
-    const size_t step = ROWS ? 1 : (size_t)a.w;
-    const size_t gstep = ROWS ? 1 : (size_t)a.guide_stride;
-    fgs_line<NRHS>(a, tab, a.u[0] + base, NRHS == 2 ? a.u[1] + base : nullptr, a.inter + base, g, step, gstep,
-                   ROWS ? a.w : a.h);
+#pragma clang fp contract(off)
+    __shared__ float Ct[FT * FP], U0[FT * FP], U1[NRHS == 2 ? FT * FP : 1], IT[FT * FP];
+    const int lane = threadIdx.x, pair = blockIdx.y;
+    const int n = ROWS ? a.w : a.h;
+    const int l0 = blockIdx.x * FT, wp = a.wp;
+    const uint64_t bytes = a.roi_pair * 4;
+    const rsrc_t u0 = make_rsrc(a.u[0] + pair * a.roi_pair, bytes);
+    const rsrc_t u1 = make_rsrc(a.u[NRHS == 2 ? 1 : 0] + pair * a.roi_pair, bytes);
+    const rsrc_t inter = make_rsrc(a.inter + pair * a.roi_pair, bytes);
+    const rsrc_t C = make_rsrc(a.C + pair * a.roi_pair, bytes);
+    // byte offset of chunk c's first access: ROWS advance 64 positions (256 B),
+    // columns advance 64 rows
+    const uint32_t voff0 = tile_voff<ROWS>(l0, 0, wp, lane);
+    const uint32_t cstep = ROWS ? FT * 4 : (uint32_t)FT * wp * 4;
+    const bool mem = !(a.dbg & 256), sweep = !(a.dbg & 128);
+    const float lam = a.lam;
+    const int nchunks = (n + FT - 1) / FT;
+    float4 rc[16], r0[16], r1[16];
+    if (mem) {
+        tile_load<ROWS>(rc, C, voff0, wp);
+        tile_load<ROWS>(r0, u0, voff0, wp);
+        if (NRHS == 2) tile_load<ROWS>(r1, u1, voff0, wp);
+        tile_to_lds<ROWS>(rc, Ct, lane);
+        tile_to_lds<ROWS>(r0, U0, lane);
+        if (NRHS == 2) tile_to_lds<ROWS>(r1, U1, lane);
+    }
+    float ip = 0.f, p0 = 0.f, p1 = 0.f, cp = 0.f;
+    for (int c = 0; c < nchunks; c++) {
+        const int j0 = c * FT;
+        const bool next = c + 1 < nchunks;
+        __syncthreads();
+        if (mem && next) {  // prefetch chunk c+1 (consumed after the sweep)
+            const uint32_t vn = voff0 + (c + 1) * cstep;
+            tile_load<ROWS>(rc, C, vn, wp);
+            tile_load<ROWS>(r0, u0, vn, wp);
+            if (NRHS == 2) tile_load<ROWS>(r1, u1, vn, wp);
+        }
+        const int m = sweep ? min(FT, n - j0) : 0;
+        for (int jj = 0; jj < m; jj++) {
+            const int t = TileMap<ROWS>::tix(lane, jj);
+            const float cj = Ct[t];
+            const float tt = 1.0f - lam * (cp + cj);
+            const float lcp = lam * cp;
+            const float r = 1.0f / (tt - lcp * ip);
+            ip = (lam * cj) * r;
+            IT[t] = ip;
+            p0 = (U0[t] - lcp * p0) * r;
+            U0[t] = p0;
+            if (NRHS == 2) {
+                p1 = (U1[t] - lcp * p1) * r;
+                U1[t] = p1;
+            }
+            cp = cj;
+        }
+        __syncthreads();
+        if (mem) {
+            const uint32_t vc = voff0 + c * cstep;
+            tile_store<ROWS>(u0, vc, U0, wp, lane);
+            if (NRHS == 2) tile_store<ROWS>(u1, vc, U1, wp, lane);
+            tile_store<ROWS>(inter, vc, IT, wp, lane);
+            if (next) {
+                __syncthreads();
+                tile_to_lds<ROWS>(rc, Ct, lane);
+                tile_to_lds<ROWS>(r0, U0, lane);
+                if (NRHS == 2) tile_to_lds<ROWS>(r1, U1, lane);
+            }
+        }
+    }
+    // backward substitution; the last chunk's d' and c' are still in LDS
+    for (int c = nchunks - 1; c >= 0; c--) {
+        const int j0 = c * FT;
+        const bool prev = c > 0;
+        __syncthreads();
+        if (mem && prev) {
+            const uint32_t vp = voff0 + (c - 1) * cstep;
+            tile_load<ROWS>(rc, inter, vp, wp);
+            tile_load<ROWS>(r0, u0, vp, wp);
+            if (NRHS == 2) tile_load<ROWS>(r1, u1, vp, wp);
+        }
+        const int m = sweep ? min(FT, n - j0) : 0;
+        for (int jj = m - 1; jj >= 0; jj--) {
+            const int t = TileMap<ROWS>::tix(lane, jj);
+            if (c == nchunks - 1 && jj == m - 1) {  // x[n-1] = d'[n-1]
+                p0 = U0[t];
+                if (NRHS == 2) p1 = U1[t];
+                continue;
+            }
+            const float f = IT[t];
+            p0 = U0[t] - f * p0;
+            U0[t] = p0;
+            if (NRHS == 2) {
+                p1 = U1[t] - f * p1;
+                U1[t] = p1;
+            }
+        }
+        __syncthreads();
+        if (mem) {
+            const uint32_t vc = voff0 + c * cstep;
+            tile_store<ROWS>(u0, vc, U0, wp, lane);
+            if (NRHS == 2) tile_store<ROWS>(u1, vc, U1, wp, lane);
+            if (prev) {
+                __syncthreads();
+                tile_to_lds<ROWS>(rc, IT, lane);
+                tile_to_lds<ROWS>(r0, U0, lane);
+                if (NRHS == 2) tile_to_lds<ROWS>(r1, U1, lane);
+            }
+        }
+    }
 }
 
 struct WlsFinalArgs {
@@ -188,7 +364,7 @@ struct WlsFinalArgs {
     size_t roi_pair;
     int16_t* out;  // [pair][H][W]
     size_t out_pair;
-    int H, W, x0, y0, w, h;
+    int H, W, x0, y0, w, h, wp;
     int fill;  // 16*(min_disp-1)
     int use_confidence;
 };
@@ -200,7 +376,7 @@ __global__ void __launch_bounds__(256) k_wls_final(WlsFinalArgs a)
     int v = a.fill;
     const int j = x - a.x0, i = y - a.y0;
     if (j >= 0 && j < a.w && i >= 0 && i < a.h) {
-        const size_t o = pair * a.roi_pair + (size_t)i * a.w + j;
+        const size_t o = pair * a.roi_pair + (size_t)i * a.wp + j;
         float q = a.num[o];
         if (a.use_confidence) {
             const float dd = a.den[o];
