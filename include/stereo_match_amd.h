@@ -49,7 +49,7 @@ typedef struct sm_params {
     int disp12_max_diff;
     int uniqueness_ratio;
     int pre_filter_cap;
-    int speckle_window_size; /* must be 0 on the GPU path for now (SM_E_UNSUPPORTED) */
+    int speckle_window_size; /* > 0: cv::filterSpeckles after the median (maxSpeckleSize) */
     int speckle_range;
     int cost_kind; /* SM_COST_* */
     int mode;      /* SM_MODE_SGBM | SM_MODE_HH */
@@ -150,6 +150,14 @@ int sm_compute_disparity_batch_device(sm_ctx* ctx, const uint8_t* d_left, const 
                                       const sm_wls_params* wls, int16_t* d_displ, int16_t* d_dispr,
                                       int16_t* d_filtered);
 
+/* cv::filterSpeckles(img, newVal, maxSpeckleSize, maxDiff) in place on an
+ * int16 map (what StereoSGBM::compute applies when speckleWindowSize > 0,
+ * with newVal = 16*(minD-1), maxDiff = 16*speckleRange).  Host version is
+ * synchronous; the device version filters nimg maps at d_img + i*H*W. */
+int sm_filter_speckles(sm_ctx* ctx, int16_t* img, int H, int W, int new_val, int max_speckle_size, int max_diff);
+int sm_filter_speckles_device(sm_ctx* ctx, int16_t* d_img, int nimg, int H, int W, int new_val,
+                              int max_speckle_size, int max_diff);
+
 /* ximgproc::createRightMatcher(StereoSGBM) parameter derivation
  * (reference call: stereo_vision/stereo_vision.py:171). */
 int sm_right_matcher_params(const sm_params* left, sm_params* right_out);
@@ -159,7 +167,7 @@ int sm_synchronize(sm_ctx* ctx);
 
 /* Per-stage device timing with hipEvents on the context stream.
  * stage: 0 cost, 1 path aggregation, 2 WTA+LR, 3 median, 4 whole matcher
- * call, 5 WLS filter (confidence + smoother + final).
+ * call, 5 WLS filter (confidence + smoother + final), 6 speckle filter.
  * total_ms: summed duration; launches: timed launches; pairs: pairs they covered. */
 #define SM_STAGE_COST 0
 #define SM_STAGE_PATHS 1
@@ -167,7 +175,8 @@ int sm_synchronize(sm_ctx* ctx);
 #define SM_STAGE_MEDIAN 3
 #define SM_STAGE_TOTAL 4
 #define SM_STAGE_WLS 5
-#define SM_NUM_STAGES 6
+#define SM_STAGE_SPECKLE 6
+#define SM_NUM_STAGES 7
 int sm_set_timing(sm_ctx* ctx, int enable);
 int sm_get_timing(sm_ctx* ctx, int stage, double* total_ms, long long* launches, long long* pairs);
 int sm_reset_timing(sm_ctx* ctx);

@@ -11,7 +11,8 @@ All compute runs in ``libstereo_match_amd.so`` (HIP, gfx950) through the
 C-ABI in ``include/stereo_match_amd.h``; there is no CPU fallback.
 """
 from .matcher import (STEREO_SGBM_MODE_HH, STEREO_SGBM_MODE_HH4, STEREO_SGBM_MODE_SGBM,
-                      STEREO_SGBM_MODE_SGBM_3WAY, StereoSGBM, StereoSGBM_create, createRightMatcher)
+                      STEREO_SGBM_MODE_SGBM_3WAY, StereoSGBM, StereoSGBM_create, createRightMatcher,
+                      filterSpeckles)
 from .settings import DEFAULT_SETTINGS, parse_config_file
 from .stereo_vision import compute_disparity, matcher_from_settings
 from ._lib import SmError
@@ -19,6 +20,6 @@ from ._lib import SmError
 __all__ = [
     "compute_disparity", "matcher_from_settings", "StereoSGBM", "StereoSGBM_create", "createRightMatcher",
     "STEREO_SGBM_MODE_SGBM", "STEREO_SGBM_MODE_HH", "STEREO_SGBM_MODE_SGBM_3WAY", "STEREO_SGBM_MODE_HH4",
-    "parse_config_file", "DEFAULT_SETTINGS", "SmError",
+    "parse_config_file", "DEFAULT_SETTINGS", "SmError", "filterSpeckles",
 ]
 __version__ = "0.1.0"

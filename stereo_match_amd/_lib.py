@@ -20,7 +20,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "stereo_match_amd.
 SM_OK, SM_E_ARG, SM_E_HIP, SM_E_UNSUPPORTED = 0, -1, -2, -4
 SM_COST_SGBM, SM_COST_CENSUS, SM_COST_VOLUME = 0, 1, 2
 SM_MODE_SGBM, SM_MODE_HH = 5, 8
-STAGES = ("cost", "paths", "wta", "median", "total", "wls")
+STAGES = ("cost", "paths", "wta", "median", "total", "wls", "speckle")
 
 
 class SmParams(ctypes.Structure):
@@ -76,6 +76,9 @@ _SIGS = {
                                                      _c.c_int, _c.c_int, _c.c_int, _c.POINTER(SmParams),
                                                      _c.POINTER(SmWlsParams), _c.c_void_p, _c.c_void_p,
                                                      _c.c_void_p]),
+    "sm_filter_speckles": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_int]),
+    "sm_filter_speckles_device": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_int, _c.c_int, _c.c_int, _c.c_int,
+                                             _c.c_int, _c.c_int]),
     "sm_right_matcher_params": (_c.c_int, [_c.POINTER(SmParams), _c.POINTER(SmParams)]),
     "sm_synchronize": (_c.c_int, [_c.c_void_p]),
     "sm_set_timing": (_c.c_int, [_c.c_void_p, _c.c_int]),
@@ -286,6 +289,22 @@ class Engine:
             self.ctx, ctypes.c_void_p(d_left), ctypes.c_void_p(d_right), npairs, pair_stride, H, W, stride,
             ctypes.byref(params), ctypes.byref(wls), ctypes.c_void_p(d_displ), ctypes.c_void_p(d_dispr),
             ctypes.c_void_p(d_filtered)))
+
+    # -- speckle filter -------------------------------------------------------
+    def filter_speckles(self, img: np.ndarray, new_val: int, max_speckle_size: int, max_diff: int) -> np.ndarray:
+        """cv::filterSpeckles on a copy of an int16 map (returns the filtered map)."""
+        out = np.array(img, dtype=np.int16, order="C", copy=True)
+        if out.ndim != 2:
+            raise ValueError("expected a 2-D int16 map")
+        H, W = out.shape
+        self._check(self._lib.sm_filter_speckles(self.ctx, out.ctypes.data, H, W, int(new_val),
+                                                 int(max_speckle_size), int(max_diff)))
+        return out
+
+    def filter_speckles_device(self, d_img: int, nimg: int, H: int, W: int, new_val: int, max_speckle_size: int,
+                               max_diff: int):
+        self._check(self._lib.sm_filter_speckles_device(self.ctx, ctypes.c_void_p(d_img), nimg, H, W, int(new_val),
+                                                        int(max_speckle_size), int(max_diff)))
 
     def synchronize(self):
         self._check(self._lib.sm_synchronize(self.ctx))

@@ -30,6 +30,7 @@
 #include "sm_post.hpp"
 #include "sm_rowwta.hpp"
 #include "sm_wls.hpp"
+#include "sm_speckle.hpp"
 
 #define SM_VERSION "stereo_match_amd 0.2.0 (gfx950)"
 
@@ -69,7 +70,7 @@ struct sm_ctx {
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;  // stream A
     hipStream_t side = nullptr;    // stream B
-    DevBuf img[2], planes, out, dbg, volbuf;
+    DevBuf img[2], planes, out, dbg, volbuf, sp_parent, sp_count;
     DevBuf wls_num, wls_den, wls_inter, wls_w, wls_disp[2], wls_out;  // WLS scratch
     BufSet set[2];
     int next_set = 0;
@@ -150,8 +151,6 @@ int normalize(sm_ctx* ctx, const sm_params* p, int H, int W, Norm& n)
         return fail(ctx, SM_E_ARG, "cost_kind %d unknown", n.cost);
     if (n.mode != SM_MODE_SGBM && n.mode != SM_MODE_HH)
         return fail(ctx, SM_E_UNSUPPORTED, "mode %d not supported (5 = MODE_SGBM, 8 = MODE_HH)", n.mode);
-    if (n.speckle_ws > 0)
-        return fail(ctx, SM_E_UNSUPPORTED, "speckleWindowSize > 0 not implemented on the GPU path yet");
     if (n.cost == SM_COST_SGBM) {
         if (n.bs > 2 * 5 + 1) return fail(ctx, SM_E_UNSUPPORTED, "blockSize %d > 11 not built", n.bs);
         const int maxpix = 2 * n.ftzero + (255 >> 2);
@@ -413,6 +412,33 @@ int ensure_event(sm_ctx* ctx, hipEvent_t& e)
     return SM_OK;
 }
 
+// cv::filterSpeckles over G int16 maps (sm_speckle.hpp), enqueued on stream st.
+int run_speckles(sm_ctx* ctx, hipStream_t st, int16_t* img, int G, int H, int W, int newval, int maxsize,
+                 int maxdiff)
+{
+    StageTimer t(ctx, st, SM_STAGE_SPECKLE, G);
+    const size_t npx = (size_t)H * W;
+    int rc;
+    if ((rc = ensure(ctx, ctx->sp_parent, G * npx * 4)) != SM_OK) return rc;
+    if ((rc = ensure(ctx, ctx->sp_count, G * npx * 4)) != SM_OK) return rc;
+    smk::SpeckleArgs sa{};
+    sa.img = img;
+    sa.parent = (int*)ctx->sp_parent.p;
+    sa.count = (int*)ctx->sp_count.p;
+    sa.H = H;
+    sa.W = W;
+    sa.newval = newval;
+    sa.maxsize = maxsize;
+    sa.maxdiff = maxdiff;
+    const dim3 grid((unsigned)((npx + 255) / 256), G);
+    hipLaunchKernelGGL(smk::k_speckle_init, grid, dim3(256), 0, st, sa);
+    hipLaunchKernelGGL(smk::k_speckle_union, grid, dim3(256), 0, st, sa);
+    hipLaunchKernelGGL(smk::k_speckle_count, grid, dim3(256), 0, st, sa);
+    hipLaunchKernelGGL(smk::k_speckle_apply, grid, dim3(256), 0, st, sa);
+    HIP_TRY(ctx, hipGetLastError());
+    return SM_OK;
+}
+
 // G pairs (device pointers; pair i at dL + i*pair_stride).
 int run_group(sm_ctx* ctx, const Src& src, const Geo& g, const Norm& n, int16_t* d_out)
 {
@@ -528,6 +554,11 @@ int run_group(sm_ctx* ctx, const Src& src, const Geo& g, const Norm& n, int16_t*
         hipLaunchKernelGGL(smk::k_median3, dim3((W + 255) / 256, H, G), dim3(256), 0, sb,
                            (const int16_t*)bs.raw.p, d_out, H, W, (size_t)H * W);
         HIP_TRY(ctx, hipGetLastError());
+    }
+    if (n.speckle_ws > 0) {  // filterSpeckles(disp, INVALID, speckleWindowSize, 16*speckleRange)
+        if ((rc = run_speckles(ctx, sb, d_out, G, H, W, (n.minD - 1) * 16, n.speckle_ws, 16 * n.speckle_range)) !=
+            SM_OK)
+            return rc;
     }
     if (sb != ctx->stream) {
         HIP_TRY(ctx, hipEventRecord(bs.wta_done, sb));
@@ -745,7 +776,7 @@ void sm_destroy(sm_ctx* ctx)
     (void)hipDeviceSynchronize();
     DevBuf* bufs[] = {&ctx->img[0],  &ctx->img[1],  &ctx->planes,    &ctx->out,         &ctx->dbg,
                       &ctx->volbuf,  &ctx->wls_num, &ctx->wls_den,   &ctx->wls_inter,   &ctx->wls_disp[0], &ctx->wls_w,
-                      &ctx->wls_disp[1], &ctx->wls_out};
+                      &ctx->wls_disp[1], &ctx->wls_out, &ctx->sp_parent, &ctx->sp_count};
     for (DevBuf* b : bufs)
         if (b->p) (void)hipFree(b->p);
     for (auto& bs : ctx->set) {
@@ -1003,6 +1034,34 @@ int sm_compute_disparity(sm_ctx* ctx, const uint8_t* L, const uint8_t* R, int H,
     if (rc != SM_OK) return rc;
     HIP_TRY(ctx, hipMemcpyAsync(displ, ctx->wls_disp[0].p, img * 2, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(filtered, ctx->wls_out.p, img * 2, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return SM_OK;
+}
+
+int sm_filter_speckles_device(sm_ctx* ctx, int16_t* d_img, int nimg, int H, int W, int new_val,
+                              int max_speckle_size, int max_diff)
+{
+    if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
+    if (!d_img || nimg < 0 || H <= 0 || W <= 0) return fail(ctx, SM_E_ARG, "bad image arguments");
+    if ((long long)H * W >= (1LL << 31)) return fail(ctx, SM_E_UNSUPPORTED, "image too large");
+    if (max_speckle_size <= 0 || nimg == 0) return SM_OK;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    return run_speckles(ctx, ctx->stream, d_img, nimg, H, W, new_val, max_speckle_size, max_diff);
+}
+
+int sm_filter_speckles(sm_ctx* ctx, int16_t* img, int H, int W, int new_val, int max_speckle_size, int max_diff)
+{
+    if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
+    if (!img || H <= 0 || W <= 0) return fail(ctx, SM_E_ARG, "bad image arguments");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    const size_t bytes = (size_t)H * W * 2;
+    int rc;
+    if ((rc = ensure(ctx, ctx->out, bytes)) != SM_OK) return rc;
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->out.p, img, bytes, hipMemcpyHostToDevice, ctx->stream));
+    if ((rc = sm_filter_speckles_device(ctx, (int16_t*)ctx->out.p, 1, H, W, new_val, max_speckle_size, max_diff)) !=
+        SM_OK)
+        return rc;
+    HIP_TRY(ctx, hipMemcpyAsync(img, ctx->out.p, bytes, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     return SM_OK;
 }

@@ -195,3 +195,23 @@ def createRightMatcher(matcher_left: StereoSGBM) -> StereoSGBM:
                       blockSize=m.blockSize, P1=m.P1, P2=m.P2, disp12MaxDiff=1000000,
                       preFilterCap=m.preFilterCap, uniquenessRatio=0, speckleWindowSize=0,
                       speckleRange=m.speckleRange, mode=m.mode, cost=m.cost, device=m.device)
+
+
+def filterSpeckles(img, newVal, maxSpeckleSize, maxDiff, buf=None, device=0):
+    """cv2.filterSpeckles(img, newVal, maxSpeckleSize, maxDiff) — in place on an
+    int16 numpy map (returns ``(img, buf)`` like the cv2 binding) or on a torch
+    CUDA int16 tensor (torch's current stream)."""
+    if _is_torch_cuda(img):
+        import torch
+
+        if img.dtype != torch.int16 or img.dim() != 2 or not img.is_contiguous():
+            raise ValueError("expected a contiguous 2-D int16 tensor")
+        eng = _lib.engine(img.device.index or 0)
+        eng.set_stream(torch.cuda.current_stream(img.device).cuda_stream)
+        eng.filter_speckles_device(img.data_ptr(), 1, img.shape[0], img.shape[1], newVal, maxSpeckleSize, maxDiff)
+        return img, buf
+    a = np.asarray(img)
+    if a.dtype != np.int16 or a.ndim != 2:
+        raise SmError(_lib.SM_E_UNSUPPORTED, "filterSpeckles: only CV_16SC1 maps are implemented on the GPU path")
+    a[...] = _lib.engine(device).filter_speckles(a, newVal, maxSpeckleSize, maxDiff)
+    return a, buf

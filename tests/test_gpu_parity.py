@@ -226,8 +226,6 @@ def test_compute_disparity_left_matcher_semantics():
 
 def test_unsupported_and_bad_args_raise(eng):
     l = np.zeros((10, 40), np.uint8)
-    with pytest.raises(_lib.SmError):
-        run(eng, l, l, dict(synthetic.parity_params(16), speckleWindowSize=50))
     with pytest.raises(ValueError):
         run(eng, l, l, dict(synthetic.parity_params(16), numDisparities=24))
     with pytest.raises(_lib.SmError):
@@ -329,3 +327,43 @@ def test_volume_bad_args(eng):
         eng.aggregate_cost_f32(vol, synthetic.to_sm_params(synthetic.cost_volume_params(32)))
     with pytest.raises(_lib.SmError):  # P2 beyond the exact range
         eng.aggregate_cost_f32(vol, synthetic.to_sm_params(dict(synthetic.cost_volume_params(16), P2=13000)))
+
+
+# ---------------------------------------------------------------- speckle filter
+_SCASES = [dict(H=int(_rng.integers(8, 90)), W=int(_rng.integers(60, 260)), D=16 * int(_rng.integers(1, 4)),
+                ws=int(_rng.choice([4, 20, 60, 200])), rng=int(_rng.choice([1, 2, 4])), cost=int(_rng.integers(0, 2)),
+                seed=int(_rng.integers(0, 1 << 30))) for _ in range(10)]
+
+
+@pytest.mark.parametrize("c", _SCASES, ids=lambda c: "H{H}W{W}D{D}ws{ws}r{rng}c{cost}".format(**c))
+def test_speckle_filter_in_matcher_vs_c_oracle(eng, c):
+    left, right, _ = synthetic.random_dot_pair(c["H"], c["W"], c["D"], seed=c["seed"])
+    base = synthetic.headline_params(c["D"]) if c["cost"] else synthetic.parity_params(c["D"])
+    p = dict(base, speckleWindowSize=c["ws"], speckleRange=c["rng"])
+    out = run(eng, left, right, p)
+    assert np.array_equal(out, ref_c.compute(left, right, p))
+
+
+def test_speckle_filter_standalone_and_full_size(eng):
+    import stereo_match_amd as sm
+
+    rng = np.random.default_rng(3)
+    # blocky map with many small and a few large regions, plus invalid pixels
+    img = (rng.integers(0, 6, (40, 50)) * 40).astype(np.int16)
+    img = np.kron(img, np.ones((3, 2), np.int16))[:100, :90]
+    img[rng.random(img.shape) < 0.1] = -16
+    for ws, md in [(1, 0), (6, 0), (30, 16), (500, 40)]:
+        exp = sgm_np.filter_speckles(img, -16, ws, md)
+        assert np.array_equal(eng.filter_speckles(img, -16, ws, md), exp), (ws, md)
+    a = img.copy()
+    sm.filterSpeckles(a, -16, 30, 16)
+    assert np.array_equal(a, sgm_np.filter_speckles(img, -16, 30, 16))
+    H, W, D = synthetic.CONFIGS["kitti"]
+    left, right, _ = synthetic.random_dot_pair(H, W, D, seed=11)
+    p = dict(synthetic.headline_params(D), speckleWindowSize=100, speckleRange=2)
+    assert np.array_equal(run(eng, left, right, p), ref_c.compute(left, right, p))
+    # the union-find is lock-free across all XCDs: repeat to catch racy links
+    base = ref_c.compute(left, right, synthetic.headline_params(D))
+    exp = sgm_np.filter_speckles(base, -16, 100, 32)
+    for _ in range(5):
+        assert np.array_equal(eng.filter_speckles(base, -16, 100, 32), exp)
