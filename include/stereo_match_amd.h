@@ -158,6 +158,18 @@ int sm_filter_speckles(sm_ctx* ctx, int16_t* img, int H, int W, int new_val, int
 int sm_filter_speckles_device(sm_ctx* ctx, int16_t* d_img, int nimg, int H, int W, int new_val,
                               int max_speckle_size, int max_diff);
 
+/* cv::reprojectImageTo3D(disparity, Q, handleMissingValues, CV_32F): the
+ * reference reprojects the filtered int16 map (disparity_calculation.py:302;
+ * mapTo3D_mc_cnn.py:124 with float32) — xyz out float32 [H][W][3].
+ * Q: 4x4 row-major float64.  Host version synchronous; the device version
+ * handles nimg maps (disp + i*H*W, xyz + i*H*W*3). */
+#define SM_DISP_S16 0
+#define SM_DISP_F32 1
+int sm_reproject_image_to_3d(sm_ctx* ctx, const void* disp, int disp_type, int H, int W, const double* Q,
+                             int handle_missing, float* xyz);
+int sm_reproject_image_to_3d_device(sm_ctx* ctx, const void* d_disp, int disp_type, int nimg, int H, int W,
+                                    const double* Q, int handle_missing, float* d_xyz);
+
 /* ximgproc::createRightMatcher(StereoSGBM) parameter derivation
  * (reference call: stereo_vision/stereo_vision.py:171). */
 int sm_right_matcher_params(const sm_params* left, sm_params* right_out);

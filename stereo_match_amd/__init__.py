@@ -16,10 +16,12 @@ from .matcher import (STEREO_SGBM_MODE_HH, STEREO_SGBM_MODE_HH4, STEREO_SGBM_MOD
 from .settings import DEFAULT_SETTINGS, parse_config_file
 from .stereo_vision import compute_disparity, matcher_from_settings
 from ._lib import SmError
+from .reproject import project_points_3D, reprojectImageTo3D, write_ply
 
 __all__ = [
     "compute_disparity", "matcher_from_settings", "StereoSGBM", "StereoSGBM_create", "createRightMatcher",
     "STEREO_SGBM_MODE_SGBM", "STEREO_SGBM_MODE_HH", "STEREO_SGBM_MODE_SGBM_3WAY", "STEREO_SGBM_MODE_HH4",
-    "parse_config_file", "DEFAULT_SETTINGS", "SmError", "filterSpeckles",
+    "parse_config_file", "DEFAULT_SETTINGS", "SmError", "filterSpeckles", "reprojectImageTo3D",
+    "project_points_3D", "write_ply",
 ]
 __version__ = "0.1.0"

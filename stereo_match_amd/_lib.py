@@ -79,6 +79,10 @@ _SIGS = {
     "sm_filter_speckles": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_int]),
     "sm_filter_speckles_device": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_int, _c.c_int, _c.c_int, _c.c_int,
                                              _c.c_int, _c.c_int]),
+    "sm_reproject_image_to_3d": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_int, _c.c_int, _c.c_int,
+                                            _c.c_void_p, _c.c_int, _c.c_void_p]),
+    "sm_reproject_image_to_3d_device": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_int, _c.c_int, _c.c_int, _c.c_int,
+                                                   _c.c_void_p, _c.c_int, _c.c_void_p]),
     "sm_right_matcher_params": (_c.c_int, [_c.POINTER(SmParams), _c.POINTER(SmParams)]),
     "sm_synchronize": (_c.c_int, [_c.c_void_p]),
     "sm_set_timing": (_c.c_int, [_c.c_void_p, _c.c_int]),
@@ -305,6 +309,26 @@ class Engine:
                                max_diff: int):
         self._check(self._lib.sm_filter_speckles_device(self.ctx, ctypes.c_void_p(d_img), nimg, H, W, int(new_val),
                                                         int(max_speckle_size), int(max_diff)))
+
+    # -- 3-D reprojection ---------------------------------------------------------
+    def reproject(self, disp: np.ndarray, Q: np.ndarray, handle_missing: bool = False) -> np.ndarray:
+        d = np.ascontiguousarray(disp)
+        kind = {np.dtype(np.int16): 0, np.dtype(np.float32): 1}.get(d.dtype)
+        if kind is None or d.ndim != 2:
+            raise ValueError("disparity must be a 2-D int16 or float32 array")
+        Qd = np.ascontiguousarray(np.asarray(Q, np.float64).reshape(16))
+        H, W = d.shape
+        out = np.empty((H, W, 3), np.float32)
+        self._check(self._lib.sm_reproject_image_to_3d(self.ctx, d.ctypes.data, kind, H, W, Qd.ctypes.data,
+                                                       int(bool(handle_missing)), out.ctypes.data))
+        return out
+
+    def reproject_device(self, d_disp: int, kind: int, nimg: int, H: int, W: int, Q: np.ndarray,
+                         handle_missing: bool, d_xyz: int):
+        Qd = np.ascontiguousarray(np.asarray(Q, np.float64).reshape(16))
+        self._check(self._lib.sm_reproject_image_to_3d_device(self.ctx, ctypes.c_void_p(d_disp), kind, nimg, H, W,
+                                                              Qd.ctypes.data, int(bool(handle_missing)),
+                                                              ctypes.c_void_p(d_xyz)))
 
     def synchronize(self):
         self._check(self._lib.sm_synchronize(self.ctx))

@@ -31,6 +31,7 @@
 #include "sm_rowwta.hpp"
 #include "sm_wls.hpp"
 #include "sm_speckle.hpp"
+#include "sm_reproject.hpp"
 
 #define SM_VERSION "stereo_match_amd 0.2.0 (gfx950)"
 
@@ -70,7 +71,7 @@ struct sm_ctx {
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;  // stream A
     hipStream_t side = nullptr;    // stream B
-    DevBuf img[2], planes, out, dbg, volbuf, sp_parent, sp_count;
+    DevBuf img[2], planes, out, dbg, volbuf, sp_parent, sp_count, rp_in, rp_out, rp_min;
     DevBuf wls_num, wls_den, wls_inter, wls_w, wls_disp[2], wls_out;  // WLS scratch
     BufSet set[2];
     int next_set = 0;
@@ -776,7 +777,8 @@ void sm_destroy(sm_ctx* ctx)
     (void)hipDeviceSynchronize();
     DevBuf* bufs[] = {&ctx->img[0],  &ctx->img[1],  &ctx->planes,    &ctx->out,         &ctx->dbg,
                       &ctx->volbuf,  &ctx->wls_num, &ctx->wls_den,   &ctx->wls_inter,   &ctx->wls_disp[0], &ctx->wls_w,
-                      &ctx->wls_disp[1], &ctx->wls_out, &ctx->sp_parent, &ctx->sp_count};
+                      &ctx->wls_disp[1], &ctx->wls_out, &ctx->sp_parent, &ctx->sp_count,
+                      &ctx->rp_in,   &ctx->rp_out,  &ctx->rp_min};
     for (DevBuf* b : bufs)
         if (b->p) (void)hipFree(b->p);
     for (auto& bs : ctx->set) {
@@ -1062,6 +1064,67 @@ int sm_filter_speckles(sm_ctx* ctx, int16_t* img, int H, int W, int new_val, int
         SM_OK)
         return rc;
     HIP_TRY(ctx, hipMemcpyAsync(img, ctx->out.p, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return SM_OK;
+}
+
+int sm_reproject_image_to_3d_device(sm_ctx* ctx, const void* d_disp, int disp_type, int nimg, int H, int W,
+                                    const double* Q, int handle_missing, float* d_xyz)
+{
+    if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
+    if (!d_disp || !d_xyz || !Q || nimg < 0 || H <= 0 || W <= 0) return fail(ctx, SM_E_ARG, "bad arguments");
+    if (disp_type != SM_DISP_S16 && disp_type != SM_DISP_F32)
+        return fail(ctx, SM_E_UNSUPPORTED, "disparity type %d not supported (int16 or float32)", disp_type);
+    if (nimg == 0) return SM_OK;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    smk::ReprojArgs ra{};
+    ra.disp = d_disp;
+    ra.xyz = d_xyz;
+    std::memcpy(ra.Q, Q, sizeof ra.Q);
+    ra.H = H;
+    ra.W = W;
+    ra.handle_missing = handle_missing != 0;
+    const size_t npx = (size_t)H * W;
+    if (ra.handle_missing) {
+        int rc;
+        if ((rc = ensure(ctx, ctx->rp_min, (size_t)nimg * 8)) != SM_OK) return rc;
+        int* keys = (int*)ctx->rp_min.p;
+        HIP_TRY(ctx, hipMemsetD32Async((hipDeviceptr_t)keys, 0x7FFFFFFF, nimg, ctx->stream));
+        const dim3 g((unsigned)std::min<size_t>((npx + 255) / 256, 1024), nimg);
+        if (disp_type == SM_DISP_S16)
+            hipLaunchKernelGGL(smk::k_disp_min<int16_t>, g, dim3(256), 0, ctx->stream, (const int16_t*)d_disp, keys, npx);
+        else
+            hipLaunchKernelGGL(smk::k_disp_min<float>, g, dim3(256), 0, ctx->stream, (const float*)d_disp, keys, npx);
+        hipLaunchKernelGGL(smk::k_keys_to_float, dim3((nimg + 63) / 64), dim3(64), 0, ctx->stream, keys,
+                           (float*)(keys + nimg), nimg);
+        ra.min_disp = (const float*)(keys + nimg);
+    }
+    const dim3 grid((W + 255) / 256, H, nimg);
+    if (disp_type == SM_DISP_S16)
+        hipLaunchKernelGGL(smk::k_reproject<int16_t>, grid, dim3(256), 0, ctx->stream, ra);
+    else
+        hipLaunchKernelGGL(smk::k_reproject<float>, grid, dim3(256), 0, ctx->stream, ra);
+    HIP_TRY(ctx, hipGetLastError());
+    return SM_OK;
+}
+
+int sm_reproject_image_to_3d(sm_ctx* ctx, const void* disp, int disp_type, int H, int W, const double* Q,
+                             int handle_missing, float* xyz)
+{
+    if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
+    if (!disp || !xyz || !Q || H <= 0 || W <= 0) return fail(ctx, SM_E_ARG, "bad arguments");
+    if (disp_type != SM_DISP_S16 && disp_type != SM_DISP_F32)
+        return fail(ctx, SM_E_UNSUPPORTED, "disparity type %d not supported (int16 or float32)", disp_type);
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    const size_t npx = (size_t)H * W, ib = npx * (disp_type == SM_DISP_S16 ? 2 : 4);
+    int rc;
+    if ((rc = ensure(ctx, ctx->rp_in, ib)) != SM_OK) return rc;
+    if ((rc = ensure(ctx, ctx->rp_out, npx * 12)) != SM_OK) return rc;
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->rp_in.p, disp, ib, hipMemcpyHostToDevice, ctx->stream));
+    if ((rc = sm_reproject_image_to_3d_device(ctx, ctx->rp_in.p, disp_type, 1, H, W, Q, handle_missing,
+                                              (float*)ctx->rp_out.p)) != SM_OK)
+        return rc;
+    HIP_TRY(ctx, hipMemcpyAsync(xyz, ctx->rp_out.p, npx * 12, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     return SM_OK;
 }
