@@ -210,7 +210,9 @@ long long sm_debug_fetch(sm_ctx* ctx, int what, void* host, size_t bytes);
  * kept on chip); bit 4 (valid results) makes that kernel store the W path
  * volume too, so sm_debug_fetch(1) returns every direction; bit 6 (valid
  * results) runs WTA + median on a second internal stream, overlapped with
- * the next launch group's path aggregation (double-buffered volumes).
+ * the next launch group's path aggregation (double-buffered volumes);
+ * bit 9 (valid results, D % 64 == 0) uses 64-lane horizontal lines (one row
+ * per wave) instead of 16-lane lines (4 rows per wave).
  * 0 = normal operation. */
 int sm_set_debug_flags(sm_ctx* ctx, int flags);
 

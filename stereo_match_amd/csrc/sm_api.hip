@@ -62,7 +62,7 @@ struct BufSet {
 };
 
 // debug flags (sm_set_debug_flags); 1 skip horizontal, 2 skip vertical and 4 drop stores are read in-kernel
-constexpr int DBG_VL16 = 8, DBG_STORE_W = 16, DBG_ROW = 32, DBG_OVERLAP = 64;
+constexpr int DBG_VL16 = 8, DBG_STORE_W = 16, DBG_ROW = 32, DBG_OVERLAP = 64, DBG_H64 = 512;
 
 }  // namespace
 
@@ -266,12 +266,12 @@ bool overlap(const sm_ctx* ctx) { return (ctx->dbg_flags & DBG_OVERLAP) != 0; }
 hipStream_t stream_b(const sm_ctx* ctx) { return overlap(ctx) ? ctx->side : ctx->stream; }
 
 // ---- stream A: path aggregation -------------------------------------------
-template <int DPLV, bool CENSUS, int VL>
+template <int DPLV, bool CENSUS, int VL, bool H16 = false>
 int launch_paths_t(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs)
 {
     using LT = typename std::conditional<CENSUS, uint8_t, uint16_t>::type;
     constexpr int D = 16 * DPLV;
-    constexpr bool WIDE = D % 64 == 0;
+    constexpr bool WIDE = D % 64 == 0 && !H16;
     constexpr int LANESH = WIDE ? 64 : 16;
     constexpr int DPLH = D / LANESH;
     smk::PathsArgs pa{};
@@ -376,11 +376,19 @@ int launch_wta_t(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs)
 template <int DPLV, bool CENSUS>
 int launch_paths_dpl(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs)
 {
+    // horizontal lines: 16 lanes (4 rows per wave); 64-lane lines (one row per
+    // wave, the round-1 layout for D % 64 == 0) with the ablation flag
+    if constexpr ((16 * DPLV) % 64 == 0) {
+        if (ctx->dbg_flags & DBG_H64) {
+            if (DPLV == 8 && !(ctx->dbg_flags & DBG_VL16)) return launch_paths_t<DPLV, CENSUS, 8>(ctx, n, g, bs);
+            return launch_paths_t<DPLV, CENSUS, 16>(ctx, n, g, bs);
+        }
+    }
     // 8-lane vertical lines at D = 128 (16-lane with the ablation flag)
     if constexpr (DPLV == 8) {
-        if (!(ctx->dbg_flags & DBG_VL16)) return launch_paths_t<DPLV, CENSUS, 8>(ctx, n, g, bs);
+        if (!(ctx->dbg_flags & DBG_VL16)) return launch_paths_t<DPLV, CENSUS, 8, true>(ctx, n, g, bs);
     }
-    return launch_paths_t<DPLV, CENSUS, 16>(ctx, n, g, bs);
+    return launch_paths_t<DPLV, CENSUS, 16, true>(ctx, n, g, bs);
 }
 
 int dispatch(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs, bool wta)

@@ -383,13 +383,50 @@ __global__ void __launch_bounds__(NT) k_wta(WtaArgs a)
     for (int x = grp; x < a.width1; x += NT / 16) {
         const size_t off = ((size_t)y * a.width1 + x) * D;
         uint32_t S[DPL];
+        if constexpr (sizeof(LT) == 1 && DPL % 4 == 0) {
+            // SWAR: bytes split into even/odd 16-bit lanes, summed with plain
+            // 32-bit adds (8 slots x 255 < 65536, no carry between lanes);
+            // all slots' loads are issued before the first add
+            constexpr int NW = DPL / 4;
+            uint32_t w[8][NW];
 #pragma unroll
-        for (int i = 0; i < DPL; i++) S[i] = 0;
-        for (int k = 0; k < a.nslots; k++) {
-            uint32_t t[DPL];
-            load_n<DPL>(Lb + (size_t)k * slot + off, t);
+            for (int k = 0; k < 8; k++) {
+                if (k < a.nslots) {
+                    const uint32_t* src = reinterpret_cast<const uint32_t*>(Lb + (size_t)k * slot + off);
 #pragma unroll
-            for (int i = 0; i < DPL; i++) S[i] += t[i];
+                    for (int j = 0; j < NW; j++) w[k][j] = src[j];
+                } else {
+#pragma unroll
+                    for (int j = 0; j < NW; j++) w[k][j] = 0;
+                }
+            }
+            uint32_t ev[NW], od[NW];
+#pragma unroll
+            for (int j = 0; j < NW; j++) ev[j] = od[j] = 0;
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+#pragma unroll
+                for (int j = 0; j < NW; j++) {
+                    ev[j] += w[k][j] & 0x00FF00FFu;
+                    od[j] += (w[k][j] >> 8) & 0x00FF00FFu;
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < NW; j++) {
+                S[4 * j + 0] = ev[j] & 0xFFFF;
+                S[4 * j + 1] = od[j] & 0xFFFF;
+                S[4 * j + 2] = ev[j] >> 16;
+                S[4 * j + 3] = od[j] >> 16;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < DPL; i++) S[i] = 0;
+            for (int k = 0; k < a.nslots; k++) {
+                uint32_t t[DPL];
+                load_n<DPL>(Lb + (size_t)k * slot + off, t);
+#pragma unroll
+                for (int i = 0; i < DPL; i++) S[i] += t[i];
+            }
         }
         uint32_t key = 0xFFFFFFFFu;
 #pragma unroll
