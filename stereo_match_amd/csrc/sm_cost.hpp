@@ -19,35 +19,61 @@ struct CensusArgs {
     int H, W, stride;
 };
 
-constexpr int CT_W = 32, CT_H = 8;
+constexpr int CT_W = 64, CT_H = 16, CT_PY = 4;  // tile; pixels per thread (vertical)
+constexpr int CT_LW = CT_W + 12;                 // LDS row: 4 left halo + 64 + 4 right halo, dword padded
 
+// Bits are assembled MSB-first with acc = 2*acc + (I[n] < I[c]) so each
+// comparison is one compare + one add-with-carry; the 62 neighbours of a
+// pixel are read as 3 aligned dwords per window row (bytes extracted by the
+// compiler), and a thread computes CT_PY vertically adjacent pixels so the
+// 7-row windows share their LDS reads.
 __global__ void __launch_bounds__(256) k_census9x7(CensusArgs a)
 {
-    __shared__ uint8_t tile[CT_H + 6][CT_W + 8];
+    __shared__ uint32_t tile[CT_H + 6][CT_LW / 4];
     const int which = blockIdx.z & 1, pair = blockIdx.z >> 1;
     const uint8_t* img = a.img[which] + (size_t)pair * a.in_pair;
     const int x0 = blockIdx.x * CT_W, y0 = blockIdx.y * CT_H;
-    for (int i = threadIdx.x; i < (CT_H + 6) * (CT_W + 8); i += 256) {
-        int ty = i / (CT_W + 8), tx = i % (CT_W + 8);
-        int y = min(max(y0 + ty - 3, 0), a.H - 1), x = min(max(x0 + tx - 4, 0), a.W - 1);
-        tile[ty][tx] = img[(size_t)y * a.stride + x];
+    uint8_t* tb = reinterpret_cast<uint8_t*>(&tile[0][0]);
+    for (int i = threadIdx.x; i < (CT_H + 6) * CT_LW; i += 256) {
+        const int ty = i / CT_LW, tx = i % CT_LW;
+        const int y = min(max(y0 + ty - 3, 0), a.H - 1), x = min(max(x0 + tx - 4, 0), a.W - 1);
+        tb[ty * CT_LW + tx] = img[(size_t)y * a.stride + x];
     }
     __syncthreads();
-    const int tx = threadIdx.x % CT_W, ty = threadIdx.x / CT_W;
-    const int x = x0 + tx, y = y0 + ty;
-    if (x >= a.W || y >= a.H) return;
-    const int c = tile[ty + 3][tx + 4];
-    uint64_t v = 0;
-    int k = 0;
+    const int tx = threadIdx.x % CT_W, ty0 = (threadIdx.x / CT_W) * CT_PY;
+    const int x = x0 + tx;
+    // window columns tx .. tx+8 in tile coordinates (tile col = image col - x0 + 4)
+    const int wd = tx >> 2, sh = (tx & 3) * 8;
+    uint32_t rows[CT_PY + 6][3];  // 12 bytes covering the 9 window columns, per tile row
 #pragma unroll
-    for (int dy = 0; dy < 7; dy++)
+    for (int r = 0; r < CT_PY + 6; r++) {
+        const uint32_t w0 = tile[ty0 + r][wd], w1 = tile[ty0 + r][wd + 1], w2 = tile[ty0 + r][wd + 2];
+        rows[r][0] = __builtin_amdgcn_alignbyte(w1, w0, sh >> 3);
+        rows[r][1] = __builtin_amdgcn_alignbyte(w2, w1, sh >> 3);
+        rows[r][2] = w2 >> sh;
+    }
+    auto px = [&](int r, int dx) -> uint32_t { return (rows[r][dx >> 2] >> ((dx & 3) * 8)) & 0xFF; };
 #pragma unroll
-        for (int dx = 0; dx < 9; dx++) {
-            if (dy == 3 && dx == 4) continue;
-            v |= (uint64_t)(tile[ty + dy][tx + dx] < c) << k;
-            k++;
+    for (int p = 0; p < CT_PY; p++) {
+        const int y = y0 + ty0 + p;
+        const uint32_t c = px(p + 3, 4);
+        uint32_t lo = 0, hi = 0;
+        // bit k <-> neighbour k in row-major order with the centre skipped
+#pragma unroll
+        for (int k = 61; k >= 32; k--) {
+            const int n = k < 31 ? k : k + 1;
+            unsigned co;
+            hi = __builtin_addc(hi, hi, px(p + n / 9, n % 9) < c ? 1u : 0u, &co);
         }
-    a.out[which][(size_t)pair * a.H * a.W + (size_t)y * a.W + x] = v;
+#pragma unroll
+        for (int k = 31; k >= 0; k--) {
+            const int n = k < 31 ? k : k + 1;
+            unsigned co;
+            lo = __builtin_addc(lo, lo, px(p + n / 9, n % 9) < c ? 1u : 0u, &co);
+        }
+        if (x < a.W && y < a.H)
+            a.out[which][(size_t)pair * a.H * a.W + (size_t)y * a.W + x] = ((uint64_t)hi << 32) | lo;
+    }
 }
 
 // Hamming cost volume C[y][x1][d] = popcount(cl[y][X] ^ cr[y][X-minD-d]),
