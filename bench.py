@@ -187,8 +187,11 @@ def main():
             try:
                 with open(args.traffic_file) as f:
                     tr = json.load(f)
-                if tr.get("config") == args.config and tr.get("mode") == args.mode and tr.get("kernel_stage") == dom:
-                    traffic = tr.get("hbm_bytes_per_launch")
+                if tr.get("config") == args.config and tr.get("mode") == args.mode:
+                    st = tr.get("stages", {}).get(dom, {})
+                    # per launch of the same pairs-per-launch as this run
+                    if st and tr.get("pairs_per_launch", pairs_per_launch) == pairs_per_launch:
+                        traffic = st.get("hbm_bytes_per_launch")
             except (OSError, ValueError):
                 traffic = None
         # SURVEY.md §8(d) whole-pipeline model: H·W·D·(1+P+4) + 2HW + 4HW per pair

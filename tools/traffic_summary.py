@@ -14,7 +14,9 @@ vals = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in glob.glob(out + "/*/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         vals[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
-summary = {"config": config, "mode": mode, "kernels": {}}
+summary = {"config": config, "mode": mode, "kernels": {},
+           "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes over bench.py; "
+                     "reads = 2*FETCH_SIZE on gfx950 (MI355X_MICROARCH.md)"}
 for k, d in vals.items():
     fs = sum(d["FETCH_SIZE"]) / max(len(d["FETCH_SIZE"]), 1) if "FETCH_SIZE" in d else None
     ws = sum(d["WRITE_SIZE"]) / max(len(d["WRITE_SIZE"]), 1) if "WRITE_SIZE" in d else None
@@ -22,8 +24,11 @@ for k, d in vals.items():
     wr = ws * 1024 if ws is not None else None
     summary["kernels"][k] = {"fetch_size_kb": fs, "write_size_kb": ws, "read_bytes_corrected": rd,
                              "write_bytes": wr, "hbm_bytes": (rd or 0) + (wr or 0)}
-    if "k_sgm_paths" in k:
-        summary["paths_hbm_bytes_per_launch"] = (rd or 0) + (wr or 0)
-        summary["paths_kernel"] = k
+    stage = ("paths" if "k_sgm_paths" in k else "wta" if ("k_wta" in k or "k_row_wta" in k)
+             else "cost" if any(c in k for c in ("k_census9x7", "k_sgbm_cost(", "k_cost_volume_f32")) else None)
+    if stage:
+        summary.setdefault("stages", {})[stage] = {"kernel": k, "hbm_bytes_per_launch": (rd or 0) + (wr or 0),
+                                                   "read_bytes": rd, "write_bytes": wr}
+summary["pairs_per_launch"] = 8  # bench.py default --pairs-per-gpu (one launch group)
 json.dump(summary, open(out + "/summary.json", "w"), indent=1)
 print(json.dumps(summary, indent=1))
