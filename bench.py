@@ -35,9 +35,10 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default=None, choices=["kitti", "middlebury", "tsukuba", "mccnn"],
                     help="default: kitti (mccnn for --mode volume8)")
-    ap.add_argument("--mode", default="census8", choices=["census8", "sgbm5", "volume8", "disparity5"],
+    ap.add_argument("--mode", default="census8", choices=["census8", "sgbm5", "volume8", "disparity5", "bm"],
                     help="census8 = headline; sgbm5 = OpenCV parity mode; volume8 = mc-cnn f32 cost volume; "
-                         "disparity5 = the reference's whole compute_disparity (left + right SGBM + WLS)")
+                         "disparity5 = the reference's whole compute_disparity (left + right SGBM + WLS); "
+                         "bm = StereoBM(numDisparities=D, blockSize=21), the method='BM' matcher")
     ap.add_argument("--pairs-per-gpu", type=int, default=8)
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--row", action="store_true",
@@ -72,6 +73,7 @@ def main():
     H, W, D = synthetic.CONFIGS[args.config]
     volume = args.mode == "volume8"
     full = args.mode == "disparity5"
+    bm = args.mode == "bm"
     if args.mode == "census8":
         p = synthetic.headline_params(D)
     elif volume:
@@ -79,6 +81,9 @@ def main():
     else:
         p = synthetic.parity_params(D)
     prm = synthetic.to_sm_params(p)
+    if bm:
+        prm = _lib.SmBmParams()
+        _lib.load().sm_bm_default_params(D, 21, prm)
     P = args.pairs_per_gpu
     gpairs = P * world
 
@@ -113,6 +118,8 @@ def main():
         if full:
             eng.compute_disparity_batch_device(dL.data_ptr(), dR.data_ptr(), P, H * W, H, W, W, prm, wprm,
                                                dOut.data_ptr(), dOutR.data_ptr(), dFilt.data_ptr())
+        elif bm:
+            eng.bm_compute_batch_device(dL.data_ptr(), dR.data_ptr(), P, H * W, H, W, W, prm, dOut.data_ptr())
         elif volume:
             eng.aggregate_cost_f32_device(vols.data_ptr(), P, D * H * W, D, H, W, prm, 0.0, synthetic.VOLUME_SCALE,
                                           dOut.data_ptr())
@@ -172,6 +179,8 @@ def main():
             paths_bytes = P_dirs * vol * eb + (census_b or P_dirs * vol * 2)
             wta_bytes = P_dirs * vol * eb + 2 * H * W
             wta_name = "k_wta"
+        if bm:  # SAD kernel reads the two prefiltered views, writes disparity (+ int32 cost)
+            wta_name, wta_bytes = "k_bm_sad (column sums in LDS + WTA)", H * W * (2 + 2 + 4)
         kern = {"paths": ("k_sgm_paths (vertical family)" if row_mode else "k_sgm_paths (all directions)",
                           paths_bytes),
                 "wta": (wta_name, wta_bytes)}
@@ -198,6 +207,8 @@ def main():
         # (mc-cnn f32 volume: H·W·D·(4·P + 8))
         if volume:
             survey_bytes = cells * (4 * P_dirs + 8)
+        elif bm:  # no volume: images in, prefiltered views, disparity + cost out
+            survey_bytes = H * W * (2 + 2 * 2 + 2 + 4)
         elif full:  # two matcher runs (left, right) per pair; WLS traffic is O(H·W)
             survey_bytes = 2 * (cells * (1 + P_dirs + 4) + 2 * H * W + 4 * H * W)
         else:
@@ -217,14 +228,16 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": {"census8": "u8", "sgbm5": "i16", "volume8": "f32->u16", "disparity5": "i16+f32"}[args.mode],
+            "dtype": {"census8": "u8", "sgbm5": "i16", "volume8": "f32->u16", "disparity5": "i16+f32",
+                      "bm": "i32"}[args.mode],
             "data": "synthetic random-dot pairs (no dataset in the image)"
                     + ("; f32 cost = 3x3-smoothed |L-R|/255 volume per pair" if volume else ""),
             "config": {
                 "workload": f"{args.config} {W}x{H} D={D} "
                             + {"census8": "census9x7 + 8-path SGM", "sgbm5": "OpenCV-SGBM 5-path",
                                "volume8": "f32 cost volume (mc-cnn) + 8-path SGM",
-                               "disparity5": "compute_disparity: left+right OpenCV-SGBM 5-path + WLS"}[args.mode],
+                               "disparity5": "compute_disparity: left+right OpenCV-SGBM 5-path + WLS",
+                               "bm": "OpenCV StereoBM blockSize 21 (X-Sobel prefilter)"}[args.mode],
                 "pairs_per_gpu": P, "global_batch": gpairs, "H": H, "W": W, "D": D,
                 "gather": world > 1 and not args.no_gather, "parallelism": f"pairs/dp{world}",
             },
@@ -242,7 +255,8 @@ def main():
                 "avg_launch_us": paths_avg_s * 1e6,
             },
             "pipeline_roofline": {
-                "model": "SURVEY §8d " + ("H·W·D·(4P+8)" if volume else "H·W·D·(1+P+4)+I/O")
+                "model": "SURVEY §8d " + ("H·W·D·(4P+8)" if volume else "H·W·(2+4+2+4) (no volume)" if bm
+                                          else "H·W·D·(1+P+4)+I/O")
                          + (" x2 matchers" if full else "") + " per pair",
                 "bytes_per_pair": survey_bytes,
                 "device_us_per_pair": pair_s * 1e6,
@@ -278,6 +292,13 @@ def cpu_baseline(args, H, W, D, p, lefts, rights, out0, volume, full=False):
 
         def one(i):
             return ref_c.compute_volume(vol0, p, 0.0, synthetic.VOLUME_SCALE)
+    elif args.mode == "bm":  # numpy restatement (vectorised over pixels, loops over d)
+        from oracle import bm_np
+        bp = dict(numDisparities=D, blockSize=21)
+        n = max(1, n // 4)
+
+        def one(i):
+            return bm_np.stereo_bm(lefts[i % len(lefts)], rights[i % len(rights)], bp)
     elif full:  # compute_disparity: C port for both matchers + the numpy WLS restatement
         from oracle import sgm_np, wls_np
         lp = dict(p, uniquenessRatio=0, disp12MaxDiff=1000000)

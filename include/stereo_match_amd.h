@@ -170,6 +170,36 @@ int sm_reproject_image_to_3d(sm_ctx* ctx, const void* disp, int disp_type, int H
 int sm_reproject_image_to_3d_device(sm_ctx* ctx, const void* d_disp, int disp_type, int nimg, int H, int W,
                                     const double* Q, int handle_missing, float* d_xyz);
 
+/* ---- StereoBM (the reference's method="BM" branch,
+ * stereo_vision/stereo_vision.py:164-166: cv2.StereoBM_create(numDisparities,
+ * blockSize)).  Fields follow cv::StereoBM's setters. */
+typedef struct sm_bm_params {
+    int min_disparity;
+    int num_disparities;   /* > 0, multiple of 16 */
+    int block_size;        /* SADWindowSize: odd, 5..255, < min(H, W) */
+    int pre_filter_type;   /* 1 = PREFILTER_XSOBEL (default); 0 = NORMALIZED_RESPONSE (SM_E_UNSUPPORTED) */
+    int pre_filter_size;   /* odd 5..255 (used by NORMALIZED_RESPONSE only) */
+    int pre_filter_cap;    /* 1..63 (31) */
+    int texture_threshold; /* 10 */
+    int uniqueness_ratio;  /* 15 */
+    int speckle_window_size;
+    int speckle_range;     /* in disparity x16 units, as cv::StereoBM */
+    int disp12_max_diff;   /* < 0: no left-right check (default -1) */
+} sm_bm_params;
+
+/* cv2.StereoBM_create(numDisparities, blockSize) defaults. */
+int sm_bm_default_params(int num_disparities, int block_size, sm_bm_params* out);
+/* ximgproc::createRightMatcher(StereoBM). */
+int sm_bm_right_matcher_params(const sm_bm_params* left, sm_bm_params* right_out);
+/* StereoBM::compute on host buffers (synchronous) / a device batch (asynchronous;
+ * pair i at +i*pair_stride_bytes, output at +i*H*W).  int16 disparity x16,
+ * invalid = 16*(minDisparity-1). */
+int sm_bm_compute(sm_ctx* ctx, const uint8_t* left, const uint8_t* right, int H, int W, int stride,
+                  const sm_bm_params* p, int16_t* disp_out);
+int sm_bm_compute_batch_device(sm_ctx* ctx, const uint8_t* d_left, const uint8_t* d_right, int npairs,
+                               size_t pair_stride_bytes, int H, int W, int stride, const sm_bm_params* p,
+                               int16_t* d_disp_out);
+
 /* ximgproc::createRightMatcher(StereoSGBM) parameter derivation
  * (reference call: stereo_vision/stereo_vision.py:171). */
 int sm_right_matcher_params(const sm_params* left, sm_params* right_out);

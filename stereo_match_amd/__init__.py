@@ -12,7 +12,7 @@ C-ABI in ``include/stereo_match_amd.h``; there is no CPU fallback.
 """
 from .matcher import (STEREO_SGBM_MODE_HH, STEREO_SGBM_MODE_HH4, STEREO_SGBM_MODE_SGBM,
                       STEREO_SGBM_MODE_SGBM_3WAY, StereoSGBM, StereoSGBM_create, createRightMatcher,
-                      filterSpeckles)
+                      filterSpeckles, StereoBM, StereoBM_create)
 from .settings import DEFAULT_SETTINGS, parse_config_file
 from .stereo_vision import compute_disparity, matcher_from_settings
 from ._lib import SmError
@@ -22,6 +22,6 @@ __all__ = [
     "compute_disparity", "matcher_from_settings", "StereoSGBM", "StereoSGBM_create", "createRightMatcher",
     "STEREO_SGBM_MODE_SGBM", "STEREO_SGBM_MODE_HH", "STEREO_SGBM_MODE_SGBM_3WAY", "STEREO_SGBM_MODE_HH4",
     "parse_config_file", "DEFAULT_SETTINGS", "SmError", "filterSpeckles", "reprojectImageTo3D",
-    "project_points_3D", "write_ply",
+    "project_points_3D", "write_ply", "StereoBM", "StereoBM_create",
 ]
 __version__ = "0.1.0"

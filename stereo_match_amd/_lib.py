@@ -46,6 +46,17 @@ class SmWlsParams(ctypes.Structure):
         return {n: getattr(self, n) for n, _ in self._fields_}
 
 
+class SmBmParams(ctypes.Structure):
+    """Mirror of ``struct sm_bm_params``."""
+    _fields_ = [(n, ctypes.c_int) for n in (
+        "min_disparity", "num_disparities", "block_size", "pre_filter_type", "pre_filter_size",
+        "pre_filter_cap", "texture_threshold", "uniqueness_ratio", "speckle_window_size", "speckle_range",
+        "disp12_max_diff")]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
 _c = ctypes
 _SIGS = {
     "sm_version": (_c.c_char_p, []),
@@ -83,6 +94,12 @@ _SIGS = {
                                             _c.c_void_p, _c.c_int, _c.c_void_p]),
     "sm_reproject_image_to_3d_device": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_int, _c.c_int, _c.c_int, _c.c_int,
                                                    _c.c_void_p, _c.c_int, _c.c_void_p]),
+    "sm_bm_default_params": (_c.c_int, [_c.c_int, _c.c_int, _c.POINTER(SmBmParams)]),
+    "sm_bm_right_matcher_params": (_c.c_int, [_c.POINTER(SmBmParams), _c.POINTER(SmBmParams)]),
+    "sm_bm_compute": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_int, _c.c_int, _c.c_int,
+                                 _c.POINTER(SmBmParams), _c.c_void_p]),
+    "sm_bm_compute_batch_device": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_int, _c.c_size_t,
+                                              _c.c_int, _c.c_int, _c.c_int, _c.POINTER(SmBmParams), _c.c_void_p]),
     "sm_right_matcher_params": (_c.c_int, [_c.POINTER(SmParams), _c.POINTER(SmParams)]),
     "sm_synchronize": (_c.c_int, [_c.c_void_p]),
     "sm_set_timing": (_c.c_int, [_c.c_void_p, _c.c_int]),
@@ -329,6 +346,22 @@ class Engine:
         self._check(self._lib.sm_reproject_image_to_3d_device(self.ctx, ctypes.c_void_p(d_disp), kind, nimg, H, W,
                                                               Qd.ctypes.data, int(bool(handle_missing)),
                                                               ctypes.c_void_p(d_xyz)))
+
+    # -- StereoBM -------------------------------------------------------------------
+    def bm_compute(self, left: np.ndarray, right: np.ndarray, params: "SmBmParams") -> np.ndarray:
+        left = np.ascontiguousarray(left)
+        right = np.ascontiguousarray(right)
+        H, W = left.shape
+        out = np.empty((H, W), np.int16)
+        self._check(self._lib.sm_bm_compute(self.ctx, left.ctypes.data, right.ctypes.data, H, W, W,
+                                            ctypes.byref(params), out.ctypes.data))
+        return out
+
+    def bm_compute_batch_device(self, d_left: int, d_right: int, npairs: int, pair_stride: int, H: int, W: int,
+                                stride: int, params: "SmBmParams", d_out: int):
+        self._check(self._lib.sm_bm_compute_batch_device(
+            self.ctx, ctypes.c_void_p(d_left), ctypes.c_void_p(d_right), npairs, pair_stride, H, W, stride,
+            ctypes.byref(params), ctypes.c_void_p(d_out)))
 
     def synchronize(self):
         self._check(self._lib.sm_synchronize(self.ctx))

@@ -32,6 +32,7 @@
 #include "sm_wls.hpp"
 #include "sm_speckle.hpp"
 #include "sm_reproject.hpp"
+#include "sm_bm.hpp"
 
 #define SM_VERSION "stereo_match_amd 0.2.0 (gfx950)"
 
@@ -71,7 +72,7 @@ struct sm_ctx {
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;  // stream A
     hipStream_t side = nullptr;    // stream B
-    DevBuf img[2], planes, out, dbg, volbuf, sp_parent, sp_count, rp_in, rp_out, rp_min;
+    DevBuf img[2], planes, out, dbg, volbuf, sp_parent, sp_count, rp_in, rp_out, rp_min, bm_pre[2], bm_cost;
     DevBuf wls_num, wls_den, wls_inter, wls_w, wls_disp[2], wls_out;  // WLS scratch
     BufSet set[2];
     int next_set = 0;
@@ -750,6 +751,150 @@ int run_wls(sm_ctx* ctx, const int16_t* dl, const int16_t* dr, size_t disp_pair,
     return SM_OK;
 }
 
+
+// ---- StereoBM (sm_bm.hpp) --------------------------------------------------------
+struct BmNorm {
+    int minD, ndisp, SW2, cap, tex, uniq, sws, srange, d12;
+    int lofs, rofs, width1;
+    int vx, vy, vw, vh;  // valid disparity ROI
+};
+
+int normalize_bm(sm_ctx* ctx, const sm_bm_params* p, int H, int W, BmNorm& n)
+{
+    if (!p) return fail(ctx, SM_E_ARG, "params is NULL");
+    if (H <= 0 || W <= 0) return fail(ctx, SM_E_ARG, "empty image (%dx%d)", W, H);
+    if (p->pre_filter_type != 0 && p->pre_filter_type != 1) return fail(ctx, SM_E_ARG, "preFilterType must be 0 or 1");
+    if (p->pre_filter_size < 5 || p->pre_filter_size > 255 || p->pre_filter_size % 2 == 0)
+        return fail(ctx, SM_E_ARG, "preFilterSize must be odd and in [5, 255]");
+    if (p->pre_filter_cap < 1 || p->pre_filter_cap > 63) return fail(ctx, SM_E_ARG, "preFilterCap must be in [1, 63]");
+    const int bs = p->block_size;
+    if (bs < 5 || bs > 255 || bs % 2 == 0 || bs >= std::min(H, W))
+        return fail(ctx, SM_E_ARG, "blockSize must be odd, in [5, 255] and < min(width, height)");
+    if (p->num_disparities <= 0 || p->num_disparities % 16 != 0)
+        return fail(ctx, SM_E_ARG, "numDisparities must be a positive multiple of 16");
+    if (p->num_disparities > 256) return fail(ctx, SM_E_UNSUPPORTED, "numDisparities %d > 256 not built", p->num_disparities);
+    if (p->texture_threshold < 0 || p->uniqueness_ratio < 0)
+        return fail(ctx, SM_E_ARG, "textureThreshold / uniquenessRatio must be >= 0");
+    if (p->pre_filter_type == 0)
+        return fail(ctx, SM_E_UNSUPPORTED, "PREFILTER_NORMALIZED_RESPONSE is not implemented on the GPU path");
+    n.minD = p->min_disparity;
+    n.ndisp = p->num_disparities;
+    n.SW2 = bs / 2;
+    n.cap = p->pre_filter_cap;
+    n.tex = p->texture_threshold;
+    n.uniq = p->uniqueness_ratio;
+    n.sws = p->speckle_window_size;
+    n.srange = p->speckle_range;
+    n.d12 = p->disp12_max_diff;
+    n.lofs = std::max(n.ndisp - 1 + n.minD, 0);
+    n.rofs = -std::min(n.ndisp - 1 + n.minD, 0);
+    n.width1 = W - n.rofs - n.ndisp + 1;
+    const int maxD = n.minD + n.ndisp - 1;
+    const int xmin = std::max(0, maxD) + n.SW2, xmax = W - n.SW2, ymin = n.SW2, ymax = H - n.SW2;
+    if (xmax - xmin > 0 && ymax - ymin > 0) {
+        n.vx = xmin;
+        n.vy = ymin;
+        n.vw = xmax - xmin;
+        n.vh = ymax - ymin;
+    } else {
+        n.vx = n.vy = n.vw = n.vh = 0;
+    }
+    if (n.d12 >= 0 && (long long)n.d12 * 16 > 0x7FFFFFFF) n.d12 = 0x7FFFFFFF / 16;
+    return SM_OK;
+}
+
+int run_bm(sm_ctx* ctx, const uint8_t* dL, const uint8_t* dR, size_t pair_stride, int npairs, int H, int W,
+           int stride, const BmNorm& n, int16_t* d_out)
+{
+    if (npairs <= 0) return SM_OK;
+    const size_t npx = (size_t)H * W;
+    const int FILTERED = (n.minD - 1) * 16;
+    const int xs = std::max(0, n.vx - n.lofs), xe = std::min(n.width1, n.vx + n.vw - n.lofs);
+    const bool region = !(n.lofs >= W || n.rofs >= W || n.width1 < 1 || n.vw == 0 || xe <= xs);
+    // strip width: largest of 64/32/16/8 whose LDS fits in 64 KB
+    int sws = 0;
+    size_t lds = 0;
+    for (int c : {64, 32, 16, 8}) {
+        const int NC = c + 2 * n.SW2;
+        const size_t b = ((size_t)NC * n.ndisp + (size_t)c * n.ndisp + NC + c) * 4 + 2 * (2 * (size_t)NC + n.ndisp) + 16;
+        if (b <= 65536) {
+            sws = c;
+            lds = b;
+            break;
+        }
+    }
+    if (region && !sws) return fail(ctx, SM_E_UNSUPPORTED, "blockSize/numDisparities too large for the GPU BM kernel");
+    const int G = std::min(npairs, kMaxGroup);
+    int rc;
+    for (int i = 0; i < 2; i++)
+        if ((rc = ensure(ctx, ctx->bm_pre[i], (size_t)G * npx)) != SM_OK) return rc;
+    if ((rc = ensure(ctx, ctx->bm_cost, (size_t)G * npx * 4)) != SM_OK) return rc;
+    StageTimer tt(ctx, ctx->stream, SM_STAGE_TOTAL, npairs);
+    for (int p0 = 0; p0 < npairs; p0 += G) {
+        const int g = std::min(G, npairs - p0);
+        int16_t* out = d_out + (size_t)p0 * npx;
+        hipLaunchKernelGGL(smk::k_bm_fill, dim3((unsigned)((npx + 255) / 256), g), dim3(256), 0, ctx->stream, out, npx,
+                           (int16_t)FILTERED);
+        if (region) {
+            {
+                StageTimer t(ctx, ctx->stream, SM_STAGE_COST, g);
+                smk::BmPrefilterArgs pa{};
+                pa.img[0] = dL + (size_t)p0 * pair_stride;
+                pa.img[1] = dR + (size_t)p0 * pair_stride;
+                pa.in_pair = pair_stride;
+                pa.stride = stride;
+                pa.out[0] = (uint8_t*)ctx->bm_pre[0].p;
+                pa.out[1] = (uint8_t*)ctx->bm_pre[1].p;
+                pa.H = H;
+                pa.W = W;
+                pa.cap = n.cap;
+                hipLaunchKernelGGL(smk::k_bm_prefilter, dim3((W + 255) / 256, H, 2 * g), dim3(256), 0, ctx->stream, pa);
+            }
+            StageTimer t(ctx, ctx->stream, SM_STAGE_WTA, g);
+            smk::BmArgs ba{};
+            ba.Lp = (const uint8_t*)ctx->bm_pre[0].p;
+            ba.Rp = (const uint8_t*)ctx->bm_pre[1].p;
+            ba.disp = out;
+            ba.cost = (int*)ctx->bm_cost.p;
+            ba.H = H;
+            ba.W = W;
+            ba.ndisp = n.ndisp;
+            ba.mind0 = n.minD;
+            ba.lofs = n.lofs;
+            ba.rofs = n.rofs;
+            ba.SW2 = n.SW2;
+            ba.cap = n.cap;
+            ba.tex_thresh = n.tex;
+            ba.uniq = n.uniq;
+            ba.xs = xs;
+            ba.xe = xe;
+            ba.y0 = n.vy;
+            ba.y1 = n.vy + n.vh;
+            ba.SWs = sws;
+            ba.band = 64;
+            ba.FILTERED = FILTERED;
+            const dim3 grid((unsigned)((xe - xs + sws - 1) / sws), (unsigned)((n.vh + ba.band - 1) / ba.band), g);
+            hipLaunchKernelGGL(smk::k_bm_sad, grid, dim3(256), lds, ctx->stream, ba);
+            HIP_TRY(ctx, hipGetLastError());
+            if (n.d12 >= 0) {
+                smk::BmValidateArgs va{};
+                va.disp = out;
+                va.cost = (const int*)ctx->bm_cost.p;
+                va.H = H;
+                va.W = W;
+                va.minD = n.minD;
+                va.ndisp = n.ndisp;
+                va.maxdiff16 = n.d12 * 16;
+                hipLaunchKernelGGL(smk::k_bm_validate, dim3(H, g), dim3(256), (size_t)W * 13, ctx->stream, va);
+                HIP_TRY(ctx, hipGetLastError());
+            }
+        }
+        if (n.sws > 0 && n.srange >= 0)
+            if ((rc = run_speckles(ctx, ctx->stream, out, g, H, W, FILTERED, n.sws, n.srange)) != SM_OK) return rc;
+    }
+    return SM_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -786,7 +931,8 @@ void sm_destroy(sm_ctx* ctx)
     DevBuf* bufs[] = {&ctx->img[0],  &ctx->img[1],  &ctx->planes,    &ctx->out,         &ctx->dbg,
                       &ctx->volbuf,  &ctx->wls_num, &ctx->wls_den,   &ctx->wls_inter,   &ctx->wls_disp[0], &ctx->wls_w,
                       &ctx->wls_disp[1], &ctx->wls_out, &ctx->sp_parent, &ctx->sp_count,
-                      &ctx->rp_in,   &ctx->rp_out,  &ctx->rp_min};
+                      &ctx->rp_in,   &ctx->rp_out,  &ctx->rp_min,    &ctx->bm_pre[0],   &ctx->bm_pre[1],
+                      &ctx->bm_cost};
     for (DevBuf* b : bufs)
         if (b->p) (void)hipFree(b->p);
     for (auto& bs : ctx->set) {
@@ -1133,6 +1279,73 @@ int sm_reproject_image_to_3d(sm_ctx* ctx, const void* disp, int disp_type, int H
                                               (float*)ctx->rp_out.p)) != SM_OK)
         return rc;
     HIP_TRY(ctx, hipMemcpyAsync(xyz, ctx->rp_out.p, npx * 12, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return SM_OK;
+}
+
+int sm_bm_default_params(int num_disparities, int block_size, sm_bm_params* out)
+{
+    if (!out) return fail(nullptr, SM_E_ARG, "out is NULL");
+    out->min_disparity = 0;
+    out->num_disparities = num_disparities;
+    out->block_size = block_size;
+    out->pre_filter_type = 1;
+    out->pre_filter_size = 9;
+    out->pre_filter_cap = 31;
+    out->texture_threshold = 10;
+    out->uniqueness_ratio = 15;
+    out->speckle_window_size = 0;
+    out->speckle_range = 0;
+    out->disp12_max_diff = -1;
+    return SM_OK;
+}
+
+int sm_bm_right_matcher_params(const sm_bm_params* left, sm_bm_params* right)
+{
+    if (!left || !right) return fail(nullptr, SM_E_ARG, "NULL params");
+    sm_bm_default_params(left->num_disparities, left->block_size, right);
+    right->min_disparity = -(left->min_disparity + left->num_disparities) + 1;
+    right->texture_threshold = 0;
+    right->uniqueness_ratio = 0;
+    right->disp12_max_diff = 1000000;
+    right->speckle_window_size = 0;
+    return SM_OK;
+}
+
+int sm_bm_compute_batch_device(sm_ctx* ctx, const uint8_t* dL, const uint8_t* dR, int npairs, size_t pair_stride,
+                               int H, int W, int stride, const sm_bm_params* p, int16_t* d_out)
+{
+    if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
+    if (npairs < 0) return fail(ctx, SM_E_ARG, "npairs < 0");
+    if (!dL || !dR || !d_out) return fail(ctx, SM_E_ARG, "NULL image/output pointer");
+    if (stride < W) return fail(ctx, SM_E_ARG, "stride %d < width %d", stride, W);
+    BmNorm n;
+    int rc = normalize_bm(ctx, p, H, W, n);
+    if (rc != SM_OK) return rc;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    return run_bm(ctx, dL, dR, pair_stride, npairs, H, W, stride, n, d_out);
+}
+
+int sm_bm_compute(sm_ctx* ctx, const uint8_t* L, const uint8_t* R, int H, int W, int stride, const sm_bm_params* p,
+                  int16_t* disp_out)
+{
+    if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
+    if (!L || !R || !disp_out) return fail(ctx, SM_E_ARG, "NULL image/output pointer");
+    if (stride < W) return fail(ctx, SM_E_ARG, "stride %d < width %d", stride, W);
+    BmNorm n;
+    int rc = normalize_bm(ctx, p, H, W, n);
+    if (rc != SM_OK) return rc;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    const size_t img = (size_t)H * W;
+    for (int i = 0; i < 2; i++)
+        if ((rc = ensure(ctx, ctx->img[i], img)) != SM_OK) return rc;
+    if ((rc = ensure(ctx, ctx->out, img * 2)) != SM_OK) return rc;
+    HIP_TRY(ctx, hipMemcpy2DAsync(ctx->img[0].p, W, L, stride, W, H, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpy2DAsync(ctx->img[1].p, W, R, stride, W, H, hipMemcpyHostToDevice, ctx->stream));
+    rc = run_bm(ctx, (const uint8_t*)ctx->img[0].p, (const uint8_t*)ctx->img[1].p, img, 1, H, W, W, n,
+                (int16_t*)ctx->out.p);
+    if (rc != SM_OK) return rc;
+    HIP_TRY(ctx, hipMemcpyAsync(disp_out, ctx->out.p, img * 2, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     return SM_OK;
 }

@@ -182,14 +182,107 @@ def StereoSGBM_create(minDisparity=0, numDisparities=16, blockSize=3, P1=0, P2=0
                       uniquenessRatio, speckleWindowSize, speckleRange, mode, cost, device)
 
 
-def createRightMatcher(matcher_left: StereoSGBM) -> StereoSGBM:
+PREFILTER_NORMALIZED_RESPONSE = 0
+PREFILTER_XSOBEL = 1
+
+
+class StereoBM:
+    """cv2.StereoBM work-alike (``cv2.StereoBM_create(numDisparities, blockSize)``,
+    reference: stereo_vision/stereo_vision.py:164-166).  The X-Sobel prefilter
+    (the default) is implemented; NORMALIZED_RESPONSE raises SmError."""
+
+    def __init__(self, numDisparities=0, blockSize=21, device=0):
+        self.minDisparity = 0
+        self.numDisparities = int(numDisparities)
+        self.blockSize = int(blockSize)
+        self.preFilterType = PREFILTER_XSOBEL
+        self.preFilterSize = 9
+        self.preFilterCap = 31
+        self.textureThreshold = 10
+        self.uniquenessRatio = 15
+        self.speckleWindowSize = 0
+        self.speckleRange = 0
+        self.disp12MaxDiff = -1
+        self.device = int(device)
+
+    def getMinDisparity(self): return self.minDisparity
+    def setMinDisparity(self, v): self.minDisparity = int(v)
+    def getNumDisparities(self): return self.numDisparities
+    def setNumDisparities(self, v): self.numDisparities = int(v)
+    def getBlockSize(self): return self.blockSize
+    def setBlockSize(self, v): self.blockSize = int(v)
+    def getPreFilterType(self): return self.preFilterType
+    def setPreFilterType(self, v): self.preFilterType = int(v)
+    def getPreFilterSize(self): return self.preFilterSize
+    def setPreFilterSize(self, v): self.preFilterSize = int(v)
+    def getPreFilterCap(self): return self.preFilterCap
+    def setPreFilterCap(self, v): self.preFilterCap = int(v)
+    def getTextureThreshold(self): return self.textureThreshold
+    def setTextureThreshold(self, v): self.textureThreshold = int(v)
+    def getUniquenessRatio(self): return self.uniquenessRatio
+    def setUniquenessRatio(self, v): self.uniquenessRatio = int(v)
+    def getSpeckleWindowSize(self): return self.speckleWindowSize
+    def setSpeckleWindowSize(self, v): self.speckleWindowSize = int(v)
+    def getSpeckleRange(self): return self.speckleRange
+    def setSpeckleRange(self, v): self.speckleRange = int(v)
+    def getDisp12MaxDiff(self): return self.disp12MaxDiff
+    def setDisp12MaxDiff(self, v): self.disp12MaxDiff = int(v)
+
+    def params(self) -> "_lib.SmBmParams":
+        return _lib.SmBmParams(self.minDisparity, self.numDisparities, self.blockSize, self.preFilterType,
+                               self.preFilterSize, self.preFilterCap, self.textureThreshold, self.uniquenessRatio,
+                               self.speckleWindowSize, self.speckleRange, self.disp12MaxDiff)
+
+    def compute(self, left, right, disparity=None):
+        """StereoBM::compute: numpy in → int16 numpy out; torch CUDA uint8
+        tensors → int16 CUDA tensor (torch's current stream)."""
+        prm = self.params()
+        if _is_torch_cuda(left) or _is_torch_cuda(right):
+            import torch
+
+            if left.shape != right.shape or left.dtype != torch.uint8 or left.dim() != 2:
+                raise ValueError("left/right must be same-shape 2-D torch.uint8 tensors")
+            left, right = left.contiguous(), right.contiguous()
+            H, W = left.shape
+            out = torch.empty((H, W), dtype=torch.int16, device=left.device)
+            eng = _lib.engine(left.device.index or 0)
+            eng.set_stream(torch.cuda.current_stream(left.device).cuda_stream)
+            eng.bm_compute_batch_device(left.data_ptr(), right.data_ptr(), 1, H * W, H, W, W, prm, out.data_ptr())
+            return out
+        left = np.asarray(left)
+        right = np.asarray(right)
+        _check_pair(left, right)
+        out = _lib.engine(self.device).bm_compute(left, right, prm)
+        if disparity is not None:
+            np.copyto(disparity, out)
+            return disparity
+        return out
+
+
+def StereoBM_create(numDisparities=0, blockSize=21, device=0):
+    """cv2.StereoBM_create (reference: stereo_vision/stereo_vision.py:165)."""
+    return StereoBM(numDisparities, blockSize, device)
+
+
+def createRightMatcher(matcher_left):
     """cv2.ximgproc.createRightMatcher (reference: stereo_vision/stereo_vision.py:171).
 
-    minDisparity = -(minD + numD) + 1, uniquenessRatio 0, disp12MaxDiff 1e6,
-    speckleWindowSize 0; P1, P2, mode, preFilterCap and blockSize copied.
+    StereoSGBM: minDisparity = -(minD + numD) + 1, uniquenessRatio 0,
+    disp12MaxDiff 1e6, speckleWindowSize 0; P1, P2, mode, preFilterCap and
+    blockSize copied.  StereoBM: a fresh StereoBM(numD, blockSize) with that
+    minDisparity, textureThreshold 0, uniquenessRatio 0, disp12MaxDiff 1e6,
+    speckleWindowSize 0.
     """
+    if isinstance(matcher_left, StereoBM):
+        r = StereoBM(matcher_left.numDisparities, matcher_left.blockSize, matcher_left.device)
+        r.setMinDisparity(-(matcher_left.minDisparity + matcher_left.numDisparities) + 1)
+        r.setTextureThreshold(0)
+        r.setUniquenessRatio(0)
+        r.setDisp12MaxDiff(1000000)
+        r.setSpeckleWindowSize(0)
+        return r
     if not isinstance(matcher_left, StereoSGBM):
-        raise SmError(_lib.SM_E_UNSUPPORTED, "createRightMatcher: only StereoSGBM matchers are implemented")
+        raise SmError(_lib.SM_E_UNSUPPORTED, "createRightMatcher: only StereoSGBM / StereoBM matchers are implemented")
     m = matcher_left
     return StereoSGBM(minDisparity=-(m.minDisparity + m.numDisparities) + 1, numDisparities=m.numDisparities,
                       blockSize=m.blockSize, P1=m.P1, P2=m.P2, disp12MaxDiff=1000000,

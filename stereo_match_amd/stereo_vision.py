@@ -39,7 +39,8 @@ def matcher_from_settings(disparity_settings, method="SGBM", device=0):
                                     cost=disparity_settings.get('cost', 'sgbm'),
                                     device=device)
     elif method == "BM":
-        raise SmError(SM_E_UNSUPPORTED, "StereoBM is not implemented on the GPU path (DESIGN.md §8 next rows)")
+        return _m.StereoBM_create(numDisparities=disparity_settings['num_disparities'],
+                                  blockSize=disparity_settings['block_size'], device=device)
     else:
         raise RuntimeError('Method not supported')
 

@@ -122,13 +122,28 @@ def _is_torch_cuda(x) -> bool:
 
 
 def createDisparityWLSFilter(matcher_left):
-    """ximgproc::createDisparityWLSFilter — mutates ``matcher_left`` like upstream."""
+    """ximgproc::createDisparityWLSFilter — mutates ``matcher_left`` like upstream
+    (disp12MaxDiff 1e6, speckleWindowSize 0; StereoBM also textureThreshold 0 and
+    uniquenessRatio 0; StereoSGBM uniquenessRatio 0) and sets the valid-ROI
+    offsets (BM: + blockSize/2 on every side) and the discontinuity radius
+    (BM: ceil(0.33*blockSize), SGBM: ceil(0.5*blockSize))."""
+    from .matcher import StereoBM
+
     matcher_left.setDisp12MaxDiff(1000000)
     matcher_left.setSpeckleWindowSize(0)
-    matcher_left.setUniquenessRatio(0)
     min_disp = matcher_left.getMinDisparity()
     num_disp = matcher_left.getNumDisparities()
     wsize = matcher_left.getBlockSize()
+    wsize2 = wsize // 2
+    if isinstance(matcher_left, StereoBM):
+        matcher_left.setTextureThreshold(0)
+        matcher_left.setUniquenessRatio(0)
+        f = DisparityWLSFilter(True, max(0, min_disp + num_disp) + wsize2, max(0, -min_disp) + wsize2, wsize2,
+                               wsize2, min_disp)
+        f.setDepthDiscontinuityRadius(int(math.ceil(0.33 * wsize)))
+        f.device = getattr(matcher_left, "device", 0)
+        return f
+    matcher_left.setUniquenessRatio(0)
     f = DisparityWLSFilter(True, max(0, min_disp + num_disp), max(0, -min_disp), 0, 0, min_disp)
     f.setDepthDiscontinuityRadius(int(math.ceil(0.5 * wsize)))
     f.device = getattr(matcher_left, "device", 0)

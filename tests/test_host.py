@@ -63,8 +63,21 @@ def test_matcher_from_settings_p1_p2():
 def test_method_errors_like_reference():
     with pytest.raises(RuntimeError, match="Method not supported"):
         matcher_from_settings(settings.DEFAULT_SETTINGS, method="ELAS")
-    with pytest.raises(sm.SmError):
-        matcher_from_settings(settings.DEFAULT_SETTINGS, method="BM")
+    bm = matcher_from_settings(settings.DEFAULT_SETTINGS, method="BM")
+    assert isinstance(bm, sm.StereoBM)
+    assert (bm.getNumDisparities(), bm.getBlockSize(), bm.getTextureThreshold(), bm.getDisp12MaxDiff()) == \
+        (160, 5, 10, -1)
+
+
+def test_bm_right_matcher_and_wls_mutation():
+    bm = sm.StereoBM_create(numDisparities=64, blockSize=15)
+    r = sm.createRightMatcher(bm)
+    assert (r.getMinDisparity(), r.getTextureThreshold(), r.getUniquenessRatio(), r.getDisp12MaxDiff()) == \
+        (-63, 0, 0, 1000000)
+    f = wls.createDisparityWLSFilter(bm)
+    assert (bm.getTextureThreshold(), bm.getUniquenessRatio(), bm.getDisp12MaxDiff()) == (0, 0, 1000000)
+    assert (f.left_offset, f.right_offset, f.top_offset, f.bottom_offset) == (64 + 7, 7, 7, 7)
+    assert f.getDepthDiscontinuityRadius() == 5  # ceil(0.33 * 15)
 
 
 def test_create_right_matcher():

@@ -219,3 +219,39 @@ def test_volume_rejects_bad_shapes():
         ref_c.compute_volume(np.zeros((16, 4, 40), np.float32), dict(numDisparities=32))
     with pytest.raises(ValueError):  # P2 outside the int16-exact range
         sgm_np.compute_volume(np.zeros((16, 4, 40), np.float32), dict(numDisparities=16, P2=20000))
+
+
+# ---------------------------------------------------------------- StereoBM
+def test_bm_prefilter_xsobel_kat():
+    from oracle import bm_np
+
+    img = np.zeros((5, 6), np.uint8)
+    img[:, 3:] = 100  # vertical step between x=2 and x=3
+    p = bm_np.prefilter_xsobel(img, 31)
+    assert np.all(p[:, 0] == 31) and np.all(p[:, -1] == 31)
+    assert np.all(p[:4, 2] == 62) and np.all(p[:4, 3] == 62)  # 4*100 clipped to +cap
+    assert np.all(p[:4, 1] == 31) and np.all(p[:4, 4] == 31)
+    assert np.all(p[4] == 31)  # odd height: last row = cap
+
+
+def test_bm_constant_shift_recovered():
+    from oracle import bm_np
+
+    left, right = synthetic.shifted_pair(60, 200, 7, seed=3)
+    out = bm_np.stereo_bm(left, right, dict(numDisparities=32, blockSize=9, uniquenessRatio=0,
+                                            textureThreshold=0))
+    roi = out[4:-4, 31 + 4:-4]
+    assert np.mean(np.abs(roi.astype(int) - 112) <= 2) > 0.97
+    assert np.all(out[:4] == -16) and np.all(out[:, :31 + 4] == -16)
+
+
+def test_bm_validate_and_arguments():
+    from oracle import bm_np
+
+    left, right, _ = synthetic.random_dot_pair(40, 120, 32, seed=4)
+    a = bm_np.stereo_bm(left, right, dict(numDisparities=32, blockSize=7, disp12MaxDiff=1))
+    b = bm_np.stereo_bm(left, right, dict(numDisparities=32, blockSize=7))
+    assert np.all((a == b) | (a == -16))
+    for bad in (dict(blockSize=4), dict(blockSize=6), dict(numDisparities=24), dict(preFilterCap=64)):
+        with pytest.raises(ValueError):
+            bm_np.stereo_bm(left, right, dict(dict(numDisparities=32, blockSize=7), **bad))
