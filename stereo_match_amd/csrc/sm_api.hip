@@ -513,42 +513,42 @@ int run_group(sm_ctx* ctx, const Src& src, const Geo& g, const Norm& n, int16_t*
                                smem, ctx->stream, va);
             HIP_TRY(ctx, hipGetLastError());
         } else {
-            if ((rc = ensure(ctx, ctx->planes, (size_t)H * W * 12)) != SM_OK) return rc;
+            if ((rc = ensure(ctx, ctx->planes, (size_t)G * 2 * H * W * 8)) != SM_OK) return rc;
             if ((rc = ensure(ctx, bs.cost, (size_t)G * g.vol * 2)) != SM_OK) return rc;
-            for (int i = 0; i < G; i++) {
-                smk::PrefilterArgs pf{};
-                pf.img[0] = dL + (size_t)i * pair_stride;
-                pf.img[1] = dR + (size_t)i * pair_stride;
-                pf.planes = (uint8_t*)ctx->planes.p;
-                pf.H = H;
-                pf.W = W;
-                pf.stride = g.stride;
-                pf.ftzero = n.ftzero;
-                hipLaunchKernelGGL(smk::k_sgbm_prefilter, dim3((W + 255) / 256, H, 2), dim3(256), 0, ctx->stream, pf);
-                HIP_TRY(ctx, hipGetLastError());
-                smk::SgbmCostArgs sc{};
-                sc.planes = pf.planes;
-                sc.C = (uint16_t*)bs.cost.p + (size_t)i * g.vol;
-                sc.H = H;
-                sc.W = W;
-                sc.width1 = n.width1;
-                sc.D = n.D;
-                sc.minD = n.minD;
-                sc.minX1 = n.minX1;
-                sc.SW2 = n.bs / 2;
-                sc.SH2 = n.bs / 2;
-                sc.Yc = std::max(1, H - n.bs / 2);
-                hipLaunchKernelGGL(smk::k_sgbm_cost,
-                                   dim3((n.width1 + smk::SC_TX - 1) / smk::SC_TX, (sc.Yc + smk::SC_TY - 1) / smk::SC_TY,
-                                        n.D / 8),
-                                   dim3(256), 0, ctx->stream, sc);
-                HIP_TRY(ctx, hipGetLastError());
-                if (sc.Yc < H) {
-                    const size_t row = (size_t)n.width1 * n.D;
+            smk::PrefilterArgs pf{};
+            pf.img[0] = dL;
+            pf.img[1] = dR;
+            pf.in_pair = pair_stride;
+            pf.planes = (uint8_t*)ctx->planes.p;
+            pf.H = H;
+            pf.W = W;
+            pf.stride = g.stride;
+            pf.ftzero = n.ftzero;
+            hipLaunchKernelGGL(smk::k_sgbm_prefilter, dim3((W + 255) / 256, H, 2 * G), dim3(256), 0, ctx->stream, pf);
+            HIP_TRY(ctx, hipGetLastError());
+            smk::SgbmCostArgs sc{};
+            sc.planes = (const uint2*)ctx->planes.p;
+            sc.C = (uint16_t*)bs.cost.p;
+            sc.C_pair = g.vol;
+            sc.H = H;
+            sc.W = W;
+            sc.width1 = n.width1;
+            sc.D = n.D;
+            sc.minD = n.minD;
+            sc.minX1 = n.minX1;
+            sc.SW2 = n.bs / 2;
+            sc.SH2 = n.bs / 2;
+            sc.Yc = std::max(1, H - n.bs / 2);
+            hipLaunchKernelGGL(smk::k_sgbm_cost,
+                               dim3((n.width1 + smk::SC_TX - 1) / smk::SC_TX, (sc.Yc + smk::SC_TY - 1) / smk::SC_TY, G),
+                               dim3(256), 0, ctx->stream, sc);
+            HIP_TRY(ctx, hipGetLastError());
+            if (sc.Yc < H) {
+                const size_t row = (size_t)n.width1 * n.D;
+                for (int i = 0; i < G; i++)
                     hipLaunchKernelGGL(smk::k_sgbm_cost_tail, dim3(grid_for((size_t)(H - sc.Yc) * row / 8)), dim3(256), 0,
-                                       ctx->stream, sc.C, H, sc.Yc, row, (int)(n.mode == SM_MODE_HH));
-                    HIP_TRY(ctx, hipGetLastError());
-                }
+                                       ctx->stream, sc.C + (size_t)i * g.vol, H, sc.Yc, row, (int)(n.mode == SM_MODE_HH));
+                HIP_TRY(ctx, hipGetLastError());
             }
         }
     }

@@ -109,7 +109,8 @@ __global__ void __launch_bounds__(256) k_census_cost(CensusCostArgs a)
 // forced to ftzero at x = 0 and x = W-1); k 0 = value, 1 = BT min, 2 = BT max.
 struct PrefilterArgs {
     const uint8_t* img[2];
-    uint8_t* planes;
+    size_t in_pair;  // bytes between pairs' images
+    uint8_t* planes;  // packed uint2 per pixel, [pair][view][H][W]
     int H, W, stride, ftzero;
 };
 
@@ -129,12 +130,16 @@ __device__ __forceinline__ int raw_px(const uint8_t* img, int stride, int W, int
     return img[(size_t)y * stride + x];
 }
 
+// Packed per-pixel planes for the BT cost: one uint2 per pixel per view,
+// bytes [g, g_min, g_max, raw, raw_min, raw_max, 0, 0] (g = clipped Sobel-x,
+// min/max over the half-pixel neighbours as calcPixelCostBT); blockIdx.z =
+// 2*pair + view.
 __global__ void __launch_bounds__(256) k_sgbm_prefilter(PrefilterArgs a)
 {
-    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y, im = blockIdx.z;
+    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y, im = blockIdx.z & 1, pair = blockIdx.z >> 1;
     if (x >= a.W) return;
-    const uint8_t* img = a.img[im];
-    const size_t plane = (size_t)a.H * a.W;
+    const uint8_t* img = a.img[im] + (size_t)pair * a.in_pair;
+    uint32_t b[6];
     for (int ch = 0; ch < 2; ch++) {
         int v, vl, vr;
         if (ch == 0) {
@@ -146,27 +151,14 @@ __global__ void __launch_bounds__(256) k_sgbm_prefilter(PrefilterArgs a)
             vl = x > 0 ? (v + raw_px(img, a.stride, a.W, y, x - 1, a.ftzero)) / 2 : v;
             vr = x < a.W - 1 ? (v + raw_px(img, a.stride, a.W, y, x + 1, a.ftzero)) / 2 : v;
         }
-        uint8_t* base = a.planes + ((size_t)(im * 2 + ch) * 3) * plane + (size_t)y * a.W + x;
-        base[0] = (uint8_t)v;
-        base[plane] = (uint8_t)min(min(vl, vr), v);
-        base[2 * plane] = (uint8_t)max(max(vl, vr), v);
+        b[3 * ch] = (uint32_t)v;
+        b[3 * ch + 1] = (uint32_t)min(min(vl, vr), v);
+        b[3 * ch + 2] = (uint32_t)max(max(vl, vr), v);
     }
-}
-
-__device__ __forceinline__ int bt_pix(const uint8_t* planes, size_t plane, int W, int y, int X, int xr)
-{
-    int acc = 0;
-#pragma unroll
-    for (int ch = 0; ch < 2; ch++) {
-        const uint8_t* L = planes + ((size_t)(0 * 2 + ch) * 3) * plane + (size_t)y * W;
-        const uint8_t* R = planes + ((size_t)(1 * 2 + ch) * 3) * plane + (size_t)y * W;
-        int u = L[X], u0 = L[plane + X], u1 = L[2 * plane + X];
-        int v = R[xr], v0 = R[plane + xr], v1 = R[2 * plane + xr];
-        int c0 = max(max(0, u - v1), v0 - u);
-        int c1 = max(max(0, v - u1), u0 - v);
-        acc += min(c0, c1) >> (ch == 0 ? 0 : 2);
-    }
-    return acc;
+    uint2 w;
+    w.x = b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
+    w.y = b[4] | (b[5] << 8);
+    reinterpret_cast<uint2*>(a.planes)[((size_t)(pair * 2 + im) * a.H + y) * a.W + x] = w;
 }
 
 // C_true[y][x1][d] for the rows OpenCV's incremental box filter actually
@@ -174,11 +166,12 @@ __device__ __forceinline__ int bt_pix(const uint8_t* planes, size_t plane, int W
 //   sum_{k=y-SH2..y+SH2} sum_{j=-SW2..SW2} pix(clamp(k,0,H-1), clamp(x1+j,0,width1-1), d)
 // Tile of SC_TY rows x SC_TX columns x 8 disparities per workgroup: BT pixel
 // costs of the halo tile -> LDS, horizontal then vertical sums in LDS.
-constexpr int SC_TX = 64, SC_TY = 8, SC_MAXR = 5;  // blockSize <= 11
+constexpr int SC_TX = 64, SC_TY = 8, SC_MAXR = 5, SC_DC = 8;  // blockSize <= 11; disparities per chunk
 
 struct SgbmCostArgs {
-    const uint8_t* planes;
-    uint16_t* C;
+    const uint2* planes;  // packed, [pair][view][H][W]
+    uint16_t* C;          // [pair][H][width1][D]
+    size_t C_pair;
     int H, W, width1, D, minD, minX1, SW2, SH2, Yc;
 };
 
@@ -199,79 +192,85 @@ __device__ __forceinline__ int bt_cost2(uint2 L, uint2 R)
     return acc;
 }
 
+// One workgroup per SC_TY x SC_TX output tile and ALL disparities (chunks of
+// SC_DC): the left halo tile is staged once, the right planes once per chunk;
+// BT pixel costs -> LDS bytes, then horizontal and vertical box sums with
+// two disparities per 32-bit lane (SWAR; sums < 2^16 by the int16-exact
+// domain check, and the int16 wrap is the low 16 bits).
 __global__ void __launch_bounds__(256) k_sgbm_cost(SgbmCostArgs a)
 {
     constexpr int HR = SC_TY + 2 * SC_MAXR, HC = SC_TX + 2 * SC_MAXR;
-    __shared__ __attribute__((aligned(16))) uint2 lpl[HR][HC];      // left planes of the halo tile
-    __shared__ __attribute__((aligned(16))) uint2 rpl[HR][HC + 8];  // right planes, shifted by the disparities
-    __shared__ __attribute__((aligned(16))) uint8_t pix[HR][HC][8];
-    __shared__ __attribute__((aligned(16))) uint16_t hs[HR][SC_TX][8];
-    const int x0 = blockIdx.x * SC_TX, y0 = blockIdx.y * SC_TY, d0 = blockIdx.z * 8;
-    const int SW2 = a.SW2, SH2 = a.SH2, W1 = a.width1, W = a.W;
+    __shared__ __attribute__((aligned(16))) uint2 lpl[HR][HC];
+    __shared__ __attribute__((aligned(16))) uint2 rpl[HR][HC + SC_DC];
+    __shared__ __attribute__((aligned(16))) uint2 pix[HR][HC];           // SC_DC byte costs
+    __shared__ __attribute__((aligned(16))) uint4 hs[HR][SC_TX];         // SC_DC u16 sums
+    const int x0 = blockIdx.x * SC_TX, y0 = blockIdx.y * SC_TY, pair = blockIdx.z;
+    const int SW2 = a.SW2, SH2 = a.SH2, W1 = a.width1, W = a.W, D = a.D;
     const int rows_h = SC_TY + 2 * SH2, cols_h = SC_TX + 2 * SW2;
-    const size_t plane = (size_t)a.H * W;
+    const uint2* Lp = a.planes + (size_t)(pair * 2) * a.H * W;
+    const uint2* Rp = Lp + (size_t)a.H * W;
     const int xlo = max(x0 - SW2, 0), xhi = min(x0 + SC_TX + SW2 - 1, W1 - 1);  // clamped x1 range
-    const int rbase = xlo + a.minX1 - a.minD - d0 - 7;                           // right column of rpl[.][0]
-    const int rcols = xhi - xlo + 8;
-    auto gather = [&](int im, int y, int X) {
-        const uint8_t* b = a.planes + (size_t)(im * 6) * plane + (size_t)y * W + X;
-        uint2 w;
-        w.x = b[0] | (b[plane] << 8) | (b[2 * plane] << 16) | (b[3 * plane] << 24);
-        w.y = b[4 * plane] | (b[5 * plane] << 8);
-        return w;
-    };
+    const int rcols = xhi - xlo + SC_DC;
+    uint16_t* Cb = a.C + pair * a.C_pair;
     for (int i = threadIdx.x; i < rows_h * cols_h; i += 256) {
-        const int r = i / cols_h, c = i % cols_h;
+        const int r = i / cols_h, c = i - r * cols_h;
         const int y = min(max(y0 - SH2 + r, 0), a.H - 1);
-        lpl[r][c] = gather(0, y, min(max(x0 - SW2 + c, 0), W1 - 1) + a.minX1);
+        lpl[r][c] = Lp[(size_t)y * W + min(max(x0 - SW2 + c, 0), W1 - 1) + a.minX1];
     }
-    for (int i = threadIdx.x; i < rows_h * rcols; i += 256) {
-        const int r = i / rcols, c = i % rcols;
-        const int y = min(max(y0 - SH2 + r, 0), a.H - 1);
-        rpl[r][c] = gather(1, y, rbase + c);
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < rows_h * cols_h; i += 256) {
-        const int r = i / cols_h, c = i % cols_h;
-        const int x1 = min(max(x0 - SW2 + c, 0), W1 - 1);
-        const int ri = x1 - xlo + 7;  // right column index for disparity d0 (j = 0)
-        const uint2 L = lpl[r][c];
-        uint2 w;
-        uint8_t* pb = reinterpret_cast<uint8_t*>(&w);
-#pragma unroll
-        for (int j = 0; j < 8; j++) pb[j] = (uint8_t)bt_cost2(L, rpl[r][ri - j]);
-        *reinterpret_cast<uint2*>(&pix[r][c][0]) = w;
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < rows_h * SC_TX; i += 256) {
-        const int r = i / SC_TX, c = i % SC_TX;
-        uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        for (int j = 0; j <= 2 * SW2; j++) {
-            const uint2 w = *reinterpret_cast<const uint2*>(&pix[r][c + j][0]);
-            const uint8_t* pb = reinterpret_cast<const uint8_t*>(&w);
-#pragma unroll
-            for (int q = 0; q < 8; q++) acc[q] += pb[q];
+    for (int d0 = 0; d0 < D; d0 += SC_DC) {
+        const int rbase = xlo + a.minX1 - a.minD - d0 - (SC_DC - 1);  // right column of rpl[.][0]
+        __syncthreads();  // previous chunk done with rpl / hs
+        for (int i = threadIdx.x; i < rows_h * rcols; i += 256) {
+            const int r = i / rcols, c = i - r * rcols;
+            const int y = min(max(y0 - SH2 + r, 0), a.H - 1);
+            rpl[r][c] = Rp[(size_t)y * W + rbase + c];
         }
-        uint4 o;
-        o.x = acc[0] | (acc[1] << 16); o.y = acc[2] | (acc[3] << 16);
-        o.z = acc[4] | (acc[5] << 16); o.w = acc[6] | (acc[7] << 16);
-        *reinterpret_cast<uint4*>(&hs[r][c][0]) = o;
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < SC_TY * SC_TX; i += 256) {
-        const int r = i / SC_TX, c = i % SC_TX;
-        const int y = y0 + r, x1 = x0 + c;
-        if (y >= a.Yc || x1 >= W1) continue;
-        uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        for (int k = 0; k <= 2 * SH2; k++) {
-            const uint4 w = *reinterpret_cast<const uint4*>(&hs[r + k][c][0]);
-            acc[0] += w.x & 0xFFFF; acc[1] += w.x >> 16; acc[2] += w.y & 0xFFFF; acc[3] += w.y >> 16;
-            acc[4] += w.z & 0xFFFF; acc[5] += w.z >> 16; acc[6] += w.w & 0xFFFF; acc[7] += w.w >> 16;
+        __syncthreads();
+        for (int i = threadIdx.x; i < rows_h * cols_h; i += 256) {
+            const int r = i / cols_h, c = i - r * cols_h;
+            const int x1 = min(max(x0 - SW2 + c, 0), W1 - 1);
+            const int ri = x1 - xlo + SC_DC - 1;  // right column index for disparity d0
+            const uint2 L = lpl[r][c];
+            uint32_t b[SC_DC];
+#pragma unroll
+            for (int j = 0; j < SC_DC; j++) b[j] = (uint32_t)bt_cost2(L, rpl[r][ri - j]);
+            pix[r][c] = make_uint2(b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24),
+                                   b[4] | (b[5] << 8) | (b[6] << 16) | (b[7] << 24));
         }
-        uint4 o;  // int16 wrap == low 16 bits
-        o.x = (acc[0] & 0xFFFF) | (acc[1] << 16); o.y = (acc[2] & 0xFFFF) | (acc[3] << 16);
-        o.z = (acc[4] & 0xFFFF) | (acc[5] << 16); o.w = (acc[6] & 0xFFFF) | (acc[7] << 16);
-        *reinterpret_cast<uint4*>(a.C + ((size_t)y * W1 + x1) * a.D + d0) = o;
+        __syncthreads();
+        for (int i = threadIdx.x; i < rows_h * SC_TX; i += 256) {
+            const int r = i / SC_TX, c = i - r * SC_TX;
+            uint32_t e0 = 0, o0 = 0, e1 = 0, o1 = 0;  // u16 lanes: (d0,d2) (d1,d3) (d4,d6) (d5,d7)
+            for (int j = 0; j <= 2 * SW2; j++) {
+                const uint2 w = pix[r][c + j];
+                e0 += w.x & 0x00FF00FFu;
+                o0 += (w.x >> 8) & 0x00FF00FFu;
+                e1 += w.y & 0x00FF00FFu;
+                o1 += (w.y >> 8) & 0x00FF00FFu;
+            }
+            hs[r][c] = make_uint4(e0, o0, e1, o1);
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < SC_TY * SC_TX; i += 256) {
+            const int r = i / SC_TX, c = i - r * SC_TX;
+            const int y = y0 + r, x1 = x0 + c;
+            if (y >= a.Yc || x1 >= W1) continue;
+            uint32_t e0 = 0, o0 = 0, e1 = 0, o1 = 0;
+            for (int k = 0; k <= 2 * SH2; k++) {
+                const uint4 w = hs[r + k][c];
+                e0 += w.x;
+                o0 += w.y;
+                e1 += w.z;
+                o1 += w.w;
+            }
+            // interleave back to d order: (d0,d1) (d2,d3) (d4,d5) (d6,d7)
+            uint4 o;
+            o.x = (e0 & 0xFFFF) | (o0 << 16);
+            o.y = (e0 >> 16) | (o0 & 0xFFFF0000u);
+            o.z = (e1 & 0xFFFF) | (o1 << 16);
+            o.w = (e1 >> 16) | (o1 & 0xFFFF0000u);
+            *reinterpret_cast<uint4*>(Cb + ((size_t)y * W1 + x1) * D + d0) = o;
+        }
     }
 }
 
