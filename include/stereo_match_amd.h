@@ -200,6 +200,15 @@ int sm_bm_compute_batch_device(sm_ctx* ctx, const uint8_t* d_left, const uint8_t
                                size_t pair_stride_bytes, int H, int W, int stride, const sm_bm_params* p,
                                int16_t* d_disp_out);
 
+/* Multi-device batch from ONE process (SURVEY §8b sm_compute_batch): ctxs[k]
+ * (one per device) computes the contiguous shard [k*npairs/ngpu,
+ * (k+1)*npairs/ngpu) of the host pairs left[i]/right[i] (uint8 H x W,
+ * C-contiguous) into out + i*H*W (host).  One host thread per context;
+ * synchronous.  The scaling path the benchmark uses is one process per GPU
+ * (torch.distributed / RCCL); this is the single-process convenience. */
+int sm_compute_batch(sm_ctx** ctxs, int ngpu, const uint8_t* const* left, const uint8_t* const* right, int npairs,
+                     int H, int W, const sm_params* p, int16_t* out);
+
 /* ximgproc::createRightMatcher(StereoSGBM) parameter derivation
  * (reference call: stereo_vision/stereo_vision.py:171). */
 int sm_right_matcher_params(const sm_params* left, sm_params* right_out);

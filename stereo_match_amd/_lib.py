@@ -100,6 +100,9 @@ _SIGS = {
                                  _c.POINTER(SmBmParams), _c.c_void_p]),
     "sm_bm_compute_batch_device": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_int, _c.c_size_t,
                                               _c.c_int, _c.c_int, _c.c_int, _c.POINTER(SmBmParams), _c.c_void_p]),
+    "sm_compute_batch": (_c.c_int, [_c.POINTER(_c.c_void_p), _c.c_int, _c.POINTER(_c.c_void_p),
+                                    _c.POINTER(_c.c_void_p), _c.c_int, _c.c_int, _c.c_int, _c.POINTER(SmParams),
+                                    _c.c_void_p]),
     "sm_right_matcher_params": (_c.c_int, [_c.POINTER(SmParams), _c.POINTER(SmParams)]),
     "sm_synchronize": (_c.c_int, [_c.c_void_p]),
     "sm_set_timing": (_c.c_int, [_c.c_void_p, _c.c_int]),
@@ -404,6 +407,30 @@ def right_matcher_params(p: SmParams) -> SmParams:
     lib = load()
     out = SmParams()
     rc = lib.sm_right_matcher_params(ctypes.byref(p), ctypes.byref(out))
+    if rc != SM_OK:
+        _raise(rc, None)
+    return out
+
+
+def compute_batch(engines, lefts, rights, params: SmParams) -> np.ndarray:
+    """sm_compute_batch over several Engines (one per device): host pairs in,
+    int16 [n, H, W] out; pairs sharded contiguously across the engines."""
+    lib = load()
+    n = len(lefts)
+    if n != len(rights):
+        raise ValueError("lefts and rights differ in length")
+    if n == 0:
+        return np.empty((0, 0, 0), np.int16)
+    L = [np.ascontiguousarray(a, np.uint8) for a in lefts]
+    R = [np.ascontiguousarray(b, np.uint8) for b in rights]
+    H, W = L[0].shape
+    if any(a.shape != (H, W) for a in L + R):
+        raise ValueError("all images must have the same shape")
+    out = np.empty((n, H, W), np.int16)
+    ctxs = (ctypes.c_void_p * len(engines))(*[e.ctx for e in engines])
+    lp = (ctypes.c_void_p * n)(*[a.ctypes.data for a in L])
+    rp = (ctypes.c_void_p * n)(*[b.ctypes.data for b in R])
+    rc = lib.sm_compute_batch(ctxs, len(engines), lp, rp, n, H, W, ctypes.byref(params), out.ctypes.data)
     if rc != SM_OK:
         _raise(rc, None)
     return out

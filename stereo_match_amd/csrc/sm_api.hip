@@ -21,6 +21,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <type_traits>
 #include <vector>
 
@@ -1347,6 +1348,65 @@ int sm_bm_compute(sm_ctx* ctx, const uint8_t* L, const uint8_t* R, int H, int W,
     if (rc != SM_OK) return rc;
     HIP_TRY(ctx, hipMemcpyAsync(disp_out, ctx->out.p, img * 2, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return SM_OK;
+}
+
+// Multi-device batch from one process: ctxs[k] (one per device,
+// possibly the same device twice) takes the contiguous shard of pairs
+// [k*npairs/ngpu, (k+1)*npairs/ngpu); one host thread per context copies its
+// pairs in, runs sm_compute_batch_device on the context's stream and copies
+// the maps out.  Synchronous.  (The driver-facing scaling path is one process
+// per GPU over RCCL, bench.py; this entry point is for single-process callers.)
+int sm_compute_batch(sm_ctx** ctxs, int ngpu, const uint8_t* const* left, const uint8_t* const* right, int npairs,
+                     int H, int W, const sm_params* p, int16_t* out)
+{
+    if (!ctxs || ngpu <= 0) return fail(nullptr, SM_E_ARG, "need at least one context");
+    if (npairs < 0 || !left || !right || !out || !p) return fail(nullptr, SM_E_ARG, "bad batch arguments");
+    for (int k = 0; k < ngpu; k++)
+        if (!ctxs[k]) return fail(nullptr, SM_E_ARG, "ctxs[%d] is NULL", k);
+    if (npairs == 0) return SM_OK;
+    std::vector<int> rcs(ngpu, SM_OK);
+    auto work = [&](int k) {
+        sm_ctx* ctx = ctxs[k];
+        const int a = (int)((long long)npairs * k / ngpu), b = (int)((long long)npairs * (k + 1) / ngpu);
+        const int n = b - a;
+        if (n <= 0) return;
+        auto run = [&]() -> int {
+            HIP_TRY(ctx, hipSetDevice(ctx->device));
+            Norm nm;
+            int rc = normalize(ctx, p, H, W, nm);
+            if (rc != SM_OK) return rc;
+            const size_t img = (size_t)H * W;
+            for (int i = 0; i < 2; i++)
+                if ((rc = ensure(ctx, ctx->img[i], img * n)) != SM_OK) return rc;
+            if ((rc = ensure(ctx, ctx->out, img * 2 * n)) != SM_OK) return rc;
+            for (int i = 0; i < n; i++) {
+                if (!left[a + i] || !right[a + i]) return fail(ctx, SM_E_ARG, "pair %d has a NULL image", a + i);
+                HIP_TRY(ctx, hipMemcpyAsync((uint8_t*)ctx->img[0].p + img * i, left[a + i], img, hipMemcpyHostToDevice,
+                                            ctx->stream));
+                HIP_TRY(ctx, hipMemcpyAsync((uint8_t*)ctx->img[1].p + img * i, right[a + i], img,
+                                            hipMemcpyHostToDevice, ctx->stream));
+            }
+            Src src;
+            src.L = (const uint8_t*)ctx->img[0].p;
+            src.R = (const uint8_t*)ctx->img[1].p;
+            src.pair_stride = img;
+            if ((rc = run_pairs(ctx, src, n, H, W, W, nm, (int16_t*)ctx->out.p)) != SM_OK) return rc;
+            HIP_TRY(ctx, hipMemcpyAsync(out + img * a, ctx->out.p, img * 2 * n, hipMemcpyDeviceToHost, ctx->stream));
+            HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+            return SM_OK;
+        };
+        rcs[k] = run();
+    };
+    std::vector<std::thread> th;
+    for (int k = 1; k < ngpu; k++) th.emplace_back(work, k);
+    work(0);
+    for (auto& t : th) t.join();
+    for (int k = 0; k < ngpu; k++)
+        if (rcs[k] != SM_OK) {
+            g_thread_error = ctxs[k]->err;
+            return rcs[k];
+        }
     return SM_OK;
 }
 

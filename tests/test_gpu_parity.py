@@ -367,3 +367,22 @@ def test_speckle_filter_standalone_and_full_size(eng):
     exp = sgm_np.filter_speckles(base, -16, 100, 32)
     for _ in range(5):
         assert np.array_equal(eng.filter_speckles(base, -16, 100, 32), exp)
+
+
+def test_single_process_multi_context_batch():
+    """sm_compute_batch: host pairs sharded over several contexts (here two
+    contexts on the one GPU of the box, each on its own host thread)."""
+    engines = [_lib.Engine(0), _lib.Engine(0)]
+    try:
+        H, W, D = 48, 170, 32
+        pairs = [synthetic.random_dot_pair(H, W, D, seed=90 + i)[:2] for i in range(5)]
+        p = synthetic.headline_params(D)
+        out = _lib.compute_batch(engines, [a for a, _ in pairs], [b for _, b in pairs], synthetic.to_sm_params(p))
+        for i, (a, b) in enumerate(pairs):
+            assert np.array_equal(out[i], ref_c.compute(a, b, p)), i
+        with pytest.raises(ValueError):
+            _lib.compute_batch(engines, [pairs[0][0]], [pairs[0][1]],
+                               synthetic.to_sm_params(dict(p, numDisparities=24)))
+    finally:
+        for e in engines:
+            e.close()
