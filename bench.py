@@ -169,14 +169,16 @@ def main():
         P_dirs = 5 if args.mode in ("sgbm5", "disparity5") else 8
         eb = 1 if args.mode == "census8" else 2  # bytes per path element
         row_mode = args.row and D % 64 == 0  # both horizontal paths fused into the row/WTA kernel
-        census_b = 2 * H * W * 8 if args.mode == "census8" else 0
+        # census mode: the path kernel reads the precomputed u8 Hamming cost volume
+        # once per direction (k_census_cost8), like the u16 cost volume in SGBM mode
+        census_b = 0
         if row_mode:
             # paths launch: vertical family only; row kernel: E (+W) paths + WTA
-            paths_bytes = (P_dirs - 2) * vol * eb + (census_b or (P_dirs - 2) * vol * 2)
+            paths_bytes = (P_dirs - 2) * vol * eb + (census_b or (P_dirs - 2) * vol * eb)
             wta_bytes = vol * eb + (P_dirs - 1) * vol * eb + (census_b or 2 * vol * 2) + 2 * H * W
             wta_name = "k_row_wta (E/W paths + WTA + disp2/LR, one wave per row)"
         else:
-            paths_bytes = P_dirs * vol * eb + (census_b or P_dirs * vol * 2)
+            paths_bytes = P_dirs * vol * eb + (census_b or P_dirs * vol * eb)
             wta_bytes = P_dirs * vol * eb + 2 * H * W
             wta_name = "k_wta"
         if bm:  # SAD kernel reads the two prefiltered views, writes disparity (+ int32 cost)

@@ -251,7 +251,10 @@ long long sm_debug_fetch(sm_ctx* ctx, int what, void* host, size_t bytes);
  * results) runs WTA + median on a second internal stream, overlapped with
  * the next launch group's path aggregation (double-buffered volumes);
  * bit 9 (valid results, D % 64 == 0) uses 64-lane horizontal lines (one row
- * per wave) instead of 16-lane lines (4 rows per wave).
+ * per wave) instead of 16-lane lines (4 rows per wave); bit 10 (valid
+ * results, census) computes Hamming costs on the fly in every direction
+ * instead of reading the precomputed u8 cost volume, bit 11 only in the
+ * horizontal family; bits 16-19: launch-group size cap (0 = none).
  * 0 = normal operation. */
 int sm_set_debug_flags(sm_ctx* ctx, int flags);
 

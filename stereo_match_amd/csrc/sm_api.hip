@@ -64,7 +64,7 @@ struct BufSet {
 };
 
 // debug flags (sm_set_debug_flags); 1 skip horizontal, 2 skip vertical and 4 drop stores are read in-kernel
-constexpr int DBG_VL16 = 8, DBG_STORE_W = 16, DBG_ROW = 32, DBG_OVERLAP = 64, DBG_H64 = 512;
+constexpr int DBG_VL16 = 8, DBG_STORE_W = 16, DBG_ROW = 32, DBG_OVERLAP = 64, DBG_H64 = 512, DBG_NO_C8 = 1024;
 
 }  // namespace
 
@@ -265,6 +265,13 @@ struct Geo {  // per-group geometry shared by the launches
 
 bool row_mode(const sm_ctx* ctx, const Norm& n) { return (ctx->dbg_flags & DBG_ROW) && n.D % 64 == 0; }
 bool overlap(const sm_ctx* ctx) { return (ctx->dbg_flags & DBG_OVERLAP) != 0; }
+// census mode: the path kernels read a precomputed u8 Hamming cost volume
+// (k_census_cost8) instead of computing popcounts per direction; ablation
+// flag 1024 restores census-on-the-fly (flag 2048: only in the horizontal family)
+bool use_cost8(const sm_ctx* ctx, const Norm& n)
+{
+    return n.cost == SM_COST_CENSUS && !(ctx->dbg_flags & DBG_NO_C8) && n.D <= 256;
+}
 hipStream_t stream_b(const sm_ctx* ctx) { return overlap(ctx) ? ctx->side : ctx->stream; }
 
 // ---- stream A: path aggregation -------------------------------------------
@@ -282,6 +289,11 @@ int launch_paths_t(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs)
     pa.census_pair = g.census_pair;
     pa.cost = (const uint16_t*)bs.cost.p;
     pa.cost_pair = g.cost_pair;
+    pa.cost8 = nullptr;
+    if (use_cost8(ctx, n)) {
+        pa.cost8 = (const uint8_t*)bs.cost.p;
+        pa.cost_pair = g.vol;
+    }
     pa.L = (uint8_t*)bs.L.p;
     pa.slot_bytes = g.slot_bytes;
     pa.L_pair_bytes = g.L_pair;
@@ -414,6 +426,8 @@ int group_size(const sm_ctx* ctx, const Norm& n, int H, int npairs)
     const size_t g = std::max<size_t>(1, kSetBudget / std::max<size_t>(per, 1));
     // at least two groups per call when possible, so WTA(g) overlaps paths(g+1)
     const size_t half = overlap(ctx) ? std::max(1, (npairs + 1) / 2) : kMaxGroup;
+    const int cap = (ctx->dbg_flags >> 16) & 15;  // ablation: launch-group size cap (0 = none)
+    if (cap) return (int)std::min<size_t>({g, (size_t)cap, half});
     return (int)std::min<size_t>({g, (size_t)kMaxGroup, half});
 }
 
@@ -495,6 +509,24 @@ int run_group(sm_ctx* ctx, const Src& src, const Geo& g, const Norm& n, int16_t*
                                dim3((W + smk::CT_W - 1) / smk::CT_W, (H + smk::CT_H - 1) / smk::CT_H, 2 * G),
                                dim3(256), 0, ctx->stream, ca);
             HIP_TRY(ctx, hipGetLastError());
+            if (use_cost8(ctx, n)) {
+                if ((rc = ensure(ctx, bs.cost, (size_t)G * g.vol)) != SM_OK) return rc;
+                smk::Cost8Args c8{};
+                c8.cl = ca.out[0];
+                c8.cr = ca.out[1];
+                c8.census_pair = g.census_pair;
+                c8.C = (uint8_t*)bs.cost.p;
+                c8.C_pair = g.vol;
+                c8.H = H;
+                c8.W = W;
+                c8.width1 = n.width1;
+                c8.D = n.D;
+                c8.minD = n.minD;
+                c8.minX1 = n.minX1;
+                hipLaunchKernelGGL(smk::k_census_cost8, dim3((n.width1 + smk::C8_TX - 1) / smk::C8_TX, H, G), dim3(256),
+                                   0, ctx->stream, c8);
+                HIP_TRY(ctx, hipGetLastError());
+            }
         } else if (n.cost == SM_COST_VOLUME) {
             if ((rc = ensure(ctx, bs.cost, (size_t)G * g.vol * 2)) != SM_OK) return rc;
             smk::VolArgs va{};

@@ -33,6 +33,7 @@ struct PathsArgs {
     size_t census_pair;  // elements per pair
     const uint16_t* cost;  // SGBM cost volume [pair][H][width1][D]
     size_t cost_pair;      // elements per pair
+    const uint8_t* cost8;  // census mode: precomputed u8 Hamming cost volume for the vertical family, or null
     uint8_t* L;            // path volumes [pair][slot][H][width1][D] (LT)
     size_t slot_bytes, L_pair_bytes;
     int H, W, width1, D, minD, minX1, P1, P2;
@@ -94,6 +95,32 @@ __device__ __forceinline__ void horz_impl(const PathsArgs& a, int pair, int hb, 
     uint32_t minLp = 0;
 
     if constexpr (CENSUS) {
+        if (a.cost8 && !(a.dbg & 2048)) {  // costs from the precomputed u8 volume (same [H][W1][D] layout as L)
+            // ring of PF loads in flight: step s uses ring[s % PF], then refills it with step s + PF
+            constexpr int PF = 8;
+            const rsrc_t rc = make_rsrc(a.cost8 + (size_t)pair * a.cost_pair, (uint64_t)H * W1 * D);
+            RawBytes<DPL> ring[PF];
+#pragma unroll
+            for (int k = 0; k < PF; k++) ring[k].load(rc, k < W1 ? (uint32_t)(off0 + k * step_bytes) : kOOB);
+            int off = off0;
+            for (int s0 = 0; s0 < W1; s0 += PF) {
+#pragma unroll
+                for (int k = 0; k < PF; k++) {
+                    const int s = s0 + k;
+                    uint32_t C[DPL], Ln[DPL];
+#pragma unroll
+                    for (int i = 0; i < DPL; i++) C[i] = ring[k].template get<uint8_t>(i);
+                    ring[k].load(rc, s + PF < W1 ? (uint32_t)(off + PF * step_bytes) : kOOB);
+                    const uint32_t mn = sgm_step<LANES, DPL>(Lp, minLp, C, P1, P2, Ln);
+                    bstore_n<LT, DPL>(rout, (line_ok && s < W1) ? (uint32_t)off : kOOB, Ln);
+                    off += step_bytes;
+#pragma unroll
+                    for (int i = 0; i < DPL; i++) Lp[i] = Ln[i];
+                    minLp = mn;
+                }
+            }
+            return;
+        }
         const rsrc_t rcl = make_rsrc(a.cl + (size_t)pair * a.census_pair, (uint64_t)H * W * 8);
         const rsrc_t rcr = make_rsrc(a.cr + (size_t)pair * a.census_pair, (uint64_t)H * W * 8);
         const int fr_off = DIR == 0 ? -minD : -minD - (D - 1);
@@ -252,6 +279,29 @@ __device__ __forceinline__ void vert_family(const PathsArgs& a, int pair, int vb
     };
 
     if constexpr (CENSUS) {
+        if (a.cost8) {  // costs read from the precomputed u8 volume [pair][H][W1][D] (same layout as L)
+            const rsrc_t rc = make_rsrc(a.cost8 + (size_t)pair * a.cost_pair, (uint64_t)H * W1 * D);
+            int coff = off;
+            RawBytes<DPL> nxt;
+            nxt.load(rc, (uint32_t)coff);
+            for (int s = s_lo; s < s_hi; s++) {
+                uint32_t C[DPL], Ln[DPL];
+#pragma unroll
+                for (int i = 0; i < DPL; i++) C[i] = nxt.template get<uint8_t>(i);
+                coff += step_bytes;
+                nxt.load(rc, (uint32_t)coff);  // out-of-range offsets read 0 (inactive lines only)
+                const uint32_t mn = sgm_step<VL, DPL>(Lp, minLp, C, P1, P2, Ln);
+                const bool active = line_ok && x1 >= 0 && x1 < W1;
+                bstore_n<LT, DPL>(rout, active ? (uint32_t)off : kOOB, Ln);
+#pragma unroll
+                for (int i = 0; i < DPL; i++) Lp[i] = Ln[i];
+                minLp = mn;
+                reset_entering();
+                off += step_bytes;
+                x1 += dx;
+            }
+            return;
+        }
         const rsrc_t rcl = make_rsrc(a.cl + (size_t)pair * a.census_pair, (uint64_t)H * W * 8);
         const rsrc_t rcr = make_rsrc(a.cr + (size_t)pair * a.census_pair, (uint64_t)H * W * 8);
         // window entry e at step s = right census (y, X0 - minD - D + 1 + e), X0 = minX1 + b0 + dx*s;

@@ -53,7 +53,8 @@ def test_census_images_match_oracle(eng):
 
 
 @pytest.mark.parametrize("cost,mode,D,flags", [(1, 8, 32, 0), (0, 5, 32, 0), (0, 8, 32, 0), (1, 8, 64, 0),
-                                                (0, 5, 64, 0), (1, 5, 128, 0), (1, 8, 64, 48), (0, 5, 128, 48)])
+                                                (0, 5, 64, 0), (1, 5, 128, 0), (1, 8, 64, 48), (0, 5, 128, 48),
+                                                (1, 8, 128, 1024), (1, 8, 128, 2048), (1, 8, 48, 1024)])
 def test_path_volumes_match_oracle(eng, cost, mode, D, flags):
     left, right, _ = synthetic.random_dot_pair(33, 101 + D, D, seed=8)
     p = dict(synthetic.headline_params(D) if cost else synthetic.parity_params(D), mode=mode)
@@ -102,7 +103,8 @@ def test_random_shapes_vs_c_oracle(eng, c):
 
 
 @pytest.mark.parametrize("name,cost,mode,flags", [("kitti", 1, 8, 0), ("kitti", 0, 5, 0), ("kitti", 0, 8, 0),
-                                                  ("kitti", 1, 5, 0), ("mccnn", 1, 8, 0), ("kitti", 1, 8, 32)])
+                                                  ("kitti", 1, 5, 0), ("mccnn", 1, 8, 0), ("kitti", 1, 8, 32),
+                                                  ("kitti", 1, 8, 1024), ("kitti", 1, 8, 512)])
 def test_full_size_bit_exact(eng, name, cost, mode, flags):
     H, W, D = synthetic.CONFIGS[name]
     left, right, gt = synthetic.random_dot_pair(H, W, D, seed=42)
