@@ -172,22 +172,30 @@ __device__ __forceinline__ void horz_impl(const PathsArgs& a, int pair, int hb, 
             __builtin_amdgcn_wave_barrier();
         }
     } else {
+        // u16 cost volume; ring of PF loads in flight (the serial chain of one
+        // line is short of independent work, so the loads are issued PF steps ahead)
+        constexpr int PF = 4;
         const rsrc_t rc = make_rsrc(a.cost + (size_t)pair * a.cost_pair, (uint64_t)H * W1 * D * 2);
         const int coff0 = off0 / (int)sizeof(LT) * 2, cstep = step_bytes / (int)sizeof(LT) * 2;
-        RawU16<DPL> nxt;
-        nxt.load(rc, (uint32_t)coff0);
-        int off = off0, coff = coff0;
-        for (int s = 0; s < W1; s++) {
-            uint32_t C[DPL], Ln[DPL];
-            nxt.unpack(C);
-            coff += cstep;
-            nxt.load(rc, s + 1 < W1 ? (uint32_t)coff : kOOB);
-            const uint32_t mn = sgm_step<LANES, DPL>(Lp, minLp, C, P1, P2, Ln);
-            bstore_n<LT, DPL>(rout, line_ok ? (uint32_t)off : kOOB, Ln);
-            off += step_bytes;
+        RawU16<DPL> ring[PF];
 #pragma unroll
-            for (int i = 0; i < DPL; i++) Lp[i] = Ln[i];
-            minLp = mn;
+        for (int k = 0; k < PF; k++) ring[k].load(rc, k < W1 ? (uint32_t)(coff0 + k * cstep) : kOOB);
+        int off = off0, coff = coff0;
+        for (int s0 = 0; s0 < W1; s0 += PF) {
+#pragma unroll
+            for (int k = 0; k < PF; k++) {
+                const int s = s0 + k;
+                uint32_t C[DPL], Ln[DPL];
+                ring[k].unpack(C);
+                ring[k].load(rc, s + PF < W1 ? (uint32_t)(coff + PF * cstep) : kOOB);
+                coff += cstep;
+                const uint32_t mn = sgm_step<LANES, DPL>(Lp, minLp, C, P1, P2, Ln);
+                bstore_n<LT, DPL>(rout, (line_ok && s < W1) ? (uint32_t)off : kOOB, Ln);
+                off += step_bytes;
+#pragma unroll
+                for (int i = 0; i < DPL; i++) Lp[i] = Ln[i];
+                minLp = mn;
+            }
         }
     }
 }

@@ -24,6 +24,14 @@ __global__ void __launch_bounds__(256) k(uint32_t* out, uint32_t seed)
             else if constexpr (OP == 5) { uint32_t t; asm volatile("v_bcnt_u32_b32 %0, %1, %2" : "=v"(t) : "v"(v), "v"(a[(i+3)&7])); v = t; }
             else if constexpr (OP == 6) { uint32_t t; asm volatile("v_xor_b32 %0, %1, %2" : "=v"(t) : "v"(v), "v"(a[(i+3)&7])); v = t; }
             else if constexpr (OP == 7) { uint32_t t; asm volatile("v_add_u32 %0, %1, %2" : "=v"(t) : "v"(v), "v"(a[(i+3)&7])); v = t; }
+            else if constexpr (OP == 8) { uint32_t t; asm volatile("v_pk_add_u16 %0, %1, %2" : "=v"(t) : "v"(v), "v"(a[(i+3)&7])); v = t; }
+            else if constexpr (OP == 9) { uint32_t t; asm volatile("v_pk_min_u16 %0, %1, %2" : "=v"(t) : "v"(v), "v"(a[(i+3)&7])); v = t; }
+            else if constexpr (OP == 10) { uint32_t t; asm volatile("v_min_u32 %0, %1, %2" : "=v"(t) : "v"(v), "v"(a[(i+3)&7])); v = t; }
+            else if constexpr (OP == 11) { uint32_t t; asm volatile("v_alignbit_b32 %0, %1, %2, 16" : "=v"(t) : "v"(v), "v"(a[(i+3)&7])); v = t; }
+            else if constexpr (OP == 12) { uint32_t t; asm volatile("v_add3_u32 %0, %1, %2, %3" : "=v"(t) : "v"(v), "v"(a[(i+3)&7]), "v"(a[(i+5)&7])); v = t; }
+            else if constexpr (OP == 13) { uint32_t t; asm volatile("v_min_u16 %0, %1, %2" : "=v"(t) : "v"(v), "v"(a[(i+3)&7])); v = t; }
+            else if constexpr (OP == 14) { uint32_t t; asm volatile("v_pk_sub_u16 %0, %1, %2" : "=v"(t) : "v"(v), "v"(a[(i+3)&7])); v = t; }
+            else if constexpr (OP == 15) { uint32_t t; asm volatile("v_sub_u32 %0, %1, %2" : "=v"(t) : "v"(v), "v"(a[(i+3)&7])); v = t; }
             a[i] = v;
         }
     }
@@ -54,11 +62,15 @@ int main()
     const int blocks = 256 * 8;  // 8 WGs of 4 waves per CU -> 8 waves/SIMD
     uint32_t* d;
     (void)hipMalloc(&d, blocks * 256 * 4);
-    const char* names[] = {"v_add (compiler)", "ubfe+bcnt (compiler)", "v_perm", "v_min3 (asm)", "v_min_dpp fused", "v_bcnt (asm)", "v_xor (asm)", "v_add (asm)"};
-    float t[8] = {run<0>(d, blocks), run<1>(d, blocks), run<2>(d, blocks), run<3>(d, blocks),
-                  run<4>(d, blocks), run<5>(d, blocks), run<6>(d, blocks), run<7>(d, blocks)};
+    const char* names[] = {"v_add (compiler)", "ubfe+bcnt (compiler)", "v_perm", "v_min3 (asm)", "v_min_dpp fused",
+                           "v_bcnt (asm)", "v_xor (asm)", "v_add (asm)", "v_pk_add_u16", "v_pk_min_u16", "v_min_u32",
+                           "v_alignbit_b32", "v_add3_u32", "v_min_u16", "v_pk_sub_u16", "v_sub_u32"};
+    float t[16] = {run<0>(d, blocks),  run<1>(d, blocks),  run<2>(d, blocks),  run<3>(d, blocks),
+                   run<4>(d, blocks),  run<5>(d, blocks),  run<6>(d, blocks),  run<7>(d, blocks),
+                   run<8>(d, blocks),  run<9>(d, blocks),  run<10>(d, blocks), run<11>(d, blocks),
+                   run<12>(d, blocks), run<13>(d, blocks), run<14>(d, blocks), run<15>(d, blocks)};
     const double waves = blocks * 4.0, instr = (double)ITERS * 8;  // per wave (approx, 1 op per chain step)
-    for (int i = 0; i < 8; i++) {
+    for (int i = 0; i < 16; i++) {
         const double per_simd = waves * instr / 1024.0;  // wave-instrs per SIMD
         printf("%-24s %8.3f ms  %6.2f cycles/wave-instr/SIMD @2.4GHz\n", names[i], t[i], t[i] * 1e-3 * 2.4e9 / per_simd);
     }
