@@ -349,7 +349,7 @@ __global__ void __launch_bounds__(256) k_sgbm_cost_tail(uint16_t* C, int H, int 
 // sgm_np.quantize_volume).  (c + offset) * scale cannot be contracted into an
 // FMA, so the two IEEE roundings match the oracle's.
 constexpr int VOL_CMAX = 4095;
-constexpr int VT_X = 64;  // columns per tile
+
 
 struct VolArgs {
     const float* vol;
@@ -369,21 +369,46 @@ __device__ inline uint32_t quant_cost(float c, float off, float sc)
     return (uint32_t)v;
 }
 
+// TX columns per tile (64 or 128): each lane reads TX/64 consecutive floats
+// of a plane row (64 lanes cover the tile's TX columns, TX*4 contiguous bytes).
+template <int TX>
 __global__ void __launch_bounds__(256) k_cost_volume_f32(VolArgs a)
 {
-    extern __shared__ uint32_t tile[];  // [VT_X][D/2 + 1] packed u16 pairs (d even | d odd << 16)
+    constexpr int PL = TX / 64;         // floats per lane per plane row
+    extern __shared__ uint32_t tile[];  // [TX][D/2 + 1] packed u16 pairs (d even | d odd << 16)
     const int half = a.D >> 1, rowdw = half + 1;
-    const int x0 = blockIdx.x * VT_X, y = blockIdx.y, pair = blockIdx.z;
-    const int nx = min(VT_X, a.width1 - x0);
+    const int x0 = blockIdx.x * TX, y = blockIdx.y, pair = blockIdx.z;
+    const int nx = min(TX, a.width1 - x0);
     const size_t plane = (size_t)a.H * a.W;
     const float* v = a.vol + pair * a.vol_pair + (size_t)y * a.W + a.minX1 + x0;
-    for (int i = threadIdx.x; i < VT_X * half; i += 256) {
-        const int xl = i & (VT_X - 1), dp = i >> 6;
-        if (xl < nx) {
-            const float c0 = __builtin_nontemporal_load(v + (size_t)(2 * dp) * plane + xl);
-            const float c1 = __builtin_nontemporal_load(v + (size_t)(2 * dp + 1) * plane + xl);
-            tile[xl * rowdw + dp] = quant_cost(c0, a.offset, a.scale) | (quant_cost(c1, a.offset, a.scale) << 16);
+    for (int i = threadIdx.x; i < 64 * half; i += 256) {
+        const int xl = (i & 63) * PL, dp = i >> 6;
+        const float* p0 = v + (size_t)(2 * dp) * plane + xl;
+        const float* p1 = p0 + plane;
+        float c0[PL], c1[PL];
+        if (xl + PL <= nx) {
+            if constexpr (PL == 2) {
+                typedef float f2v __attribute__((ext_vector_type(2)));
+                const f2v a0 = __builtin_nontemporal_load(reinterpret_cast<const f2v*>(p0));
+                const f2v a1 = __builtin_nontemporal_load(reinterpret_cast<const f2v*>(p1));
+                c0[0] = a0[0]; c0[1] = a0[1]; c1[0] = a1[0]; c1[1] = a1[1];
+            } else {
+#pragma unroll
+                for (int k = 0; k < PL; k++) {
+                    c0[k] = __builtin_nontemporal_load(p0 + k);
+                    c1[k] = __builtin_nontemporal_load(p1 + k);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < PL; k++) {
+                c0[k] = xl + k < nx ? p0[k] : 0.f;
+                c1[k] = xl + k < nx ? p1[k] : 0.f;
+            }
         }
+#pragma unroll
+        for (int k = 0; k < PL; k++)
+            tile[(xl + k) * rowdw + dp] = quant_cost(c0[k], a.offset, a.scale) | (quant_cost(c1[k], a.offset, a.scale) << 16);
     }
     __syncthreads();
     uint32_t* out = reinterpret_cast<uint32_t*>(a.C + pair * a.C_pair + ((size_t)y * a.width1 + x0) * a.D);
