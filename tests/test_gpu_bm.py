@@ -98,3 +98,23 @@ def test_bm_torch_batch_and_errors(eng):
             eng.bm_compute(pairs[0][0], pairs[0][1], bm_params(dict(p, **bad)))
     with pytest.raises(_lib.SmError):
         eng.bm_compute(pairs[0][0], pairs[0][1], bm_params(dict(p, preFilterType=0)))
+
+
+from hypothesis import HealthCheck, given, settings, strategies as st  # noqa: E402
+
+
+@settings(max_examples=40, deadline=None, suppress_health_check=[HealthCheck.function_scoped_fixture])
+@given(H=st.integers(6, 50), W=st.integers(10, 160), Dk=st.integers(1, 4), minD=st.integers(-20, 20),
+       bs=st.sampled_from([5, 7, 9, 11, 15, 21]), cap=st.integers(1, 63), tex=st.integers(0, 300),
+       uniq=st.integers(0, 40), d12=st.integers(-1, 5), sws=st.sampled_from([0, 0, 10]), srange=st.integers(0, 32),
+       seed=st.integers(0, 2**31 - 1))
+def test_hypothesis_bm_vs_oracle(eng, H, W, Dk, minD, bs, cap, tex, uniq, d12, sws, srange, seed):
+    D = 16 * Dk
+    left, right, _ = synthetic.random_dot_pair(H, W, D, seed=seed)
+    p = dict(numDisparities=D, blockSize=bs, minDisparity=minD, preFilterCap=cap, textureThreshold=tex,
+             uniquenessRatio=uniq, disp12MaxDiff=d12, speckleWindowSize=sws, speckleRange=srange)
+    if bs >= min(H, W):
+        with pytest.raises(ValueError):
+            eng.bm_compute(left, right, bm_params(p))
+        return
+    assert np.array_equal(eng.bm_compute(left, right, bm_params(p)), bm_np.stereo_bm(left, right, p))

@@ -388,3 +388,32 @@ def test_single_process_multi_context_batch():
     finally:
         for e in engines:
             e.close()
+
+
+# ---------------------------------------------------------------- property-based sweep over the whole parameter space
+from hypothesis import HealthCheck, given, settings, strategies as st  # noqa: E402
+
+
+@settings(max_examples=60, deadline=None, suppress_health_check=[HealthCheck.function_scoped_fixture])
+@given(H=st.integers(1, 48), W=st.integers(8, 200), Dk=st.integers(1, 6), minD=st.integers(-20, 20),
+       cost=st.sampled_from([0, 1]), mode=st.sampled_from([5, 8]), bs=st.sampled_from([1, 3, 5, 7, 9, 11]),
+       P1=st.integers(0, 40), P2x=st.integers(0, 8), uniq=st.integers(-1, 30), d12=st.integers(-1, 6),
+       pfc=st.integers(0, 63), sws=st.sampled_from([0, 0, 0, 5, 40]), srange=st.integers(0, 4),
+       seed=st.integers(0, 2**31 - 1))
+def test_hypothesis_matcher_vs_c_oracle(eng, H, W, Dk, minD, cost, mode, bs, P1, P2x, uniq, d12, pfc, sws, srange,
+                                        seed):
+    D = 16 * Dk
+    left, right, _ = synthetic.random_dot_pair(H, W, D, seed=seed)
+    P2 = P1 * P2x  # 0 lets the normaliser pick max(5, P1+1)
+    if cost == 1:
+        P1, P2 = min(P1, 40), min(P2, 193)
+    p = dict(minDisparity=minD, numDisparities=D, blockSize=bs, P1=P1, P2=P2, disp12MaxDiff=d12,
+             uniquenessRatio=uniq, preFilterCap=pfc, speckleWindowSize=sws, speckleRange=srange, mode=mode,
+             cost=cost)
+    prm = sgm_np.normalize_params(p)
+    if cost == 0 and prm["bs"] ** 2 * (2 * prm["ftzero"] + 63) + prm["P2"] > 16383:
+        with pytest.raises(_lib.SmError):
+            run(eng, left, right, p)
+        return
+    out = run(eng, left, right, p)
+    assert np.array_equal(out, ref_c.compute(left, right, p))

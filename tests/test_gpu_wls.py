@@ -144,3 +144,23 @@ def test_wls_bad_args(eng):
         eng.wls_filter(d, g, None, wls_params(dict(), 10, 40))  # confidence needs dispr
     with pytest.raises(ValueError):
         eng.wls_filter(d, g, d, wls_params(dict(left_offset=-1), 10, 40))
+
+
+from hypothesis import HealthCheck, given, settings, strategies as st  # noqa: E402
+
+
+@settings(max_examples=25, deadline=None, suppress_health_check=[HealthCheck.function_scoped_fixture])
+@given(H=st.integers(2, 60), W=st.integers(20, 200), lo=st.integers(0, 40), ro=st.integers(0, 10),
+       to=st.integers(0, 5), bo=st.integers(0, 5), r=st.integers(0, 6), lam=st.floats(0.0, 1e5),
+       sigma=st.floats(0.3, 5.0), lrc=st.integers(0, 64), conf=st.booleans(), it=st.integers(1, 4),
+       seed=st.integers(0, 2**31 - 1))
+def test_hypothesis_wls_vs_oracle(eng, H, W, lo, ro, to, bo, r, lam, sigma, lrc, conf, it, seed):
+    rng = np.random.default_rng(seed)
+    displ = rng.integers(-16, 40 * 16, (H, W)).astype(np.int16)
+    dispr = (-rng.integers(0, 40 * 16, (H, W))).astype(np.int16)
+    guide = rng.integers(0, 256, (H, W)).astype(np.uint8)
+    p = dict(lmbda=float(np.float32(lam)), sigma=float(np.float32(sigma)), lrc_thresh=lrc, radius=r,
+             use_confidence=conf, left_offset=lo, right_offset=ro, top_offset=to, bottom_offset=bo, num_iter=it,
+             min_disp=int(rng.integers(-3, 3)))
+    out = eng.wls_filter(displ, guide, dispr if conf else None, wls_params(p, H, W))
+    assert np.array_equal(out, wls_np.wls_filter(displ, guide, dispr if conf else None, p))
