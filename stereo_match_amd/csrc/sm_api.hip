@@ -572,9 +572,15 @@ int run_group(sm_ctx* ctx, const Src& src, const Geo& g, const Norm& n, int16_t*
             sc.SW2 = n.bs / 2;
             sc.SH2 = n.bs / 2;
             sc.Yc = std::max(1, H - n.bs / 2);
-            hipLaunchKernelGGL(smk::k_sgbm_cost,
-                               dim3((n.width1 + smk::SC_TX - 1) / smk::SC_TX, (sc.Yc + smk::SC_TY - 1) / smk::SC_TY, G),
-                               dim3(256), 0, ctx->stream, sc);
+            // 64-column tiles up to blockSize 7; 32-column tiles keep blockSize 9..11 within 64 KB of LDS
+            if (n.bs <= 7)
+                hipLaunchKernelGGL((smk::k_sgbm_cost<64, 3>),
+                                   dim3((n.width1 + 63) / 64, (sc.Yc + smk::SC_TY - 1) / smk::SC_TY, G), dim3(256), 0,
+                                   ctx->stream, sc);
+            else
+                hipLaunchKernelGGL((smk::k_sgbm_cost<32, 5>),
+                                   dim3((n.width1 + 31) / 32, (sc.Yc + smk::SC_TY - 1) / smk::SC_TY, G), dim3(256), 0,
+                                   ctx->stream, sc);
             HIP_TRY(ctx, hipGetLastError());
             if (sc.Yc < H) {
                 const size_t row = (size_t)n.width1 * n.D;

@@ -220,7 +220,7 @@ __global__ void __launch_bounds__(256) k_sgbm_prefilter(PrefilterArgs a)
 //   sum_{k=y-SH2..y+SH2} sum_{j=-SW2..SW2} pix(clamp(k,0,H-1), clamp(x1+j,0,width1-1), d)
 // Tile of SC_TY rows x SC_TX columns x 8 disparities per workgroup: BT pixel
 // costs of the halo tile -> LDS, horizontal then vertical sums in LDS.
-constexpr int SC_TX = 64, SC_TY = 8, SC_MAXR = 5, SC_DC = 8;  // blockSize <= 11; disparities per chunk
+constexpr int SC_TY = 8, SC_DC = 8;  // output rows per tile; disparities per chunk
 
 struct SgbmCostArgs {
     const uint2* planes;  // packed, [pair][view][H][W]
@@ -229,93 +229,151 @@ struct SgbmCostArgs {
     int H, W, width1, D, minD, minX1, SW2, SH2, Yc;
 };
 
-__device__ __forceinline__ int bt_cost2(uint2 L, uint2 R)
-{
-    // bytes: [g, g_min, g_max, raw, raw_min, raw_max, -, -] of left (u) / right (v)
-    int acc = 0;
-#pragma unroll
-    for (int ch = 0; ch < 2; ch++) {
-        const uint32_t lw = ch == 0 ? L.x : (L.x >> 24) | (L.y << 8);
-        const uint32_t rw = ch == 0 ? R.x : (R.x >> 24) | (R.y << 8);
-        const int u = lw & 0xFF, u0 = (lw >> 8) & 0xFF, u1 = (lw >> 16) & 0xFF;
-        const int v = rw & 0xFF, v0 = (rw >> 8) & 0xFF, v1 = (rw >> 16) & 0xFF;
-        const int c0 = max(max(0, u - v1), v0 - u);
-        const int c1 = max(max(0, v - u1), u0 - v);
-        acc += min(c0, c1) >> (ch == 0 ? 0 : 2);
-    }
-    return acc;
-}
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u16x2 as_u16x2(uint32_t w) { return __builtin_bit_cast(u16x2, w); }
+__device__ __forceinline__ uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+__device__ __forceinline__ u16x2 subsat(u16x2 a, u16x2 b) { return __builtin_elementwise_sub_sat(a, b); }
 
-// One workgroup per SC_TY x SC_TX output tile and ALL disparities (chunks of
-// SC_DC): the left halo tile is staged once, the right planes once per chunk;
-// BT pixel costs -> LDS bytes, then horizontal and vertical box sums with
-// two disparities per 32-bit lane (SWAR; sums < 2^16 by the int16-exact
-// domain check, and the int16 wrap is the low 16 bits).
+// (r, c) walk over a rows x cols item grid with a 256-thread stride, no division per item
+struct Walk {
+    int r, c, rs, cs, cols;
+    __device__ Walk(int tid, int cols_) : cols(cols_)
+    {
+        r = tid / cols;
+        c = tid - r * cols;
+        rs = 256 / cols;
+        cs = 256 - rs * cols;
+    }
+    __device__ void next()
+    {
+        r += rs;
+        c += cs;
+        if (c >= cols) {
+            c -= cols;
+            r++;
+        }
+    }
+};
+
+// One workgroup per SC_TY x TX output tile and ALL disparities (chunks of
+// SC_DC).  The BT costs run two disparities per 32-bit lane: the right
+// view's six byte quantities (g, g_min, g_max, raw, raw_min, raw_max) are
+// staged per chunk as u16 pairs of adjacent columns, so one LDS word feeds
+// the (d, d+1) pair and the BT min/max/saturating-subtract work is packed
+// 16-bit math.  Box sums: horizontal then vertical, SWAR u16 lanes (sums
+// < 2^16 by the int16-exact domain check; the int16 wrap is the low 16 bits).
+template <int TX, int MAXR>
 __global__ void __launch_bounds__(256) k_sgbm_cost(SgbmCostArgs a)
 {
-    constexpr int HR = SC_TY + 2 * SC_MAXR, HC = SC_TX + 2 * SC_MAXR;
+    constexpr int HR = SC_TY + 2 * MAXR, HC = TX + 2 * MAXR, RC = HC + SC_DC;
     __shared__ __attribute__((aligned(16))) uint2 lpl[HR][HC];
-    __shared__ __attribute__((aligned(16))) uint2 rpl[HR][HC + SC_DC];
-    __shared__ __attribute__((aligned(16))) uint2 pix[HR][HC];           // SC_DC byte costs
-    __shared__ __attribute__((aligned(16))) uint4 hs[HR][SC_TX];         // SC_DC u16 sums
-    const int x0 = blockIdx.x * SC_TX, y0 = blockIdx.y * SC_TY, pair = blockIdx.z;
+    // the pair planes and the horizontal sums are never live together: one buffer
+    constexpr int QW = 6 * HR * RC, HW = 4 * HR * TX;
+    __shared__ __attribute__((aligned(16))) uint32_t qh[QW > HW ? QW : HW];
+    __shared__ __attribute__((aligned(16))) uint2 pix[HR][HC];  // SC_DC byte costs
+    auto Q = reinterpret_cast<uint32_t(*)[HR][RC]>(qh);
+    auto hs = reinterpret_cast<uint4(*)[TX]>(qh);
+    constexpr int NQ = (HR * (HC + SC_DC - 1) + 255) / 256;  // pair items per thread (max)
+    const int x0 = blockIdx.x * TX, y0 = blockIdx.y * SC_TY, pair = blockIdx.z;
     const int SW2 = a.SW2, SH2 = a.SH2, W1 = a.width1, W = a.W, D = a.D;
-    const int rows_h = SC_TY + 2 * SH2, cols_h = SC_TX + 2 * SW2;
+    const int rows_h = SC_TY + 2 * SH2, cols_h = TX + 2 * SW2;
     const uint2* Lp = a.planes + (size_t)(pair * 2) * a.H * W;
     const uint2* Rp = Lp + (size_t)a.H * W;
-    const int xlo = max(x0 - SW2, 0), xhi = min(x0 + SC_TX + SW2 - 1, W1 - 1);  // clamped x1 range
-    const int rcols = xhi - xlo + SC_DC;
+    const int xlo = max(x0 - SW2, 0), xhi = min(x0 + TX + SW2 - 1, W1 - 1);  // clamped x1 range
+    const int rpairs = xhi - xlo + SC_DC - 1;  // column pairs (k, k+1) needed per chunk
     uint16_t* Cb = a.C + pair * a.C_pair;
-    for (int i = threadIdx.x; i < rows_h * cols_h; i += 256) {
-        const int r = i / cols_h, c = i - r * cols_h;
-        const int y = min(max(y0 - SH2 + r, 0), a.H - 1);
-        lpl[r][c] = Lp[(size_t)y * W + min(max(x0 - SW2 + c, 0), W1 - 1) + a.minX1];
+    const int tid = threadIdx.x;
+    for (Walk w(tid, cols_h); w.r < rows_h; w.next()) {
+        const int y = min(max(y0 - SH2 + w.r, 0), a.H - 1);
+        lpl[w.r][w.c] = Lp[(size_t)y * W + min(max(x0 - SW2 + w.c, 0), W1 - 1) + a.minX1];
     }
-    for (int d0 = 0; d0 < D; d0 += SC_DC) {
-        const int rbase = xlo + a.minX1 - a.minD - d0 - (SC_DC - 1);  // right column of rpl[.][0]
-        __syncthreads();  // previous chunk done with rpl / hs
-        for (int i = threadIdx.x; i < rows_h * rcols; i += 256) {
-            const int r = i / rcols, c = i - r * rcols;
-            const int y = min(max(y0 - SH2 + r, 0), a.H - 1);
-            rpl[r][c] = Rp[(size_t)y * W + rbase + c];
-        }
-        __syncthreads();
-        for (int i = threadIdx.x; i < rows_h * cols_h; i += 256) {
-            const int r = i / cols_h, c = i - r * cols_h;
-            const int x1 = min(max(x0 - SW2 + c, 0), W1 - 1);
-            const int ri = x1 - xlo + SC_DC - 1;  // right column index for disparity d0
-            const uint2 L = lpl[r][c];
-            uint32_t b[SC_DC];
+    // right-view columns of the next chunk are loaded into registers while
+    // the current chunk computes (L2 latency off the barrier-separated phases)
+    uint2 pc0[NQ], pc1[NQ];
+    auto load_right = [&](int d0) {
+        const int rbase = xlo + a.minX1 - a.minD - d0 - (SC_DC - 1);  // right column of pair index 0
+        Walk w(tid, rpairs);
 #pragma unroll
-            for (int j = 0; j < SC_DC; j++) b[j] = (uint32_t)bt_cost2(L, rpl[r][ri - j]);
-            pix[r][c] = make_uint2(b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24),
-                                   b[4] | (b[5] << 8) | (b[6] << 16) | (b[7] << 24));
+        for (int i = 0; i < NQ; i++, w.next()) {
+            if (w.r < rows_h && d0 < D) {
+                const uint2* row = Rp + (size_t)min(max(y0 - SH2 + w.r, 0), a.H - 1) * W + rbase;
+                pc0[i] = row[w.c];
+                pc1[i] = row[w.c + 1];
+            }
+        }
+    };
+    load_right(0);
+    for (int d0 = 0; d0 < D; d0 += SC_DC) {
+        __syncthreads();  // previous chunk done with Q / hs
+        {
+            Walk w(tid, rpairs);
+#pragma unroll
+            for (int i = 0; i < NQ; i++, w.next()) {
+                if (w.r < rows_h) {
+                    const uint2 c0 = pc0[i], c1 = pc1[i];
+                    // u16 pair (col k, col k+1) of each byte quantity
+                    Q[0][w.r][w.c] = __builtin_amdgcn_perm(c1.x, c0.x, 0x0c040c00u);
+                    Q[1][w.r][w.c] = __builtin_amdgcn_perm(c1.x, c0.x, 0x0c050c01u);
+                    Q[2][w.r][w.c] = __builtin_amdgcn_perm(c1.x, c0.x, 0x0c060c02u);
+                    Q[3][w.r][w.c] = __builtin_amdgcn_perm(c1.x, c0.x, 0x0c070c03u);
+                    Q[4][w.r][w.c] = __builtin_amdgcn_perm(c1.y, c0.y, 0x0c040c00u);
+                    Q[5][w.r][w.c] = __builtin_amdgcn_perm(c1.y, c0.y, 0x0c050c01u);
+                }
+            }
+        }
+        load_right(d0 + SC_DC);
+        __syncthreads();
+        for (Walk w(tid, cols_h); w.r < rows_h; w.next()) {
+            const int x1 = min(max(x0 - SW2 + w.c, 0), W1 - 1);
+            const int ri = x1 - xlo + SC_DC - 1;  // right column index (pair grid) of disparity d0
+            const uint2 L = lpl[w.r][w.c];
+            // left quantities broadcast to both lanes
+            const u16x2 U0 = as_u16x2(__builtin_amdgcn_perm(0, L.x, 0x0c000c00u));
+            const u16x2 U1 = as_u16x2(__builtin_amdgcn_perm(0, L.x, 0x0c010c01u));
+            const u16x2 U2 = as_u16x2(__builtin_amdgcn_perm(0, L.x, 0x0c020c02u));
+            const u16x2 U3 = as_u16x2(__builtin_amdgcn_perm(0, L.x, 0x0c030c03u));
+            const u16x2 U4 = as_u16x2(__builtin_amdgcn_perm(0, L.y, 0x0c000c00u));
+            const u16x2 U5 = as_u16x2(__builtin_amdgcn_perm(0, L.y, 0x0c010c01u));
+            uint32_t P[SC_DC / 2];
+#pragma unroll
+            for (int j = 0; j < SC_DC; j += 2) {
+                const int k = ri - j - 1;  // lanes: (d0+j+1, d0+j)
+                const u16x2 V0 = as_u16x2(Q[0][w.r][k]), V1 = as_u16x2(Q[1][w.r][k]), V2 = as_u16x2(Q[2][w.r][k]);
+                const u16x2 V3 = as_u16x2(Q[3][w.r][k]), V4 = as_u16x2(Q[4][w.r][k]), V5 = as_u16x2(Q[5][w.r][k]);
+                // c0 = max(0, u - v1, v0 - u); c1 = max(0, v - u1, u0 - v); per channel min(c0, c1)
+                const u16x2 g = __builtin_elementwise_min(__builtin_elementwise_max(subsat(U0, V2), subsat(V1, U0)),
+                                                          __builtin_elementwise_max(subsat(V0, U2), subsat(U1, V0)));
+                const u16x2 r = __builtin_elementwise_min(__builtin_elementwise_max(subsat(U3, V5), subsat(V4, U3)),
+                                                          __builtin_elementwise_max(subsat(V3, U5), subsat(U4, V3)));
+                P[j / 2] = as_u32(g + (r >> (u16x2)2));
+            }
+            // bytes in disparity order: P[j/2] holds (cost d0+j+1 | cost d0+j << 16)
+            pix[w.r][w.c] = make_uint2(__builtin_amdgcn_perm(P[1], P[0], 0x04060002u),
+                                       __builtin_amdgcn_perm(P[3], P[2], 0x04060002u));
         }
         __syncthreads();
-        for (int i = threadIdx.x; i < rows_h * SC_TX; i += 256) {
-            const int r = i / SC_TX, c = i - r * SC_TX;
+        for (Walk w(tid, TX); w.r < rows_h; w.next()) {
             uint32_t e0 = 0, o0 = 0, e1 = 0, o1 = 0;  // u16 lanes: (d0,d2) (d1,d3) (d4,d6) (d5,d7)
             for (int j = 0; j <= 2 * SW2; j++) {
-                const uint2 w = pix[r][c + j];
-                e0 += w.x & 0x00FF00FFu;
-                o0 += (w.x >> 8) & 0x00FF00FFu;
-                e1 += w.y & 0x00FF00FFu;
-                o1 += (w.y >> 8) & 0x00FF00FFu;
+                const uint2 v = pix[w.r][w.c + j];
+                e0 += v.x & 0x00FF00FFu;
+                o0 += (v.x >> 8) & 0x00FF00FFu;
+                e1 += v.y & 0x00FF00FFu;
+                o1 += (v.y >> 8) & 0x00FF00FFu;
             }
-            hs[r][c] = make_uint4(e0, o0, e1, o1);
+            hs[w.r][w.c] = make_uint4(e0, o0, e1, o1);
         }
         __syncthreads();
-        for (int i = threadIdx.x; i < SC_TY * SC_TX; i += 256) {
-            const int r = i / SC_TX, c = i - r * SC_TX;
-            const int y = y0 + r, x1 = x0 + c;
+        for (Walk w(tid, TX); w.r < SC_TY; w.next()) {
+            const int y = y0 + w.r, x1 = x0 + w.c;
             if (y >= a.Yc || x1 >= W1) continue;
             uint32_t e0 = 0, o0 = 0, e1 = 0, o1 = 0;
             for (int k = 0; k <= 2 * SH2; k++) {
-                const uint4 w = hs[r + k][c];
-                e0 += w.x;
-                o0 += w.y;
-                e1 += w.z;
-                o1 += w.w;
+                const uint4 v = hs[w.r + k][w.c];
+                e0 += v.x;
+                o0 += v.y;
+                e1 += v.z;
+                o1 += v.w;
             }
             // interleave back to d order: (d0,d1) (d2,d3) (d4,d5) (d6,d7)
             uint4 o;
