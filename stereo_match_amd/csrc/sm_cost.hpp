@@ -270,8 +270,9 @@ __global__ void __launch_bounds__(256) k_sgbm_cost(SgbmCostArgs a)
     // the pair planes and the horizontal sums are never live together: one buffer
     constexpr int QW = 6 * HR * RC, HW = 4 * HR * TX;
     __shared__ __attribute__((aligned(16))) uint32_t qh[QW > HW ? QW : HW];
-    __shared__ __attribute__((aligned(16))) uint2 pix[HR][HC];  // SC_DC byte costs
-    auto Q = reinterpret_cast<uint32_t(*)[HR][RC]>(qh);
+    __shared__ __attribute__((aligned(16))) uint4 pix[HR][HC];  // SC_DC costs as u16 pairs
+    auto Qa = reinterpret_cast<uint4(*)[RC]>(qh);                // g, g_min, g_max, raw
+    auto Qb = reinterpret_cast<uint2(*)[RC]>(qh + 4 * HR * RC);  // raw_min, raw_max
     auto hs = reinterpret_cast<uint4(*)[TX]>(qh);
     constexpr int NQ = (HR * (HC + SC_DC - 1) + 255) / 256;  // pair items per thread (max)
     const int x0 = blockIdx.x * TX, y0 = blockIdx.y * SC_TY, pair = blockIdx.z;
@@ -311,13 +312,13 @@ __global__ void __launch_bounds__(256) k_sgbm_cost(SgbmCostArgs a)
             for (int i = 0; i < NQ; i++, w.next()) {
                 if (w.r < rows_h) {
                     const uint2 c0 = pc0[i], c1 = pc1[i];
-                    // u16 pair (col k, col k+1) of each byte quantity
-                    Q[0][w.r][w.c] = __builtin_amdgcn_perm(c1.x, c0.x, 0x0c040c00u);
-                    Q[1][w.r][w.c] = __builtin_amdgcn_perm(c1.x, c0.x, 0x0c050c01u);
-                    Q[2][w.r][w.c] = __builtin_amdgcn_perm(c1.x, c0.x, 0x0c060c02u);
-                    Q[3][w.r][w.c] = __builtin_amdgcn_perm(c1.x, c0.x, 0x0c070c03u);
-                    Q[4][w.r][w.c] = __builtin_amdgcn_perm(c1.y, c0.y, 0x0c040c00u);
-                    Q[5][w.r][w.c] = __builtin_amdgcn_perm(c1.y, c0.y, 0x0c050c01u);
+                    // u16 pair (col k+1 | col k << 16) of each byte quantity
+                    Qa[w.r][w.c] = make_uint4(__builtin_amdgcn_perm(c1.x, c0.x, 0x0c000c04u),
+                                              __builtin_amdgcn_perm(c1.x, c0.x, 0x0c010c05u),
+                                              __builtin_amdgcn_perm(c1.x, c0.x, 0x0c020c06u),
+                                              __builtin_amdgcn_perm(c1.x, c0.x, 0x0c030c07u));
+                    Qb[w.r][w.c] = make_uint2(__builtin_amdgcn_perm(c1.y, c0.y, 0x0c000c04u),
+                                              __builtin_amdgcn_perm(c1.y, c0.y, 0x0c010c05u));
                 }
             }
         }
@@ -337,9 +338,11 @@ __global__ void __launch_bounds__(256) k_sgbm_cost(SgbmCostArgs a)
             uint32_t P[SC_DC / 2];
 #pragma unroll
             for (int j = 0; j < SC_DC; j += 2) {
-                const int k = ri - j - 1;  // lanes: (d0+j+1, d0+j)
-                const u16x2 V0 = as_u16x2(Q[0][w.r][k]), V1 = as_u16x2(Q[1][w.r][k]), V2 = as_u16x2(Q[2][w.r][k]);
-                const u16x2 V3 = as_u16x2(Q[3][w.r][k]), V4 = as_u16x2(Q[4][w.r][k]), V5 = as_u16x2(Q[5][w.r][k]);
+                const int k = ri - j - 1;  // lanes: (d0+j, d0+j+1)
+                const uint4 qa = Qa[w.r][k];
+                const uint2 qb = Qb[w.r][k];
+                const u16x2 V0 = as_u16x2(qa.x), V1 = as_u16x2(qa.y), V2 = as_u16x2(qa.z);
+                const u16x2 V3 = as_u16x2(qa.w), V4 = as_u16x2(qb.x), V5 = as_u16x2(qb.y);
                 // c0 = max(0, u - v1, v0 - u); c1 = max(0, v - u1, u0 - v); per channel min(c0, c1)
                 const u16x2 g = __builtin_elementwise_min(__builtin_elementwise_max(subsat(U0, V2), subsat(V1, U0)),
                                                           __builtin_elementwise_max(subsat(V0, U2), subsat(U1, V0)));
@@ -347,40 +350,32 @@ __global__ void __launch_bounds__(256) k_sgbm_cost(SgbmCostArgs a)
                                                           __builtin_elementwise_max(subsat(V3, U5), subsat(U4, V3)));
                 P[j / 2] = as_u32(g + (r >> (u16x2)2));
             }
-            // bytes in disparity order: P[j/2] holds (cost d0+j+1 | cost d0+j << 16)
-            pix[w.r][w.c] = make_uint2(__builtin_amdgcn_perm(P[1], P[0], 0x04060002u),
-                                       __builtin_amdgcn_perm(P[3], P[2], 0x04060002u));
+            pix[w.r][w.c] = make_uint4(P[0], P[1], P[2], P[3]);  // (d0 | d1 << 16), (d2 | d3 << 16), ...
         }
         __syncthreads();
         for (Walk w(tid, TX); w.r < rows_h; w.next()) {
-            uint32_t e0 = 0, o0 = 0, e1 = 0, o1 = 0;  // u16 lanes: (d0,d2) (d1,d3) (d4,d6) (d5,d7)
-            for (int j = 0; j <= 2 * SW2; j++) {
-                const uint2 v = pix[w.r][w.c + j];
-                e0 += v.x & 0x00FF00FFu;
-                o0 += (v.x >> 8) & 0x00FF00FFu;
-                e1 += v.y & 0x00FF00FFu;
-                o1 += (v.y >> 8) & 0x00FF00FFu;
+            uint4 h = pix[w.r][w.c];
+            for (int j = 1; j <= 2 * SW2; j++) {
+                const uint4 v = pix[w.r][w.c + j];
+                h.x += v.x;
+                h.y += v.y;
+                h.z += v.z;
+                h.w += v.w;
             }
-            hs[w.r][w.c] = make_uint4(e0, o0, e1, o1);
+            hs[w.r][w.c] = h;
         }
         __syncthreads();
         for (Walk w(tid, TX); w.r < SC_TY; w.next()) {
             const int y = y0 + w.r, x1 = x0 + w.c;
             if (y >= a.Yc || x1 >= W1) continue;
-            uint32_t e0 = 0, o0 = 0, e1 = 0, o1 = 0;
-            for (int k = 0; k <= 2 * SH2; k++) {
+            uint4 o = hs[w.r][w.c];
+            for (int k = 1; k <= 2 * SH2; k++) {
                 const uint4 v = hs[w.r + k][w.c];
-                e0 += v.x;
-                o0 += v.y;
-                e1 += v.z;
-                o1 += v.w;
+                o.x += v.x;
+                o.y += v.y;
+                o.z += v.z;
+                o.w += v.w;
             }
-            // interleave back to d order: (d0,d1) (d2,d3) (d4,d5) (d6,d7)
-            uint4 o;
-            o.x = (e0 & 0xFFFF) | (o0 << 16);
-            o.y = (e0 >> 16) | (o0 & 0xFFFF0000u);
-            o.z = (e1 & 0xFFFF) | (o1 << 16);
-            o.w = (e1 >> 16) | (o1 & 0xFFFF0000u);
             *reinterpret_cast<uint4*>(Cb + ((size_t)y * W1 + x1) * D + d0) = o;
         }
     }
