@@ -213,7 +213,9 @@ int sm_compute_batch(sm_ctx** ctxs, int ngpu, const uint8_t* const* left, const 
  * (reference call: stereo_vision/stereo_vision.py:171). */
 int sm_right_matcher_params(const sm_params* left, sm_params* right_out);
 
-/* Wait for all work enqueued on the context stream. */
+/* Wait for all work enqueued on the context stream; reports (and clears) a
+ * device-side failure of the fused-sweep engine (a strip-boundary hand-off
+ * that timed out) as SM_E_HIP.  Synchronous entry points check it themselves. */
 int sm_synchronize(sm_ctx* ctx);
 
 /* Per-stage device timing with hipEvents on the context stream.
@@ -227,7 +229,12 @@ int sm_synchronize(sm_ctx* ctx);
 #define SM_STAGE_TOTAL 4
 #define SM_STAGE_WLS 5
 #define SM_STAGE_SPECKLE 6
-#define SM_NUM_STAGES 7
+/* fused-sweep engine kernels (inside stages 1 and 2): E/W volumes, the
+ * first (down) sweep writing the partial sums, the sweep fused with the WTA */
+#define SM_STAGE_HORIZONTAL 7
+#define SM_STAGE_SWEEP 8
+#define SM_STAGE_SWEEP_WTA 9
+#define SM_NUM_STAGES 10
 int sm_set_timing(sm_ctx* ctx, int enable);
 int sm_get_timing(sm_ctx* ctx, int stage, double* total_ms, long long* launches, long long* pairs);
 int sm_reset_timing(sm_ctx* ctx);
@@ -254,7 +261,10 @@ long long sm_debug_fetch(sm_ctx* ctx, int what, void* host, size_t bytes);
  * per wave) instead of 16-lane lines (4 rows per wave); bit 10 (valid
  * results, census) computes Hamming costs on the fly in every direction
  * instead of reading the precomputed u8 cost volume, bit 11 only in the
- * horizontal family; bits 16-19: launch-group size cap (0 = none).
+ * horizontal family; bit 12 (valid results) uses the per-direction engine
+ * (one path volume per direction + WTA kernel) instead of the fused sweeps,
+ * so that sm_debug_fetch(1) has every direction; bits 16-19: launch-group
+ * size cap (0 = none).
  * 0 = normal operation. */
 int sm_set_debug_flags(sm_ctx* ctx, int flags);
 

@@ -14,13 +14,14 @@ import threading
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libstereo_match_amd.so")
+# STEREO_MATCH_AMD_LIB: alternative build of the same library (kernel experiments only)
+LIB_PATH = os.environ.get("STEREO_MATCH_AMD_LIB") or os.path.join(_HERE, "libstereo_match_amd.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "stereo_match_amd.h")
 
 SM_OK, SM_E_ARG, SM_E_HIP, SM_E_UNSUPPORTED = 0, -1, -2, -4
 SM_COST_SGBM, SM_COST_CENSUS, SM_COST_VOLUME = 0, 1, 2
 SM_MODE_SGBM, SM_MODE_HH = 5, 8
-STAGES = ("cost", "paths", "wta", "median", "total", "wls", "speckle")
+STAGES = ("cost", "paths", "wta", "median", "total", "wls", "speckle", "horizontal", "sweep", "sweep_wta")
 
 
 class SmParams(ctypes.Structure):

@@ -34,6 +34,7 @@
 #include "sm_speckle.hpp"
 #include "sm_reproject.hpp"
 #include "sm_bm.hpp"
+#include "sm_sweep_host.hpp"
 
 #define SM_VERSION "stereo_match_amd 0.2.0 (gfx950)"
 
@@ -59,12 +60,15 @@ struct TimedEvent {
 // per-group device buffers (double-buffered across launch groups)
 struct BufSet {
     DevBuf census[2], cost, L, raw;
+    DevBuf part, key2, pre;  // sweep engine: u16 partial sums, disp2 keys, WTA output before the LR check
     hipEvent_t paths_done = nullptr, wta_done = nullptr;
     bool pending = false;  // wta_done recorded and not yet waited for by stream A
 };
 
 // debug flags (sm_set_debug_flags); 1 skip horizontal, 2 skip vertical and 4 drop stores are read in-kernel
 constexpr int DBG_VL16 = 8, DBG_STORE_W = 16, DBG_ROW = 32, DBG_OVERLAP = 64, DBG_H64 = 512, DBG_NO_C8 = 1024;
+// 4096: per-direction engine (one path volume per direction + k_wta) instead of the fused sweeps
+constexpr int DBG_LEGACY = 4096, DBG_SWEEP1 = 8192, DBG_SWEEP8 = 16384;
 
 }  // namespace
 
@@ -75,6 +79,9 @@ struct sm_ctx {
     hipStream_t side = nullptr;    // stream B
     DevBuf img[2], planes, out, dbg, volbuf, sp_parent, sp_count, rp_in, rp_out, rp_min, bm_pre[2], bm_cost;
     DevBuf wls_num, wls_den, wls_inter, wls_w, wls_disp[2], wls_out;  // WLS scratch
+    DevBuf hop, sweep_err;  // sweep engine: strip-boundary granules, device error word
+    uint32_t hop_epoch = 0;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;  // sweep engine: E/W kernel on the side stream
     BufSet set[2];
     int next_set = 0;
     // geometry of the last computation (for sm_debug_fetch): its last pair
@@ -261,6 +268,7 @@ struct Src {  // where a launch group's pairs come from (device pointers)
 struct Geo {  // per-group geometry shared by the launches
     int H, W, stride, G;
     size_t vol, slot_bytes, L_pair, census_pair, cost_pair;
+    bool sweep;  // fused-sweep engine (sm_sweep.hpp) instead of per-direction volumes
 };
 
 bool row_mode(const sm_ctx* ctx, const Norm& n) { return (ctx->dbg_flags & DBG_ROW) && n.D % 64 == 0; }
@@ -276,7 +284,7 @@ hipStream_t stream_b(const sm_ctx* ctx) { return overlap(ctx) ? ctx->side : ctx-
 
 // ---- stream A: path aggregation -------------------------------------------
 template <int DPLV, bool CENSUS, int VL, bool H16 = false>
-int launch_paths_t(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs)
+int launch_paths_t(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs, bool horiz_only)
 {
     using LT = typename std::conditional<CENSUS, uint8_t, uint16_t>::type;
     constexpr int D = 16 * DPLV;
@@ -308,7 +316,7 @@ int launch_paths_t(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs)
     pa.dbg = ctx->dbg_flags;
     const int lines_per_wg = 4 * (64 / LANESH);
     pa.hblocks = row_mode(ctx, n) ? 0 : (g.H + lines_per_wg - 1) / lines_per_wg;
-    pa.nv = n.ndirs - 2;
+    pa.nv = horiz_only ? 0 : n.ndirs - 2;  // sweep engine: E and W only
     int blocks = 0;
     constexpr int LPWV = 64 / VL;
     for (int k = 0; k < pa.nv; k++) {
@@ -322,7 +330,7 @@ int launch_paths_t(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs)
         blocks += ((pa.v_nlines[k] + 8 * LPWV - 1) / (8 * LPWV)) * 2;
     }
     for (int k = pa.nv; k <= 6; k++) pa.v_blk_start[k] = blocks;
-    StageTimer t(ctx, ctx->stream, SM_STAGE_PATHS, g.G);
+    StageTimer t(ctx, ctx->stream, horiz_only ? SM_STAGE_HORIZONTAL : SM_STAGE_PATHS, g.G);
     hipLaunchKernelGGL((smk::k_sgm_paths<VL, DPLV * 16 / VL, LANESH, DPLH, CENSUS, LT>),
                        dim3(2 * pa.hblocks + blocks, g.G), dim3(256), 0, ctx->stream, pa);
     HIP_TRY(ctx, hipGetLastError());
@@ -388,31 +396,36 @@ int launch_wta_t(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs)
 }
 
 template <int DPLV, bool CENSUS>
-int launch_paths_dpl(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs)
+int launch_paths_dpl(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs, bool horiz_only)
 {
     // horizontal lines: 16 lanes (4 rows per wave); 64-lane lines (one row per
     // wave, the round-1 layout for D % 64 == 0) with the ablation flag
     if constexpr ((16 * DPLV) % 64 == 0) {
         if (ctx->dbg_flags & DBG_H64) {
-            if (DPLV == 8 && !(ctx->dbg_flags & DBG_VL16)) return launch_paths_t<DPLV, CENSUS, 8>(ctx, n, g, bs);
-            return launch_paths_t<DPLV, CENSUS, 16>(ctx, n, g, bs);
+            if (DPLV == 8 && !(ctx->dbg_flags & DBG_VL16))
+                return launch_paths_t<DPLV, CENSUS, 8>(ctx, n, g, bs, horiz_only);
+            return launch_paths_t<DPLV, CENSUS, 16>(ctx, n, g, bs, horiz_only);
         }
     }
     // 8-lane vertical lines at D = 128 (16-lane with the ablation flag)
     if constexpr (DPLV == 8) {
-        if (!(ctx->dbg_flags & DBG_VL16)) return launch_paths_t<DPLV, CENSUS, 8, true>(ctx, n, g, bs);
+        if (!(ctx->dbg_flags & DBG_VL16)) return launch_paths_t<DPLV, CENSUS, 8, true>(ctx, n, g, bs, horiz_only);
     }
-    return launch_paths_t<DPLV, CENSUS, 16, true>(ctx, n, g, bs);
+    return launch_paths_t<DPLV, CENSUS, 16, true>(ctx, n, g, bs, horiz_only);
 }
 
-int dispatch(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs, bool wta)
+enum { DISPATCH_PATHS = 0, DISPATCH_WTA = 1, DISPATCH_HORIZONTAL = 2 };
+
+int dispatch(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs, int what)
 {
     const bool census = n.cost == SM_COST_CENSUS;
+    const bool h = what == DISPATCH_HORIZONTAL;
     switch (n.dpl) {
-#define CASE(k)                                                                                           \
-    case k:                                                                                               \
-        if (wta) return census ? launch_wta_t<k, true>(ctx, n, g, bs) : launch_wta_t<k, false>(ctx, n, g, bs); \
-        return census ? launch_paths_dpl<k, true>(ctx, n, g, bs) : launch_paths_dpl<k, false>(ctx, n, g, bs);
+#define CASE(k)                                                                                               \
+    case k:                                                                                                   \
+        if (what == DISPATCH_WTA)                                                                             \
+            return census ? launch_wta_t<k, true>(ctx, n, g, bs) : launch_wta_t<k, false>(ctx, n, g, bs);     \
+        return census ? launch_paths_dpl<k, true>(ctx, n, g, bs, h) : launch_paths_dpl<k, false>(ctx, n, g, bs, h);
         CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
         CASE(9) CASE(10) CASE(11) CASE(12) CASE(13) CASE(14) CASE(15) CASE(16)
 #undef CASE
@@ -420,9 +433,171 @@ int dispatch(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs, bool wta)
     }
 }
 
-int group_size(const sm_ctx* ctx, const Norm& n, int H, int npairs)
+// ---- fused-sweep engine (sm_sweep.hpp) -----------------------------------------
+int ensure_event(sm_ctx* ctx, hipEvent_t& e);
+
+bool use_sweep(const sm_ctx* ctx, const Norm& n, int H)
 {
-    const size_t per = (size_t)H * std::max(n.width1, 1) * n.D * elem_bytes(n) * n.ndirs;
+    if (ctx->dbg_flags & (DBG_LEGACY | DBG_ROW)) return false;
+    // 8 paths: the per-direction engine stays the default until the sweeps beat
+    // it there; flag 16384 selects the sweeps for 8 paths too
+    if (n.ndirs == 8 && !(ctx->dbg_flags & DBG_SWEEP8)) return false;
+    if (n.cost == SM_COST_CENSUS && !use_cost8(ctx, n)) return false;  // the sweeps read the u8 cost volume
+    if (H > 65535 || n.width1 <= 0) return false;                      // row index lives in 16 tag bits
+    return (uint64_t)H * n.width1 * n.D * 2 <= smk::kMaxRecords;
+}
+
+struct SweepJob {
+    const uint8_t* cost;
+    size_t cost_pair;
+    const uint8_t* ew;
+    size_t ew_pair, ew_slot;
+    uint16_t* part;
+    size_t part_pair;
+    uint32_t* key2;
+    int16_t* pre;
+    int G;
+};
+
+// one sweep pass (MODE 0/1/2, sm_sweep.hpp) over the job's G pairs, in launches
+// whose workgroups are all co-resident (strips of a pair wait on each other)
+int sweep_pass(sm_ctx* ctx, const Norm& n, const Geo& g, const SweepJob& j, int mode)
+{
+    const int ct = (int)elem_bytes(n);
+    smk::SweepInfo si{};
+    if (smk::sweep_info(n.D, ct, mode, ctx->device, &si) != hipSuccess)
+        return fail(ctx, SM_E_UNSUPPORTED, "sweep: numDisparities %d not built", n.D);
+    int ncu = 0;
+    HIP_TRY(ctx, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    // one block per CU of margin below the API's answer (MI355X guide: residency can be one lower)
+    const int cap = std::max(si.blocks_per_cu - 1, 1) * std::max(ncu, 1);
+    const int nwg = (n.width1 + si.cw - 1) / si.cw;
+    if (nwg > cap) return fail(ctx, SM_E_UNSUPPORTED, "sweep: %d strips exceed %d resident workgroups", nwg, cap);
+    // ablation / test flag 8192: one pair per sweep launch (exercises the chunked launches)
+    const int per_launch = (ctx->dbg_flags & DBG_SWEEP1) ? 1 : std::max(1, std::min(j.G, cap / nwg));
+    const size_t hop_pair = (size_t)nwg * 2 * g.H * si.ngr;
+    const size_t hop_bytes = hop_pair * 8 * per_launch;
+    if (hop_pair * 8 > smk::kMaxRecords) return fail(ctx, SM_E_UNSUPPORTED, "sweep: boundary buffer too large");
+    int rc;
+    if (ctx->hop.n < hop_bytes || !ctx->hop.p) {
+        if ((rc = ensure(ctx, ctx->hop, hop_bytes)) != SM_OK) return rc;
+        HIP_TRY(ctx, hipMemsetAsync(ctx->hop.p, 0, ctx->hop.n, ctx->stream));
+        ctx->hop_epoch = 0;
+    }
+    if (!ctx->sweep_err.p) {
+        if ((rc = ensure(ctx, ctx->sweep_err, 256)) != SM_OK) return rc;
+        HIP_TRY(ctx, hipMemsetAsync(ctx->sweep_err.p, 0, 256, ctx->stream));
+    }
+    for (int p0 = 0; p0 < j.G; p0 += per_launch) {
+        const int np = std::min(per_launch, j.G - p0);
+        if (++ctx->hop_epoch > 0xFFFFu) {  // tags repeat: clear the granules once per 65535 launches
+            HIP_TRY(ctx, hipMemsetAsync(ctx->hop.p, 0, ctx->hop.n, ctx->stream));
+            ctx->hop_epoch = 1;
+        }
+        smk::SweepArgs a{};
+        a.cost = j.cost + (size_t)p0 * j.cost_pair;
+        a.cost_pair = j.cost_pair;
+        a.ew = j.ew ? j.ew + (size_t)p0 * j.ew_pair : nullptr;
+        a.ew_pair = j.ew_pair;
+        a.ew_slot = j.ew_slot;
+        a.part = j.part ? (uint16_t*)((uint8_t*)j.part + (size_t)p0 * j.part_pair) : nullptr;
+        a.part_pair = j.part_pair;
+        a.hop = (unsigned long long*)ctx->hop.p;
+        a.hop_pair = hop_pair;
+        a.key2 = j.key2 ? j.key2 + (size_t)p0 * g.H * g.W : nullptr;
+        a.disp = j.pre ? j.pre + (size_t)p0 * g.H * g.W : nullptr;
+        a.err = (uint32_t*)ctx->sweep_err.p;
+        a.H = g.H;
+        a.W = g.W;
+        a.W1 = n.width1;
+        a.D = n.D;
+        a.minD = n.minD;
+        a.minX1 = n.minX1;
+        a.P1 = n.P1;
+        a.P2 = n.P2;
+        a.uniq = n.uniq;
+        a.nwg = nwg;
+        a.epoch = ctx->hop_epoch;
+        a.dbg = (ctx->dbg_flags >> 24) & 15;  // timing ablations (results wrong): 1 no polls
+        HIP_TRY(ctx, smk::sweep_launch(n.D, ct, mode, a, np, ctx->stream));
+    }
+    return SM_OK;
+}
+
+// E/W volumes -> [down sweep partial] -> WTA sweep -> LR check into bs.raw
+int run_sweep(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs)
+{
+    const int G = g.G;
+    int rc;
+    const size_t et = elem_bytes(n);
+    SweepJob j{};
+    j.cost = (const uint8_t*)bs.cost.p;
+    j.cost_pair = g.vol * et;
+    j.ew = (const uint8_t*)bs.L.p;
+    j.ew_pair = g.L_pair;
+    j.ew_slot = g.slot_bytes;
+    j.G = G;
+    if ((rc = ensure(ctx, bs.key2, (size_t)G * g.H * g.W * 4)) != SM_OK) return rc;
+    if ((rc = ensure(ctx, bs.pre, (size_t)G * g.H * g.W * 2)) != SM_OK) return rc;
+    j.key2 = (uint32_t*)bs.key2.p;
+    j.pre = (int16_t*)bs.pre.p;
+    {
+        StageTimer t(ctx, ctx->stream, SM_STAGE_PATHS, G);
+        if (n.ndirs == 8) {
+            // 8 paths: the E/W kernel (latency-bound serial rows) runs on the side
+            // stream beside the down sweep (latency-bound serial columns); the
+            // WTA sweep needs both
+            if ((rc = ensure_event(ctx, ctx->ev_fork)) != SM_OK) return rc;
+            if ((rc = ensure_event(ctx, ctx->ev_join)) != SM_OK) return rc;
+            HIP_TRY(ctx, hipEventRecord(ctx->ev_fork, ctx->stream));
+            HIP_TRY(ctx, hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
+            const hipStream_t main = ctx->stream;
+            ctx->stream = ctx->side;
+            rc = dispatch(ctx, n, g, bs, DISPATCH_HORIZONTAL);
+            ctx->stream = main;
+            if (rc != SM_OK) return rc;
+            HIP_TRY(ctx, hipEventRecord(ctx->ev_join, ctx->side));
+            if ((rc = ensure(ctx, bs.part, (size_t)G * g.vol * 2)) != SM_OK) return rc;
+            j.part = (uint16_t*)bs.part.p;
+            j.part_pair = g.vol * 2;
+            {
+                StageTimer ts(ctx, ctx->stream, SM_STAGE_SWEEP, G);
+                if ((rc = sweep_pass(ctx, n, g, j, 0)) != SM_OK) return rc;
+            }
+            HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
+        } else if ((rc = dispatch(ctx, n, g, bs, DISPATCH_HORIZONTAL)) != SM_OK) {
+            return rc;
+        }
+    }
+    StageTimer t(ctx, ctx->stream, SM_STAGE_WTA, G);
+    HIP_TRY(ctx, hipMemsetAsync(bs.key2.p, 0xFF, (size_t)G * g.H * g.W * 4, ctx->stream));
+    {
+        StageTimer ts(ctx, ctx->stream, SM_STAGE_SWEEP_WTA, G);
+        if ((rc = sweep_pass(ctx, n, g, j, n.ndirs == 8 ? 2 : 1)) != SM_OK) return rc;
+    }
+    HIP_TRY(ctx, smk::lr_check_launch((const int16_t*)bs.pre.p, (const uint32_t*)bs.key2.p, (int16_t*)bs.raw.p, G, g.H,
+                                      g.W, n.minD, n.minX1, n.maxX1, n.disp12, ctx->stream));
+    return SM_OK;
+}
+
+// device-side error word of the sweep engine (boundary poll timeout); clears it
+int check_sweep_errors(sm_ctx* ctx)
+{
+    if (!ctx->sweep_err.p) return SM_OK;
+    uint32_t e = 0;
+    HIP_TRY(ctx, hipMemcpy(&e, ctx->sweep_err.p, 4, hipMemcpyDeviceToHost));
+    if (e) {
+        HIP_TRY(ctx, hipMemset(ctx->sweep_err.p, 0, 4));
+        return fail(ctx, SM_E_HIP, "sweep: strip-boundary hand-off timed out (workgroups not co-resident?)");
+    }
+    return SM_OK;
+}
+
+int group_size(const sm_ctx* ctx, const Norm& n, int H, int npairs, bool sweep)
+{
+    const size_t cells = (size_t)H * std::max(n.width1, 1) * n.D;
+    // sweep engine: E + W volumes (+ the u16 partial at 8 paths); else one volume per direction
+    const size_t per = sweep ? cells * (2 * elem_bytes(n) + (n.ndirs == 8 ? 2 : 0)) : cells * elem_bytes(n) * n.ndirs;
     const size_t g = std::max<size_t>(1, kSetBudget / std::max<size_t>(per, 1));
     // at least two groups per call when possible, so WTA(g) overlaps paths(g+1)
     const size_t half = overlap(ctx) ? std::max(1, (npairs + 1) / 2) : kMaxGroup;
@@ -591,13 +766,17 @@ int run_group(sm_ctx* ctx, const Src& src, const Geo& g, const Norm& n, int16_t*
             }
         }
     }
-    if ((rc = dispatch(ctx, n, g, bs, false)) != SM_OK) return rc;
+    if (g.sweep) {
+        if ((rc = run_sweep(ctx, n, g, bs)) != SM_OK) return rc;
+    } else if ((rc = dispatch(ctx, n, g, bs, DISPATCH_PATHS)) != SM_OK) {
+        return rc;
+    }
     const hipStream_t sb = stream_b(ctx);
     if (sb != ctx->stream) {
         HIP_TRY(ctx, hipEventRecord(bs.paths_done, ctx->stream));
         HIP_TRY(ctx, hipStreamWaitEvent(sb, bs.paths_done, 0));
     }
-    if ((rc = dispatch(ctx, n, g, bs, true)) != SM_OK) return rc;
+    if (!g.sweep && (rc = dispatch(ctx, n, g, bs, DISPATCH_WTA)) != SM_OK) return rc;
     {
         StageTimer t(ctx, sb, SM_STAGE_MEDIAN, G);
         hipLaunchKernelGGL(smk::k_median3, dim3((W + 255) / 256, H, G), dim3(256), 0, sb,
@@ -635,10 +814,12 @@ int run_pairs(sm_ctx* ctx, const Src& src, int npairs, int H, int W, int stride,
     g.stride = stride;
     g.vol = (size_t)H * std::max(n.width1, 0) * n.D;
     g.slot_bytes = (g.vol * elem_bytes(n) + 255) & ~size_t(255);
-    g.L_pair = g.slot_bytes * n.ndirs;
+    g.sweep = use_sweep(ctx, n, H);
+    g.L_pair = g.slot_bytes * (g.sweep ? 2 : n.ndirs);  // sweep engine keeps only the E and W volumes
     g.census_pair = (size_t)H * W;
     g.cost_pair = n.cost == SM_COST_CENSUS ? 0 : g.vol;
-    const int G = group_size(ctx, n, H, npairs);
+    ctx->last_ndirs = g.sweep ? 2 : n.ndirs;
+    const int G = group_size(ctx, n, H, npairs, g.sweep);
     int rc = SM_OK;
     {
         StageTimer total(ctx, ctx->stream, SM_STAGE_TOTAL, npairs);
@@ -971,11 +1152,11 @@ void sm_destroy(sm_ctx* ctx)
                       &ctx->volbuf,  &ctx->wls_num, &ctx->wls_den,   &ctx->wls_inter,   &ctx->wls_disp[0], &ctx->wls_w,
                       &ctx->wls_disp[1], &ctx->wls_out, &ctx->sp_parent, &ctx->sp_count,
                       &ctx->rp_in,   &ctx->rp_out,  &ctx->rp_min,    &ctx->bm_pre[0],   &ctx->bm_pre[1],
-                      &ctx->bm_cost};
+                      &ctx->bm_cost, &ctx->hop,     &ctx->sweep_err};
     for (DevBuf* b : bufs)
         if (b->p) (void)hipFree(b->p);
     for (auto& bs : ctx->set) {
-        DevBuf* sb[] = {&bs.census[0], &bs.census[1], &bs.cost, &bs.L, &bs.raw};
+        DevBuf* sb[] = {&bs.census[0], &bs.census[1], &bs.cost, &bs.L, &bs.raw, &bs.part, &bs.key2, &bs.pre};
         for (DevBuf* b : sb)
             if (b->p) (void)hipFree(b->p);
         if (bs.paths_done) (void)hipEventDestroy(bs.paths_done);
@@ -986,6 +1167,8 @@ void sm_destroy(sm_ctx* ctx)
         (void)hipEventDestroy(t.b);
     }
     for (auto e : ctx->free_events) (void)hipEventDestroy(e);
+    if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
+    if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
     if (ctx->side) (void)hipStreamDestroy(ctx->side);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
     delete ctx;
@@ -1073,7 +1256,7 @@ int sm_compute(sm_ctx* ctx, const uint8_t* L, const uint8_t* R, int H, int W, in
     if (rc != SM_OK) return rc;
     HIP_TRY(ctx, hipMemcpyAsync(disp_out, ctx->out.p, img * 2, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    return SM_OK;
+    return check_sweep_errors(ctx);
 }
 
 int sm_aggregate_cost_f32_device(sm_ctx* ctx, const float* d_cost, int npairs, size_t pair_stride_elems, int D,
@@ -1116,7 +1299,7 @@ int sm_aggregate_cost_f32(sm_ctx* ctx, const float* cost, int D, int H, int W, c
     if (rc != SM_OK) return rc;
     HIP_TRY(ctx, hipMemcpyAsync(disp_out, ctx->out.p, img * 2, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    return SM_OK;
+    return check_sweep_errors(ctx);
 }
 
 int sm_wls_default_params(const sm_params* left, sm_wls_params* out)
@@ -1180,7 +1363,7 @@ int sm_wls_filter(sm_ctx* ctx, const int16_t* displ, const int16_t* dispr, const
     if (rc != SM_OK) return rc;
     HIP_TRY(ctx, hipMemcpyAsync(out, ctx->wls_out.p, img * 2, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    return SM_OK;
+    return check_sweep_errors(ctx);
 }
 
 // compute_disparity (stereo_vision/stereo_vision.py:132-184) in one call, on
@@ -1230,7 +1413,7 @@ int sm_compute_disparity(sm_ctx* ctx, const uint8_t* L, const uint8_t* R, int H,
     HIP_TRY(ctx, hipMemcpyAsync(displ, ctx->wls_disp[0].p, img * 2, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(filtered, ctx->wls_out.p, img * 2, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    return SM_OK;
+    return check_sweep_errors(ctx);
 }
 
 int sm_filter_speckles_device(sm_ctx* ctx, int16_t* d_img, int nimg, int H, int W, int new_val,
@@ -1258,7 +1441,7 @@ int sm_filter_speckles(sm_ctx* ctx, int16_t* img, int H, int W, int new_val, int
         return rc;
     HIP_TRY(ctx, hipMemcpyAsync(img, ctx->out.p, bytes, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    return SM_OK;
+    return check_sweep_errors(ctx);
 }
 
 int sm_reproject_image_to_3d_device(sm_ctx* ctx, const void* d_disp, int disp_type, int nimg, int H, int W,
@@ -1319,7 +1502,7 @@ int sm_reproject_image_to_3d(sm_ctx* ctx, const void* disp, int disp_type, int H
         return rc;
     HIP_TRY(ctx, hipMemcpyAsync(xyz, ctx->rp_out.p, npx * 12, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    return SM_OK;
+    return check_sweep_errors(ctx);
 }
 
 int sm_bm_default_params(int num_disparities, int block_size, sm_bm_params* out)
@@ -1386,7 +1569,7 @@ int sm_bm_compute(sm_ctx* ctx, const uint8_t* L, const uint8_t* R, int H, int W,
     if (rc != SM_OK) return rc;
     HIP_TRY(ctx, hipMemcpyAsync(disp_out, ctx->out.p, img * 2, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    return SM_OK;
+    return check_sweep_errors(ctx);
 }
 
 // Multi-device batch from one process: ctxs[k] (one per device,
@@ -1453,7 +1636,7 @@ int sm_synchronize(sm_ctx* ctx)
     if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->side));
-    return SM_OK;
+    return check_sweep_errors(ctx);
 }
 
 int sm_set_timing(sm_ctx* ctx, int enable)

@@ -216,14 +216,18 @@ __device__ __forceinline__ void store_n(T* __restrict__ p, const uint32_t (&in)[
 using rsrc_t = __amdgpu_buffer_rsrc_t;
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-constexpr uint32_t kOOB = 0x80000000u;
+// out-of-range offset for masked lanes: above every volume a descriptor
+// covers (per-pair volumes are limited to kMaxRecords bytes on the host side)
+// and far enough below 2^32 that the small per-chunk increments never wrap
+constexpr uint32_t kOOB = 0xFFFF0000u;
+constexpr uint64_t kMaxRecords = 0xFFFE0000ull;
 
 __device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint64_t bytes)
 {
     const uint64_t p = (uint64_t)base;
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p);
     const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
-    const uint32_t n = __builtin_amdgcn_readfirstlane((uint32_t)(bytes > 0xFFFFFFFFull ? 0xFFFFFFFFull : bytes));
+    const uint32_t n = __builtin_amdgcn_readfirstlane((uint32_t)(bytes > kMaxRecords ? kMaxRecords : bytes));
     return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, (int)n, 0x00020000);
 }
 

@@ -1,0 +1,99 @@
+// sm_sweep.hip — translation unit of the fused-sweep kernels (sm_sweep.hpp):
+// instantiates k_sweep for every built (D, cost type, mode) and exposes a
+// plain host interface to sm_api.hip, so the two units compile in parallel.
+#include "sm_sweep.hpp"
+#include "sm_sweep_host.hpp"
+
+namespace smk {
+
+namespace {
+
+// calls f.template run<VL, DPL, CT, SWEEP_MODE>() for the instance serving (D, ct_bytes); this unit
+// is compiled once per mode (-DSWEEP_MODE=0/1/2) so the three compile in parallel
+template <class F>
+hipError_t with_sweep(int D, int ct_bytes, F& f)
+{
+    return ct_bytes == 1 ? with_d<uint8_t, SWEEP_MODE>(D, f) : with_d<uint16_t, SWEEP_MODE>(D, f);
+}
+
+}  // namespace
+
+template <typename CT, int MODE, class F>
+hipError_t with_d(int D, F& f)
+{
+    switch (D) {
+        // 8-lane lines up to D = 64, 16-lane lines above (<= 16 disparities per lane)
+#define SW8(d) \
+    case d: return f.template run<8, d / 8, CT, MODE>();
+#define SW16(d) \
+    case d: return f.template run<16, d / 16, CT, MODE>();
+        SW8(16) SW8(32) SW8(48) SW8(64) SW16(80) SW16(96) SW16(112) SW16(128)
+        SW16(144) SW16(160) SW16(176) SW16(192) SW16(208) SW16(224) SW16(240) SW16(256)
+#undef SW8
+#undef SW16
+    default: return hipErrorInvalidValue;
+    }
+}
+
+namespace {
+
+struct InfoF {
+    int device;
+    SweepInfo* out;
+    template <int VL, int DPL, typename CT, int MODE>
+    hipError_t run()
+    {
+        using SG = SweepGeo<VL, DPL>;
+        static int per_cu = -1;  // per instance (one device type per process)
+        if (per_cu < 0) {
+            int nb = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_sweep<VL, DPL, CT, MODE>, 256, 0) != hipSuccess) nb = 1;
+            per_cu = nb;
+        }
+        out->cw = SG::CW;
+        out->ngr = SG::NGR;
+        out->blocks_per_cu = per_cu;
+        return hipSuccess;
+    }
+};
+
+struct LaunchF {
+    const SweepArgs* a;
+    dim3 grid;
+    hipStream_t stream;
+    template <int VL, int DPL, typename CT, int MODE>
+    hipError_t run()
+    {
+        hipLaunchKernelGGL((k_sweep<VL, DPL, CT, MODE>), grid, dim3(256), 0, stream, *a);
+        return hipGetLastError();
+    }
+};
+
+}  // namespace
+
+#define SW_CAT2(a, b) a##b
+#define SW_CAT(a, b) SW_CAT2(a, b)
+
+hipError_t SW_CAT(sweep_info_m, SWEEP_MODE)(int D, int ct_bytes, int device, SweepInfo* out)
+{
+    InfoF f{device, out};
+    return with_sweep(D, ct_bytes, f);
+}
+
+hipError_t SW_CAT(sweep_launch_m, SWEEP_MODE)(int D, int ct_bytes, const SweepArgs& a, int npairs, hipStream_t stream)
+{
+    LaunchF f{&a, dim3(a.nwg, npairs), stream};
+    return with_sweep(D, ct_bytes, f);
+}
+
+#if SWEEP_MODE == 0
+hipError_t lr_check_launch(const int16_t* pre, const uint32_t* key2, int16_t* out, int G, int H, int W, int minD,
+                           int minX1, int maxX1, int disp12, hipStream_t stream)
+{
+    hipLaunchKernelGGL(k_lr_check, dim3((W + 255) / 256, H, G), dim3(256), 0, stream, pre, key2, out, H, W, minD, minX1,
+                       maxX1, disp12);
+    return hipGetLastError();
+}
+#endif
+
+}  // namespace smk

@@ -1,0 +1,63 @@
+// sm_sweep_host.hpp — host interface of the fused-sweep kernels (sm_sweep.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace smk {
+
+// MODE: 0 = down sweep writing the u16 partial (8 paths, first pass)
+//       1 = down sweep + E/W + WTA (MODE_SGBM: 5 paths)
+//       2 = up sweep + E/W + down partial + WTA (8 paths, second pass)
+struct SweepArgs {
+    const uint8_t* cost;  // [pair][H][W1][D] of CT
+    size_t cost_pair;     // bytes
+    const uint8_t* ew;    // E volume; W at ew + ew_slot (same layout, CT)
+    size_t ew_pair, ew_slot;
+    uint16_t* part;  // [pair][H][W1][D] u16 partial (written by MODE 0, read by MODE 2)
+    size_t part_pair;  // bytes
+    unsigned long long* hop;  // boundary granules [pair][nwg][2][H][NGR]
+    size_t hop_pair;          // granules per pair
+    uint32_t* key2;  // [pair][H][W] disp2 keys (minS << 16 | 0xFFFF - X), preset to ~0
+    int16_t* disp;   // [pair][H][W] WTA output before the LR check (domain columns only)
+    uint32_t* err;   // bit 0: a boundary poll timed out
+    int H, W, W1, D, minD, minX1, P1, P2, uniq;
+    int nwg;
+    uint32_t epoch;  // 1..65535, distinct from the previous launches on the same hop buffer
+    int dbg;         // timing ablations only: 1 no waiting in the boundary polls, 2 no polls
+};
+
+
+struct SweepInfo {
+    int cw;             // columns per workgroup (strip width)
+    int ngr;            // boundary granules per (strip, direction, row)
+    int blocks_per_cu;  // occupancy API answer for 256-thread blocks
+};
+
+template <typename CT, int MODE, class F>
+hipError_t with_d(int D, F& f);
+
+// per mode (one translation unit each); hipErrorInvalidValue when (D, ct_bytes) is not built
+hipError_t sweep_info_m0(int D, int ct_bytes, int device, SweepInfo* out);
+hipError_t sweep_info_m1(int D, int ct_bytes, int device, SweepInfo* out);
+hipError_t sweep_info_m2(int D, int ct_bytes, int device, SweepInfo* out);
+// grid (a.nwg, npairs), 256 threads
+hipError_t sweep_launch_m0(int D, int ct_bytes, const SweepArgs& a, int npairs, hipStream_t stream);
+hipError_t sweep_launch_m1(int D, int ct_bytes, const SweepArgs& a, int npairs, hipStream_t stream);
+hipError_t sweep_launch_m2(int D, int ct_bytes, const SweepArgs& a, int npairs, hipStream_t stream);
+
+inline hipError_t sweep_info(int D, int ct_bytes, int mode, int device, SweepInfo* out)
+{
+    return mode == 0 ? sweep_info_m0(D, ct_bytes, device, out)
+         : mode == 1 ? sweep_info_m1(D, ct_bytes, device, out)
+                     : sweep_info_m2(D, ct_bytes, device, out);
+}
+inline hipError_t sweep_launch(int D, int ct_bytes, int mode, const SweepArgs& a, int npairs, hipStream_t stream)
+{
+    return mode == 0 ? sweep_launch_m0(D, ct_bytes, a, npairs, stream)
+         : mode == 1 ? sweep_launch_m1(D, ct_bytes, a, npairs, stream)
+                     : sweep_launch_m2(D, ct_bytes, a, npairs, stream);
+}
+hipError_t lr_check_launch(const int16_t* pre, const uint32_t* key2, int16_t* out, int G, int H, int W, int minD,
+                           int minX1, int maxX1, int disp12, hipStream_t stream);
+
+}  // namespace smk

@@ -58,8 +58,9 @@ def test_census_images_match_oracle(eng):
 def test_path_volumes_match_oracle(eng, cost, mode, D, flags):
     left, right, _ = synthetic.random_dot_pair(33, 101 + D, D, seed=8)
     p = dict(synthetic.headline_params(D) if cost else synthetic.parity_params(D), mode=mode)
-    # flags 48 = fused row kernel (32) + keep its W volume (16), which it normally never writes
-    eng.set_debug_flags(flags)
+    # flags 48 = fused row kernel (32) + keep its W volume (16), which it normally never writes;
+    # 4096 = per-direction engine (the fused sweeps never materialise the per-direction volumes)
+    eng.set_debug_flags(flags | 4096)
     try:
         run(eng, left, right, p)
     finally:
@@ -87,8 +88,21 @@ for _i in range(36):
                       d12=int(_rng.choice([1, 2, 1000000])), seed=int(_rng.integers(0, 1 << 30))))
 
 
+@pytest.mark.parametrize("flags", [0, 16384], ids=["default", "sweep8"])
 @pytest.mark.parametrize("c", CASES, ids=lambda c: "H{H}W{W}D{D}m{minD}c{cost}p{mode}".format(**c))
-def test_random_shapes_vs_c_oracle(eng, c):
+def test_random_shapes_vs_c_oracle(eng, c, flags):
+    """Default engines, then the fused sweeps for 8 paths too (16384; 5 paths
+    run on the sweeps by default)."""
+    if flags and c["mode"] != 8:
+        pytest.skip("5 paths already run on the sweeps by default")
+    eng.set_debug_flags(flags)
+    try:
+        _random_case(eng, c)
+    finally:
+        eng.set_debug_flags(0)
+
+
+def _random_case(eng, c):
     left, right, _ = synthetic.random_dot_pair(c["H"], c["W"], c["D"], seed=c["seed"])
     if c["cost"]:
         p = dict(synthetic.headline_params(c["D"]), minDisparity=c["minD"], mode=c["mode"],
@@ -104,7 +118,9 @@ def test_random_shapes_vs_c_oracle(eng, c):
 
 @pytest.mark.parametrize("name,cost,mode,flags", [("kitti", 1, 8, 0), ("kitti", 0, 5, 0), ("kitti", 0, 8, 0),
                                                   ("kitti", 1, 5, 0), ("mccnn", 1, 8, 0), ("kitti", 1, 8, 32),
-                                                  ("kitti", 1, 8, 1024), ("kitti", 1, 8, 512)])
+                                                  ("kitti", 1, 8, 1024), ("kitti", 1, 8, 512),
+                                                  ("kitti", 1, 8, 16384), ("kitti", 0, 8, 16384),
+                                                  ("kitti", 0, 5, 4096), ("mccnn", 1, 8, 16384)])
 def test_full_size_bit_exact(eng, name, cost, mode, flags):
     H, W, D = synthetic.CONFIGS[name]
     left, right, gt = synthetic.random_dot_pair(H, W, D, seed=42)
@@ -165,12 +181,14 @@ def test_batch_device_matches_single(eng):
         assert np.array_equal(got[i], ref_c.compute(a, b, q))
 
 
-@pytest.mark.parametrize("flags", [0, 32, 64, 96])
+@pytest.mark.parametrize("flags", [0, 32, 64, 96, 4096, 8192, 16384, 16384 | 8192])
 def test_batch_pipeline_groups(eng, flags):
-    """Batches through the normal pipeline, the fused row kernel (32) and the
-    two-stream overlap (64: 7 pairs -> launch groups of 4 + 3 on alternating
-    buffer sets, WTA of group g on the second stream beside paths of group
-    g+1); then a call with a different geometry reuses (and regrows) the sets."""
+    """Batches through the normal pipeline (fused sweeps), the fused row kernel
+    (32), the two-stream overlap (64: 7 pairs -> launch groups of 4 + 3 on
+    alternating buffer sets, WTA of group g on the second stream beside paths
+    of group g+1), the per-direction engine (4096) and one pair per sweep
+    launch (8192); then a call with a different geometry reuses (and regrows)
+    the sets."""
     import torch
 
     eng.set_debug_flags(flags)
@@ -185,6 +203,7 @@ def test_batch_pipeline_groups(eng, flags):
                 eng.compute_batch_device(L.data_ptr(), R.data_ptr(), n, H * W, H, W, W,
                                          synthetic.to_sm_params(p), out.data_ptr())
                 got = out.cpu().numpy()  # same stream: ordered after both internal streams
+                eng.synchronize()  # raises if a sweep strip hand-off timed out
                 eng.set_stream(None)
                 for i, (a, b) in enumerate(pairs):
                     assert np.array_equal(got[i], ref_c.compute(a, b, p)), (H, W, D, i, p.get("cost"))
@@ -244,6 +263,14 @@ def test_timing_counters(eng):
     eng.set_timing(False)
     assert t["paths"][1] == 3 and t["total"][1] == 3
     assert 0 < t["paths"][0] <= t["total"][0]
+    # sweep engine (5 paths): E/W kernel and the WTA sweep are timed on their own too
+    eng.set_timing(True)
+    eng.reset_timing()
+    for _ in range(2):
+        run(eng, left, right, synthetic.parity_params(64))
+    t = eng.timing()
+    eng.set_timing(False)
+    assert t["paths"][1] == 2 and t["horizontal"][1] == 2 and t["sweep_wta"][1] == 2 and t["wta"][1] == 2
 
 
 # ---------------------------------------------------------------- mc-cnn cost volume

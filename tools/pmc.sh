@@ -21,7 +21,7 @@ for f in glob.glob(out + "/p*/**/*counter_collection.csv", recursive=True):
         k = r.get("Kernel_Name", "")[:60]
         agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, d in agg.items():
-    if "paths" not in k and "wta" not in k: continue
+    if "paths" not in k and "wta" not in k and "sweep" not in k: continue
     print(k)
     for c, v in sorted(d.items()):
         print(f"   {c:28s} mean/dispatch {sum(v)/len(v):.4g}  (n={len(v)})")
