@@ -60,7 +60,7 @@ struct TimedEvent {
 // per-group device buffers (double-buffered across launch groups)
 struct BufSet {
     DevBuf census[2], cost, L, raw;
-    DevBuf part, key2, pre;  // sweep engine: u16 partial sums, disp2 keys, WTA output before the LR check
+    DevBuf part, key2, pre;  // sweep engine: u16 partial sums, WTA winner records, sub-pixel inputs
     hipEvent_t paths_done = nullptr, wta_done = nullptr;
     bool pending = false;  // wta_done recorded and not yet waited for by stream A
 };
@@ -444,6 +444,7 @@ bool use_sweep(const sm_ctx* ctx, const Norm& n, int H)
     if (n.ndirs == 8 && !(ctx->dbg_flags & DBG_SWEEP8)) return false;
     if (n.cost == SM_COST_CENSUS && !use_cost8(ctx, n)) return false;  // the sweeps read the u8 cost volume
     if (H > 65535 || n.width1 <= 0) return false;                      // row index lives in 16 tag bits
+    if ((size_t)n.maxX1 * 6 + 16 > 65536) return false;                 // k_lr_rows keeps a row in LDS
     return (uint64_t)H * n.width1 * n.D * 2 <= smk::kMaxRecords;
 }
 
@@ -455,7 +456,7 @@ struct SweepJob {
     uint16_t* part;
     size_t part_pair;
     uint32_t* key2;
-    int16_t* pre;
+    uint32_t* pre;  // sub-pixel inputs (SweepArgs::nb)
     int G;
 };
 
@@ -469,13 +470,16 @@ int sweep_pass(sm_ctx* ctx, const Norm& n, const Geo& g, const SweepJob& j, int 
         return fail(ctx, SM_E_UNSUPPORTED, "sweep: numDisparities %d not built", n.D);
     int ncu = 0;
     HIP_TRY(ctx, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
-    // one block per CU of margin below the API's answer (MI355X guide: residency can be one lower)
-    const int cap = std::max(si.blocks_per_cu - 1, 1) * std::max(ncu, 1);
+    // the API's answer can be one block per CU high at >= 82 SGPRs (MI355X guide);
+    // for 512-thread blocks SGPRs allow >= 3 per CU, so a margin is kept only above 2
+    const int per_cu = si.blocks_per_cu >= 3 ? si.blocks_per_cu - 1 : std::max(si.blocks_per_cu, 1);
+    const int cap = per_cu * std::max(ncu, 1);
     const int nwg = (n.width1 + si.cw - 1) / si.cw;
+    const int nblk = (g.H + si.hb - 1) / si.hb;
     if (nwg > cap) return fail(ctx, SM_E_UNSUPPORTED, "sweep: %d strips exceed %d resident workgroups", nwg, cap);
     // ablation / test flag 8192: one pair per sweep launch (exercises the chunked launches)
     const int per_launch = (ctx->dbg_flags & DBG_SWEEP1) ? 1 : std::max(1, std::min(j.G, cap / nwg));
-    const size_t hop_pair = (size_t)nwg * 2 * g.H * si.ngr;
+    const size_t hop_pair = (size_t)nwg * 2 * nblk * si.ngr;
     const size_t hop_bytes = hop_pair * 8 * per_launch;
     if (hop_pair * 8 > smk::kMaxRecords) return fail(ctx, SM_E_UNSUPPORTED, "sweep: boundary buffer too large");
     int rc;
@@ -504,8 +508,8 @@ int sweep_pass(sm_ctx* ctx, const Norm& n, const Geo& g, const SweepJob& j, int 
         a.part_pair = j.part_pair;
         a.hop = (unsigned long long*)ctx->hop.p;
         a.hop_pair = hop_pair;
-        a.key2 = j.key2 ? j.key2 + (size_t)p0 * g.H * g.W : nullptr;
-        a.disp = j.pre ? j.pre + (size_t)p0 * g.H * g.W : nullptr;
+        a.rec = j.key2 ? j.key2 + (size_t)p0 * g.H * g.W : nullptr;
+        a.nb = j.pre ? j.pre + (size_t)p0 * g.H * g.W : nullptr;
         a.err = (uint32_t*)ctx->sweep_err.p;
         a.H = g.H;
         a.W = g.W;
@@ -538,9 +542,9 @@ int run_sweep(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs)
     j.ew_slot = g.slot_bytes;
     j.G = G;
     if ((rc = ensure(ctx, bs.key2, (size_t)G * g.H * g.W * 4)) != SM_OK) return rc;
-    if ((rc = ensure(ctx, bs.pre, (size_t)G * g.H * g.W * 2)) != SM_OK) return rc;
+    if ((rc = ensure(ctx, bs.pre, (size_t)G * g.H * g.W * 4)) != SM_OK) return rc;
     j.key2 = (uint32_t*)bs.key2.p;
-    j.pre = (int16_t*)bs.pre.p;
+    j.pre = (uint32_t*)bs.pre.p;
     {
         StageTimer t(ctx, ctx->stream, SM_STAGE_PATHS, G);
         if (n.ndirs == 8) {
@@ -570,13 +574,12 @@ int run_sweep(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs)
         }
     }
     StageTimer t(ctx, ctx->stream, SM_STAGE_WTA, G);
-    HIP_TRY(ctx, hipMemsetAsync(bs.key2.p, 0xFF, (size_t)G * g.H * g.W * 4, ctx->stream));
     {
         StageTimer ts(ctx, ctx->stream, SM_STAGE_SWEEP_WTA, G);
         if ((rc = sweep_pass(ctx, n, g, j, n.ndirs == 8 ? 2 : 1)) != SM_OK) return rc;
     }
-    HIP_TRY(ctx, smk::lr_check_launch((const int16_t*)bs.pre.p, (const uint32_t*)bs.key2.p, (int16_t*)bs.raw.p, G, g.H,
-                                      g.W, n.minD, n.minX1, n.maxX1, n.disp12, ctx->stream));
+    HIP_TRY(ctx, smk::lr_rows_launch((const uint32_t*)bs.key2.p, (const uint32_t*)bs.pre.p, (int16_t*)bs.raw.p, G,
+                                     g.H, g.W, n.D, n.minD, n.minX1, n.maxX1, n.disp12, ctx->stream));
     return SM_OK;
 }
 

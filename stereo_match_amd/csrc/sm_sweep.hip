@@ -47,11 +47,15 @@ struct InfoF {
         static int per_cu = -1;  // per instance (one device type per process)
         if (per_cu < 0) {
             int nb = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_sweep<VL, DPL, CT, MODE>, 256, 0) != hipSuccess) nb = 1;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_sweep<VL, DPL, CT, MODE>, SG::THREADS, 0) !=
+                hipSuccess)
+                nb = 1;
             per_cu = nb;
         }
         out->cw = SG::CW;
+        out->hb = SG::HB;
         out->ngr = SG::NGR;
+        out->threads = SG::THREADS;
         out->blocks_per_cu = per_cu;
         return hipSuccess;
     }
@@ -64,7 +68,7 @@ struct LaunchF {
     template <int VL, int DPL, typename CT, int MODE>
     hipError_t run()
     {
-        hipLaunchKernelGGL((k_sweep<VL, DPL, CT, MODE>), grid, dim3(256), 0, stream, *a);
+        hipLaunchKernelGGL((k_sweep<VL, DPL, CT, MODE>), grid, dim3(SweepGeo<VL, DPL>::THREADS), 0, stream, *a);
         return hipGetLastError();
     }
 };
@@ -87,10 +91,10 @@ hipError_t SW_CAT(sweep_launch_m, SWEEP_MODE)(int D, int ct_bytes, const SweepAr
 }
 
 #if SWEEP_MODE == 0
-hipError_t lr_check_launch(const int16_t* pre, const uint32_t* key2, int16_t* out, int G, int H, int W, int minD,
-                           int minX1, int maxX1, int disp12, hipStream_t stream)
+hipError_t lr_rows_launch(const uint32_t* rec, const uint32_t* nb, int16_t* out, int G, int H, int W, int D, int minD,
+                          int minX1, int maxX1, int disp12, hipStream_t stream)
 {
-    hipLaunchKernelGGL(k_lr_check, dim3((W + 255) / 256, H, G), dim3(256), 0, stream, pre, key2, out, H, W, minD, minX1,
+    hipLaunchKernelGGL(k_lr_rows, dim3(H, G), dim3(256), (size_t)W * 6 + 16, stream, rec, nb, out, H, W, D, minD, minX1,
                        maxX1, disp12);
     return hipGetLastError();
 }

@@ -8,24 +8,37 @@
 //   up sweep:   N (0,-1), NE (+1,-1), NW (-1,-1)
 // and their per-cell sum never leaves the chip except as one u16 partial
 // (8 paths) — or not at all: the last sweep adds the horizontal (E, W) volumes
-// and the other sweep's partial and runs the WTA / uniqueness / sub-pixel /
-// disp2 step in place.  Traffic per cell (census, 8 paths): cost 1 B written,
-// 4 B read (E, W, down, up), E/W 2 B written + 2 B read, partial 2 + 2 B = 13 B.
+// and the other sweep's partial and runs the WTA / uniqueness / sub-pixel
+// step in place (disp2 + the LR check follow in k_lr_rows).  Traffic per cell
+// (census, 8 paths): cost 1 B written, 4 B read (E, W, down, up), E/W 2 B
+// written + 2 B read, partial 2 + 2 B = 13 B.
 //
-// Decomposition: a workgroup owns a strip of CW adjacent columns of one pair
-// for all rows (4 waves, 64/VL columns per wave, VL lanes per column, DPL =
-// D/VL disparities per lane).  The vertical direction is private to a lane
-// group.  The diagonals read the previous row's L vector of the neighbouring
-// column: inside the strip through a double-buffered LDS row (one barrier per
-// row); across strips through tagged 8-byte granules written `sc1` by the
-// edge column and polled `sc1` by the neighbouring workgroup (MI355X guide
-// §6 Guideline 16, form R2: the data is the flag, no fence).  All workgroups
-// of a pair must be co-resident: the host sizes the grid from the occupancy
-// query, and every poll is bounded (timeout -> error word, never a hang).
+// Decomposition.  A workgroup owns a strip of CW adjacent columns of one pair
+// for all rows.  Its compute waves hold NCW*LPW columns (LPW = 64/VL columns
+// per wave, VL lanes per column, DPL = D/VL disparities per lane): wave 0 is
+// a LEFT HALO (the neighbour strip's last LPW columns, direction A = +dx only),
+// waves 1..NCW-2 are the strip's own columns, wave NCW-1 is a RIGHT HALO (the
+// next strip's first LPW columns, direction B = -dx only).  The vertical path
+// is private to a lane group; the diagonals read the previous row's L vector
+// of the neighbouring column through a double-buffered LDS row (one LDS-only
+// barrier per row).
+//
+// Trapezoid exchange.  Rows run in blocks of HB = LPW.  At a block boundary
+// the halo columns' A / B state is replaced by the neighbouring strips' own
+// state of the block's last row; inside the block a halo column's value goes
+// stale one column per row from the outer edge in, which never reaches an own
+// column within HB rows.  So strips hand each other one LPW-column snapshot
+// per HB rows (tagged 8-byte granules written `sc1`, polled `sc1`: MI355X guide
+// §6 Guideline 16 form R2) instead of one column per row.  A dedicated POLLER
+// wave does the polling and writes the snapshot into the halo columns' LDS
+// slots between two barriers: it issues no other memory operation, so its
+// vmcnt waits never drain the compute waves' load rings.  All workgroups of a
+// pair must be co-resident (the host sizes the grid from the occupancy query);
+// every poll is bounded (timeout -> error word, never a hang).
 //
 // Recurrence and domain exactly as sm_paths.hpp / oracle/sgm_np.py: a path
-// enters [minX1, maxX1) x [0, H) with Lp = 0 and minLp = 0 (the LDS halo
-// columns of the outermost strips stay zero, inactive columns hold zero).
+// enters [minX1, maxX1) x [0, H) with Lp = 0 and minLp = 0 (columns outside
+// the domain hold the zero state).
 #pragma once
 #include "sm_common.hpp"
 #include "sm_sweep_host.hpp"
@@ -34,19 +47,21 @@ namespace smk {
 
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 
-constexpr int SW_WAVES = 4;
 constexpr uint32_t SW_SPIN_LIMIT = 1u << 19;
-constexpr int SW_PF = 3;  // rows of inputs in flight per lane
 
 template <int VL, int DPL>
 struct SweepGeo {
-    static constexpr int LPW = 64 / VL;            // columns per wave
-    static constexpr int CW = SW_WAVES * LPW;      // columns per workgroup
-    static constexpr int COLS = CW + 2;            // + one halo column each side
+    static constexpr int LPW = 64 / VL;             // columns per wave
+    static constexpr int NCW = 7;                   // compute waves: left halo, 5 own, right halo
+    static constexpr int THREADS = (NCW + 1) * 64;  // + the poller wave
+    static constexpr int HB = LPW;                  // rows per block = halo width
+    static constexpr int NCOL = NCW * LPW;          // columns held by the compute waves
+    static constexpr int COLS = NCOL + 2;           // + one never-written zero column each side
+    static constexpr int CW = (NCW - 2) * LPW;      // own columns per workgroup
     static constexpr int D = VL * DPL;
-    static constexpr int NG = (DPL + 1) / 2;       // granules per lane (two u16 per granule)
-    static constexpr int NGR = VL * NG;            // granules per (strip, direction, row)
-    static constexpr int LDS_BYTES = 2 * 2 * COLS * D * 2 + 2 * 2 * COLS * 4;
+    static constexpr int NG = (DPL + 1) / 2;        // granules per lane (two u16 per granule)
+    static constexpr int NGR = 64 * NG;             // granules per (strip, direction, block)
+    static constexpr int PF = 4;                    // rows of inputs in flight per lane
 };
 
 template <int VL>
@@ -59,13 +74,24 @@ __device__ __forceinline__ uint32_t line_or(uint32_t v)
     return v;
 }
 
-template <int VL>
-__device__ __forceinline__ uint32_t line_min(uint32_t v)
+// minimum over aligned groups of N lanes (N = 4, 8 or 16)
+template <int N>
+__device__ __forceinline__ uint32_t group_min(uint32_t v)
 {
     v = ::min(v, perm_dpp<DPP_QP_XOR1>(v));
     v = ::min(v, perm_dpp<DPP_QP_XOR2>(v));
-    v = ::min(v, perm_dpp<DPP_ROW_HALF_MIRROR>(v));
-    if constexpr (VL == 16) v = ::min(v, perm_dpp<DPP_ROW_MIRROR>(v));
+    if constexpr (N >= 8) v = ::min(v, perm_dpp<DPP_ROW_HALF_MIRROR>(v));
+    if constexpr (N >= 16) v = ::min(v, perm_dpp<DPP_ROW_MIRROR>(v));
+    return v;
+}
+
+template <int N>
+__device__ __forceinline__ uint32_t group_max(uint32_t v)
+{
+    v = ::max(v, perm_dpp<DPP_QP_XOR1>(v));
+    v = ::max(v, perm_dpp<DPP_QP_XOR2>(v));
+    if constexpr (N >= 8) v = ::max(v, perm_dpp<DPP_ROW_HALF_MIRROR>(v));
+    if constexpr (N >= 16) v = ::max(v, perm_dpp<DPP_ROW_MIRROR>(v));
     return v;
 }
 
@@ -87,7 +113,7 @@ __device__ __forceinline__ uint32_t sweep_step(const uint32_t (&Lp)[DPL], uint32
         Ln[i] = C[i] + v - minLp;
         mn = min(mn, Ln[i]);
     }
-    return line_min<VL>(mn);
+    return group_min<VL>(mn);
 }
 
 // DPL u16 values of one lane in LDS (little-endian pairs), widest aligned chunks
@@ -159,10 +185,9 @@ __device__ __forceinline__ void unpack_ct(const RawBytes<DPL * (int)sizeof(CT)>&
 }
 
 // Workgroup barrier that orders LDS only.  __syncthreads() is a workgroup
-// release of global memory too: each wave then waits (vmcnt) for its own
-// just-issued global stores to be acknowledged before every row's barrier.
-// Nothing global is exchanged inside a workgroup here (the strip hand-off has
-// its own protocol), so only the LDS writes have to land first.
+// release of global memory too: each wave would then wait (vmcnt) for its own
+// just-issued global stores before every row's barrier.  Nothing global is
+// exchanged inside a workgroup here, so only the LDS writes have to land first.
 __device__ __forceinline__ void lds_barrier()
 {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
@@ -170,17 +195,17 @@ __device__ __forceinline__ void lds_barrier()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-// Poll NG granules of one lane until every tag equals `tag` (lanes with !need
+// Poll N granules of one lane until every tag equals `tag` (lanes with !need
 // do not load).  Wave-uniform exit; gives up after SW_SPIN_LIMIT passes.
-template <int NG>
-__device__ __forceinline__ void poll_granules(const gu64* src, bool need, uint32_t tag, uint32_t (&v)[NG], bool& dead,
+template <int N>
+__device__ __forceinline__ void poll_granules(const gu64* src, bool need, uint32_t tag, uint32_t (&v)[N], bool& dead,
                                               uint32_t* err)
 {
     for (uint32_t spins = 0;; spins++) {
         bool ok = true;
         if (need) {
 #pragma unroll
-            for (int k = 0; k < NG; k++) {
+            for (int k = 0; k < N; k++) {
                 const unsigned long long x = __hip_atomic_load(src + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 v[k] = (uint32_t)x;
                 ok &= (uint32_t)(x >> 32) == tag;
@@ -197,94 +222,141 @@ __device__ __forceinline__ void poll_granules(const gu64* src, bool need, uint32
 }
 
 template <int VL, int DPL, typename CT, int MODE>
-__global__ void __launch_bounds__(256) k_sweep(SweepArgs a)
+__global__ void __launch_bounds__((SweepGeo<VL, DPL>::THREADS)) k_sweep(SweepArgs a)
 {
     using G = SweepGeo<VL, DPL>;
     constexpr bool UP = MODE == 2;
     constexpr bool WTA = MODE != 0;
-    constexpr int LPW = G::LPW, CW = G::CW, COLS = G::COLS, D = G::D, NG = G::NG, NGR = G::NGR;
+    constexpr int LPW = G::LPW, NCW = G::NCW, HB = G::HB, NCOL = G::NCOL, COLS = G::COLS, CW = G::CW, D = G::D;
+    constexpr int NG = G::NG, NGR = G::NGR, PF = G::PF;
     constexpr int CB = DPL * (int)sizeof(CT);  // cost / E / W bytes per lane and cell
     __shared__ __attribute__((aligned(16))) uint16_t lv[2][2][COLS][D];  // [buf][A=+dx, B=-dx][col+1][d]
     __shared__ uint32_t lmin[2][2][COLS];
+    // WTA sweeps: each own column's aggregated costs S of the current row
+    // (wave-local; the line's first lane reads S[best-1], S[best+1] back)
+    __shared__ __attribute__((aligned(16))) uint16_t srow[WTA ? NCW - 2 : 1][WTA ? LPW : 1][WTA ? D : 2];
 
-    for (int i = threadIdx.x; i < 2 * 2 * COLS * D / 2; i += 256) reinterpret_cast<uint32_t*>(&lv[0][0][0][0])[i] = 0;
-    for (int i = threadIdx.x; i < 2 * 2 * COLS; i += 256) (&lmin[0][0][0])[i] = 0;
+    for (int i = threadIdx.x; i < 2 * 2 * COLS * D / 2; i += G::THREADS)
+        reinterpret_cast<uint32_t*>(&lv[0][0][0][0])[i] = 0;
+    for (int i = threadIdx.x; i < 2 * 2 * COLS; i += G::THREADS) (&lmin[0][0][0])[i] = 0;
     __syncthreads();
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int kl = lane / VL, g = lane % VL;
-    const int c = wave * LPW + kl;  // column inside the strip
     const int wg = blockIdx.x, pair = blockIdx.y;
     const int H = a.H, W1 = a.W1;
-    const int x1 = wg * CW + c;
-    const bool active = x1 < W1;
-    const bool wave_ragged = wg * CW + wave * LPW + LPW > W1;  // wave-uniform
+    const int nblk = (H + HB - 1) / HB;
+    const bool has_left = wg > 0, has_right = wg + 1 < a.nwg;
+    const uint32_t tag0 = a.epoch << 16;
+    unsigned long long* hopp = a.hop + (size_t)pair * a.hop_pair;
+    auto gbase = [&](int strip, int dir, int b) -> size_t { return ((size_t)(strip * 2 + dir) * nblk + b) * NGR; };
+
+    if (wave == NCW) {
+        // ---- poller: halo snapshots of the neighbouring strips, once per block
+        constexpr int GPL = 2 * NG;            // granules per poller lane (both directions: 2*NGR / 64)
+        const int q0 = lane * GPL;
+        const int dir = q0 / NGR;              // lanes 0-31: A from the left strip, 32-63: B from the right
+        const int r0 = q0 - dir * NGR;         // (kl * VL + g) * NG + t of the publishing wave
+        const int pkl = r0 / (VL * NG);
+        const int g0 = (r0 % (VL * NG)) / NG;  // this lane covers lane slices g0 and g0 + 1
+        const bool need = dir == 0 ? has_left : has_right;
+        const int src_strip = need ? (dir == 0 ? wg - 1 : wg + 1) : wg;
+        const int col = (dir == 0 ? pkl : NCOL - LPW + pkl) + 1;  // LDS column slot
+        bool dead = (a.dbg & 1) != 0;
+        for (int b = 0; b < nblk; b++) {
+#pragma unroll 1
+            for (int j = 0; j < HB; j++) lds_barrier();
+            if (b + 1 < nblk) {
+                if ((has_left || has_right) && !(a.dbg & 2)) {  // wave-uniform
+                    uint32_t v[GPL];
+                    const gu64* src = (const gu64*)(hopp + gbase(src_strip, dir, b) + r0);
+                    poll_granules<GPL>(src, need, tag0 | (uint32_t)(b + 1), v, dead, a.err);
+                    const int wb = (b * HB + HB - 1) & 1;
+                    uint32_t mn = 0xFFFFFFFFu;
+#pragma unroll
+                    for (int t = 0; t < GPL; t++) {
+                        const int g = g0 + t / NG, tt = t % NG;
+                        const int d = g * DPL + 2 * tt;
+                        const uint32_t lo = v[t] & 0xFFFFu, hi = v[t] >> 16;
+                        if (need) {
+                            lv[wb][dir][col][d] = (uint16_t)lo;
+                            if (2 * tt + 1 < DPL) lv[wb][dir][col][d + 1] = (uint16_t)hi;
+                        }
+                        mn = min(mn, lo);
+                        if (2 * tt + 1 < DPL) mn = min(mn, hi);
+                    }
+                    mn = group_min<VL / 2>(mn);  // over the VL/2 poller lanes of one column
+                    if (need && (lane % (VL / 2)) == 0) lmin[wb][dir][col] = mn;
+                }
+                lds_barrier();
+            }
+        }
+        return;
+    }
+
+    // ---- compute waves
+    const int kl = lane / VL, g = lane % VL;
+    const int c = wave * LPW + kl;  // column slot among the compute waves
+    const int x1 = wg * CW + c - LPW;
+    const bool active = x1 >= 0 && x1 < W1;
+    const bool halo_l = wave == 0, halo_r = wave == NCW - 1, own = !halo_l && !halo_r;  // wave-uniform
+    const int wx0 = wg * CW + wave * LPW - LPW;
+    const bool wave_ragged = wx0 < 0 || wx0 + LPW > W1;  // wave-uniform: some column outside [0, W1)
     const uint32_t P1 = (uint32_t)a.P1, P2 = (uint32_t)a.P2;
 
     const uint64_t cells = (uint64_t)H * W1 * D;
     const rsrc_t rc = make_rsrc(a.cost + (size_t)pair * a.cost_pair, cells * sizeof(CT));
-    rsrc_t re = make_rsrc(nullptr, 0), rw = re, rp = re;
+    rsrc_t re = make_rsrc(nullptr, 0), rw = re, rp = re, rrec = re, rnb = re;
     if constexpr (WTA) {
         re = make_rsrc(a.ew + (size_t)pair * a.ew_pair, cells * sizeof(CT));
         rw = make_rsrc(a.ew + (size_t)pair * a.ew_pair + a.ew_slot, cells * sizeof(CT));
+        rrec = make_rsrc(a.rec + (size_t)pair * H * a.W, (uint64_t)H * a.W * 4);
+        rnb = make_rsrc(a.nb + (size_t)pair * H * a.W, (uint64_t)H * a.W * 4);
     }
+    // uniqueness: S*(100-u) < 100*minS  <=>  S < ceil(100*minS / (100-u)) when 100-u > 0
+    const int ku = 100 - a.uniq;
     if constexpr (MODE != 1) rp = make_rsrc((const uint8_t*)a.part + (size_t)pair * a.part_pair, cells * 2);
-    // element offset of this lane's slice in row y
+    const rsrc_t rhop = make_rsrc(hopp, (uint64_t)a.hop_pair * 8);
+    constexpr uint32_t NONE = 0xFFFFFFFFu;
+    // element offset of this lane's slice in row y (cost: every compute wave;
+    // E/W/partial inputs and outputs: own columns only)
     auto cell = [&](int y) -> uint32_t {
-        return active ? ((uint32_t)y * (uint32_t)W1 + (uint32_t)x1) * (uint32_t)D + (uint32_t)(g * DPL) : 0xFFFFFFFFu;
+        return active ? ((uint32_t)y * (uint32_t)W1 + (uint32_t)x1) * (uint32_t)D + (uint32_t)(g * DPL) : NONE;
     };
-    auto boff = [&](uint32_t e, int bytes) -> uint32_t { return e == 0xFFFFFFFFu ? kOOB : e * (uint32_t)bytes; };
-
-    gu64* hop = (gu64*)(a.hop + (size_t)pair * a.hop_pair);
-    auto slot = [&](int strip, int dir, int s) -> size_t {
-        return ((size_t)(strip * 2 + dir) * H + s) * NGR + (size_t)g * NG;
-    };
-    // the edge waves exchange with the neighbouring strips
-    const bool has_left = wg > 0, has_right = wg + 1 < a.nwg;
-    const bool cons_a = wave == 0 && has_left;                  // left halo of A (= SE / NE)
-    const bool cons_b = wave == SW_WAVES - 1 && has_right;      // right halo of B (= SW / NW)
-    const uint32_t tag0 = a.epoch << 16;
-    // publishing: buffer stores (sc1) at an out-of-range offset for every other lane
-    const rsrc_t rhop = make_rsrc(a.hop + (size_t)pair * a.hop_pair, (uint64_t)a.hop_pair * 8);
-    const bool pub_a = wave == SW_WAVES - 1 && has_right && kl == LPW - 1;  // last column -> right strip
-    const bool pub_b = wave == 0 && has_left && kl == 0;                   // first column -> left strip
-    const bool edge_wave = (wave == 0 && has_left) || (wave == SW_WAVES - 1 && has_right);  // wave-uniform
-    bool dead = (a.dbg & 1) != 0;
+    auto boff = [&](uint32_t e, int bytes) -> uint32_t { return e == NONE ? kOOB : e * (uint32_t)bytes; };
 
     uint32_t LV[DPL];
 #pragma unroll
     for (int i = 0; i < DPL; i++) LV[i] = 0;
     uint32_t mV = 0;
 
-    // per-step inputs through a ring of SW_PF rows in flight (the step is
-    // short next to HBM latency under load; one row ahead left every step
-    // waiting for its loads)
-    constexpr int PF = SW_PF;
+    // per-step inputs through a ring of PF rows in flight; every memory
+    // operation of the step loop is issued by every compute wave (masked ones
+    // at out-of-range offsets), so the compiler's counted vmcnt waits hold for
+    // all of them and no wave waits for a load it issued this step
     RawBytes<CB> rc_[PF], re_[PF], rw_[PF];
     RawBytes<DPL * 2> rp_[PF];
     auto issue = [&](int k, int s) {  // loads of step s into ring slot k (rows past the end read 0)
-        const uint32_t en = s < H ? cell(UP ? H - 1 - s : s) : 0xFFFFFFFFu;
+        const uint32_t en = s < H ? cell(UP ? H - 1 - s : s) : NONE;
+        const uint32_t eo = own ? en : NONE;
         rc_[k].load(rc, boff(en, sizeof(CT)));
         if constexpr (WTA) {
-            re_[k].load(re, boff(en, sizeof(CT)));
-            rw_[k].load(rw, boff(en, sizeof(CT)));
+            re_[k].load(re, boff(eo, sizeof(CT)));
+            rw_[k].load(rw, boff(eo, sizeof(CT)));
         }
-        if constexpr (MODE == 2) rp_[k].load(rp, boff(en, 2));
+        if constexpr (MODE == 2) rp_[k].load(rp, boff(eo, 2));
     };
 #pragma unroll
     for (int k = 0; k < PF; k++) issue(k, k);
 
-    for (int s0 = 0; s0 < H; s0 += PF) {
+    for (int b = 0; b < nblk; b++) {
 #pragma unroll
-        for (int k = 0; k < PF; k++) {
-            // whole ring rounds (no early exit: a break here makes the compiler
-            // rotate the ring registers with moves that wait for the newest load);
-            // steps s >= H run masked: out-of-range offsets, no hand-off, no WTA output
-            const int s = s0 + k;
+        for (int j = 0; j < HB; j++) {
+            const int k = j % PF;
+            const int s = b * HB + j;
             const bool live = s < H;
             const int y = UP ? H - 1 - s : s;
             const int rb = (s + 1) & 1, wb = s & 1;
-            const uint32_t e = live ? cell(y) : 0xFFFFFFFFu;
+            const uint32_t e = live ? cell(y) : NONE;
             uint32_t C[DPL];
             unpack_ct<CT, DPL>(rc_[k], C);
             uint32_t Ein[DPL], Win[DPL], Pin[DPL];
@@ -293,174 +365,182 @@ __global__ void __launch_bounds__(256) k_sweep(SweepArgs a)
                 unpack_ct<CT, DPL>(rw_[k], Win);
             }
             if constexpr (MODE == 2) unpack_ct<uint16_t, DPL>(rp_[k], Pin);
-
-            // diagonal predecessors: column c-1 (A) and c+1 (B) of the previous row
-            uint32_t LA[DPL], LB[DPL];
-            lds_get<DPL>(&lv[rb][0][c][g * DPL], LA);
-            lds_get<DPL>(&lv[rb][1][c + 2][g * DPL], LB);
-            uint32_t mA = lmin[rb][0][c], mB = lmin[rb][1][c + 2];
-#ifndef SWEEP_NOPOLL
-            if (s > 0 && live && !(a.dbg & 2)) {
-                if (cons_a) {  // wave 0, column 0 <- last column of strip wg-1
-                    uint32_t v[NG];
-                    poll_granules<NG>(hop + slot(wg - 1, 0, s - 1), kl == 0, tag0 | (uint32_t)s, v, dead, a.err);
-                    uint32_t mn = 0xFFFFFFFFu;
+            // materialise the unpacked values before the slot is refilled: if the
+            // unpack sinks below the refill, old and new slot values overlap and the
+            // ring gets rotated by moves at the back-edge, which wait for the newest loads
 #pragma unroll
-                    for (int i = 0; i < DPL; i++) {
-                        const uint32_t t = (v[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
-                        LA[i] = kl == 0 ? t : LA[i];
-                        mn = min(mn, t);
-                    }
-                    mn = line_min<VL>(mn);
-                    mA = kl == 0 ? mn : mA;
-                }
-                if (cons_b) {  // last wave, last column <- column 0 of strip wg+1
-                    uint32_t v[NG];
-                    poll_granules<NG>(hop + slot(wg + 1, 1, s - 1), kl == LPW - 1, tag0 | (uint32_t)s, v, dead,
-                                      a.err);
-                    uint32_t mn = 0xFFFFFFFFu;
-#pragma unroll
-                    for (int i = 0; i < DPL; i++) {
-                        const uint32_t t = (v[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
-                        LB[i] = kl == LPW - 1 ? t : LB[i];
-                        mn = min(mn, t);
-                    }
-                    mn = line_min<VL>(mn);
-                    mB = kl == LPW - 1 ? mn : mB;
-                }
+            for (int i = 0; i < DPL; i++) {
+                asm volatile("" : "+v"(C[i])::"memory");
+                if constexpr (WTA) asm volatile("" : "+v"(Ein[i]), "+v"(Win[i])::"memory");
+                if constexpr (MODE == 2) asm volatile("" : "+v"(Pin[i])::"memory");
             }
-#endif
-
-            // refill the ring only now: the polls above wait (vmcnt) for every older
-            // load of the wave, so loads issued before them would be waited for too
             issue(k, s + PF);
 
-            uint32_t nA[DPL], nB[DPL];
-            uint32_t mnA = sweep_step<VL, DPL>(LA, mA, C, P1, P2, nA);
-            uint32_t mnB = sweep_step<VL, DPL>(LB, mB, C, P1, P2, nB);
-            if (wave_ragged) {  // columns past W1 stay at the entering state
+            // diagonal predecessors: column c-1 (A) and c+1 (B) of the previous row
+            uint32_t nA[DPL], nB[DPL];  // a halo wave leaves its other direction unset (never read)
+            uint32_t mnA = 0, mnB = 0;
+            if (!halo_r) {
+                uint32_t LA[DPL];
+                lds_get<DPL>(&lv[rb][0][c][g * DPL], LA);
+                mnA = sweep_step<VL, DPL>(LA, lmin[rb][0][c], C, P1, P2, nA);
+                if (wave_ragged) {  // columns outside [0, W1) stay at the entering state
 #pragma unroll
-                for (int i = 0; i < DPL; i++) {
-                    nA[i] = active ? nA[i] : 0u;
-                    nB[i] = active ? nB[i] : 0u;
+                    for (int i = 0; i < DPL; i++) nA[i] = active ? nA[i] : 0u;
+                    mnA = active ? mnA : 0u;
                 }
-                mnA = active ? mnA : 0u;
-                mnB = active ? mnB : 0u;
+                lds_put<DPL>(&lv[wb][0][c + 1][g * DPL], nA);
+                if (g == 0) lmin[wb][0][c + 1] = mnA;
             }
-            // hand the strip-edge columns to the neighbouring strips (sc1 stores by the
-            // edge waves only: every store holds a vmcnt slot of the storing wave)
-            if (edge_wave && live) {
-                const uint32_t tag = tag0 | (uint32_t)(s + 1);
-                const uint32_t oa = pub_a ? (uint32_t)(slot(wg, 0, s) * 8) : kOOB;
-                const uint32_t ob = pub_b ? (uint32_t)(slot(wg, 1, s) * 8) : kOOB;
+            if (!halo_l) {
+                uint32_t LB[DPL];
+                lds_get<DPL>(&lv[rb][1][c + 2][g * DPL], LB);
+                mnB = sweep_step<VL, DPL>(LB, lmin[rb][1][c + 2], C, P1, P2, nB);
+                if (wave_ragged) {
 #pragma unroll
-                for (int q = 0; q < NG; q++) {
-                    const uint32_t va = nA[2 * q] | (2 * q + 1 < DPL ? nA[2 * q + 1] << 16 : 0u);
-                    const uint32_t vb = nB[2 * q] | (2 * q + 1 < DPL ? nB[2 * q + 1] << 16 : 0u);
-                    __builtin_amdgcn_raw_buffer_store_b64(u32x2{va, tag}, rhop, oa + 8 * q, 0, 16);
-                    __builtin_amdgcn_raw_buffer_store_b64(u32x2{vb, tag}, rhop, ob + 8 * q, 0, 16);
+                    for (int i = 0; i < DPL; i++) nB[i] = active ? nB[i] : 0u;
+                    mnB = active ? mnB : 0u;
                 }
+                lds_put<DPL>(&lv[wb][1][c + 1][g * DPL], nB);
+                if (g == 0) lmin[wb][1][c + 1] = mnB;
             }
-            lds_put<DPL>(&lv[wb][0][c + 1][g * DPL], nA);
-            lds_put<DPL>(&lv[wb][1][c + 1][g * DPL], nB);
-            if (g == 0) {
-                lmin[wb][0][c + 1] = mnA;
-                lmin[wb][1][c + 1] = mnB;
-            }
-
-            uint32_t nV[DPL];
-            const uint32_t mnV = sweep_step<VL, DPL>(LV, mV, C, P1, P2, nV);
+            // snapshot of the block's last row for the neighbouring strips' halos
+            if (j == HB - 1 && b + 1 < nblk) {
+                const bool pa = wave == NCW - 2 && has_right, pb = wave == 1 && has_left;  // wave-uniform
+                if (pa || pb) {
+                    const uint32_t tag = tag0 | (uint32_t)(b + 1);
+                    const uint32_t o = (uint32_t)((gbase(wg, pa ? 0 : 1, b) + (size_t)(kl * VL + g) * NG) * 8);
 #pragma unroll
-            for (int i = 0; i < DPL; i++) LV[i] = nV[i];
-            mV = mnV;
-
-            if constexpr (MODE == 0) {
-                uint32_t sum[DPL];
-#pragma unroll
-                for (int i = 0; i < DPL; i++) sum[i] = nV[i] + nA[i] + nB[i];
-                bstore_n<uint16_t, DPL>(rp, boff(e, 2), sum);
-            } else {
-                uint32_t S[DPL];
-                uint32_t key = 0xFFFFFFFFu;
-#pragma unroll
-                for (int i = 0; i < DPL; i++) {
-                    uint32_t t = nV[i] + nA[i] + nB[i] + Ein[i] + Win[i];
-                    if constexpr (MODE == 2) t += Pin[i];
-                    S[i] = min(t, 32767u);
-                    key = min(key, (S[i] << 16) | (uint32_t)(g * DPL + i));
-                }
-                key = line_min<VL>(key);
-                const int minS = (int)(key >> 16), best = (int)(key & 0xFFFF);
-                const int u = a.uniq;
-                uint32_t bad = 0, nb = 0;
-#pragma unroll
-                for (int i = 0; i < DPL; i++) {
-                    const int d = g * DPL + i;
-                    const int dd = best - d;
-                    bad |= ((int)S[i] * (100 - u) < minS * 100 && (dd > 1 || dd < -1)) ? 1u : 0u;
-                    nb |= d == best - 1 ? S[i] : 0u;
-                    nb |= d == best + 1 ? (S[i] << 16) : 0u;
-                }
-                bad = line_or<VL>(bad);
-                nb = line_or<VL>(nb);
-                if (g == 0 && active && live) {
-                    const int X = x1 + a.minX1;
-                    int d1 = (a.minD - 1) * 16;
-                    if (!bad && minS < 32767) {
-                        const int x2 = X - best - a.minD;
-                        atomicMin(a.key2 + ((size_t)pair * H + y) * a.W + x2,
-                                  ((uint32_t)minS << 16) | (uint32_t)(0xFFFF - X));
-                        int d16;
-                        if (best > 0 && best < D - 1) {
-                            const int Sm = (int)(nb & 0xFFFF), Sq = (int)(nb >> 16);
-                            const int den = max(Sm + Sq - 2 * minS, 1);
-                            d16 = best * 16 + ((Sm - Sq) * 16 + den) / (den * 2);  // C truncation
-                        } else {
-                            d16 = best * 16;
-                        }
-                        d1 = d16 + a.minD * 16;
+                    for (int q = 0; q < NG; q++) {
+                        const uint32_t lo = pa ? nA[2 * q] : nB[2 * q];
+                        const uint32_t hi = 2 * q + 1 < DPL ? (pa ? nA[2 * q + 1] : nB[2 * q + 1]) : 0u;
+                        __builtin_amdgcn_raw_buffer_store_b64(u32x2{lo | (hi << 16), tag}, rhop, o + 8 * q, 0, 16);
                     }
-                    a.disp[((size_t)pair * H + y) * a.W + X] = (int16_t)d1;
                 }
+            }
+
+            uint32_t out[DPL];  // MODE 0: partial sum of the three directions
+#pragma unroll
+            for (int i = 0; i < DPL; i++) out[i] = 0;
+            uint32_t recw = 0, nbw = 0;
+            bool wpx = false;
+            if (own) {
+                uint32_t nV[DPL];
+                const uint32_t mnV = sweep_step<VL, DPL>(LV, mV, C, P1, P2, nV);
+#pragma unroll
+                for (int i = 0; i < DPL; i++) LV[i] = nV[i];
+                mV = mnV;
+                if constexpr (MODE == 0) {
+#pragma unroll
+                    for (int i = 0; i < DPL; i++) out[i] = nV[i] + nA[i] + nB[i];
+                } else {
+                    uint32_t S[DPL];
+                    uint32_t key = 0xFFFFFFFFu;
+#pragma unroll
+                    for (int i = 0; i < DPL; i++) {
+                        uint32_t t = nV[i] + nA[i] + nB[i] + Ein[i] + Win[i];
+                        if constexpr (MODE == 2) t += Pin[i];
+                        if constexpr (sizeof(CT) == 2) t = min(t, 32767u);  // census sums stay below 2^11
+                        S[i] = t;
+                        key = min(key, (t << 16) | (uint32_t)(g * DPL + i));
+                    }
+                    lds_put<DPL>(&srow[(wave - 1) % (NCW - 2)][kl][g * DPL], S);
+                    key = group_min<VL>(key);
+                    const uint32_t minS = key >> 16;
+                    const int best = (int)(key & 0xFFFF);
+                    // far entries (|d - best| > 1) below the uniqueness threshold
+                    uint32_t far = 0;
+                    const int gb = g * DPL - best + 1;  // d - best + 1 of element 0
+                    if (ku > 0) {
+                        const uint32_t T = (100u * minS + (uint32_t)ku - 1u) / (uint32_t)ku;
+#pragma unroll
+                        for (int i = 0; i < DPL; i++) far = max(far, S[i] < T ? (uint32_t)(gb + i) : 0u);
+                    } else {  // uniquenessRatio >= 100: the product form (rare)
+#pragma unroll
+                        for (int i = 0; i < DPL; i++)
+                            far = max(far, (int)S[i] * ku < (int)minS * 100 ? (uint32_t)(gb + i) : 0u);
+                    }
+                    far = group_max<VL>(far);
+                    const bool ok = far <= 2u && minS < 32767u;
+                    const int bm = max(best - 1, 0), bq = min(best + 1, D - 1);
+                    const uint32_t Sm = srow[(wave - 1) % (NCW - 2)][kl][bm];
+                    const uint32_t Sq = srow[(wave - 1) % (NCW - 2)][kl][bq];
+                    // disp2 candidate / sub-pixel inputs for k_lr_rows (~0: rejected)
+                    recw = ok ? ((minS << 16) | (uint32_t)best) : 0xFFFFFFFFu;
+                    nbw = Sm | (Sq << 16);
+                    wpx = g == 0 && active && live;
+                }
+            }
+            if constexpr (MODE == 0) {
+                bstore_n<uint16_t, DPL>(rp, own ? boff(e, 2) : kOOB, out);
+            } else {
+                const uint32_t px = (uint32_t)y * (uint32_t)a.W + (uint32_t)(x1 + a.minX1);
+                __builtin_amdgcn_raw_buffer_store_b32(recw, rrec, wpx ? px * 4 : kOOB, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b32(nbw, rnb, wpx ? px * 4 : kOOB, 0, 0);
             }
             lds_barrier();
         }
+        if (b + 1 < nblk) lds_barrier();  // the poller has written the halo snapshot
     }
 }
 
 #if !defined(SWEEP_MODE) || SWEEP_MODE == 0  // one unit owns the non-template kernel
-// LR consistency (disp12MaxDiff) against the disp2 keys of the whole row:
-// same test as k_wta's tail (sm_paths.hpp); columns outside [minX1, maxX1)
-// are INVALID.  blockIdx = (x tile, y, pair).
-__global__ void __launch_bounds__(256) k_lr_check(const int16_t* __restrict__ pre, const uint32_t* __restrict__ key2,
-                                                  int16_t* __restrict__ out, int H, int W, int minD, int minX1, int maxX1,
-                                                  int disp12)
+// Winner's sub-pixel value, disp2 (right-view argmin, cv::StereoSGBM's
+// disp2/disp2cost) and the disp12MaxDiff check from the WTA sweep's per-pixel
+// records: the tail of k_wta (sm_paths.hpp) over one row per workgroup.
+// rec = minS << 16 | best (~0: rejected by the uniqueness test or saturated),
+// nb = S[best-1] | S[best+1] << 16.  Columns outside [minX1, maxX1) are
+// INVALID.  blockIdx = (y, pair); dynamic LDS = 4*W bytes (disp2 keys) + 2*W
+// (the row's sub-pixel disparities).
+__global__ void __launch_bounds__(256) k_lr_rows(const uint32_t* __restrict__ rec, const uint32_t* __restrict__ nbs,
+                                                 int16_t* __restrict__ out, int H, int W, int D, int minD, int minX1,
+                                                 int maxX1, int disp12)
 {
-    const int X = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
-    if (X >= W) return;
-    const size_t row = ((size_t)blockIdx.z * H + y) * W;
+    extern __shared__ uint32_t key2[];
+    int16_t* drow = reinterpret_cast<int16_t*>(key2 + W);
+    const int y = blockIdx.x;
+    const size_t row = ((size_t)blockIdx.y * H + y) * W;
     const int INVALID = (minD - 1) * 16;
-    int d1 = INVALID;
-    if (X >= minX1 && X < maxX1) {
-        d1 = pre[row + X];
-        if (d1 != INVALID) {
+    for (int X = threadIdx.x; X < W; X += 256) {
+        key2[X] = 0xFFFFFFFFu;
+        drow[X] = (int16_t)INVALID;
+    }
+    __syncthreads();
+    for (int X = minX1 + (int)threadIdx.x; X < maxX1; X += 256) {
+        const uint32_t r = rec[row + X];
+        if (r != 0xFFFFFFFFu) {
+            const int best = (int)(r & 0xFFFF), minS = (int)(r >> 16);
+            atomicMin(&key2[X - best - minD], (r & 0xFFFF0000u) | (uint32_t)(0xFFFF - X));
+            int d16 = best * 16;
+            if (best > 0 && best < D - 1) {
+                const uint32_t nb = nbs[row + X];
+                const int Sm = (int)(nb & 0xFFFF), Sq = (int)(nb >> 16);
+                const int den = max(Sm + Sq - 2 * minS, 1);
+                d16 += ((Sm - Sq) * 16 + den) / (den * 2);  // C truncation
+            }
+            drow[X] = (int16_t)(d16 + minD * 16);
+        }
+    }
+    __syncthreads();
+    for (int X = threadIdx.x; X < W; X += 256) {
+        int d1 = drow[X];
+        if (X >= minX1 && X < maxX1 && d1 != INVALID) {
             const int _d = d1 >> 4, d_ = (d1 + 15) >> 4;
             const int _x = X - _d, x_ = X - d_;
             bool rej1 = false, rej2 = false;
             if (_x >= 0 && _x < W) {
-                const uint32_t kk = key2[row + _x];
+                const uint32_t kk = key2[_x];
                 const int d2 = kk == 0xFFFFFFFFu ? INVALID : (int)(0xFFFF - (kk & 0xFFFF)) - _x;
                 rej1 = d2 >= minD && abs(d2 - _d) > disp12;
             }
             if (x_ >= 0 && x_ < W) {
-                const uint32_t kk = key2[row + x_];
+                const uint32_t kk = key2[x_];
                 const int d2 = kk == 0xFFFFFFFFu ? INVALID : (int)(0xFFFF - (kk & 0xFFFF)) - x_;
                 rej2 = d2 >= minD && abs(d2 - d_) > disp12;
             }
             if (rej1 && rej2) d1 = INVALID;
         }
+        out[row + X] = (int16_t)d1;
     }
-    out[row + X] = (int16_t)d1;
 }
 #endif
 

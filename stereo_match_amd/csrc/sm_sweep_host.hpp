@@ -15,22 +15,24 @@ struct SweepArgs {
     size_t ew_pair, ew_slot;
     uint16_t* part;  // [pair][H][W1][D] u16 partial (written by MODE 0, read by MODE 2)
     size_t part_pair;  // bytes
-    unsigned long long* hop;  // boundary granules [pair][nwg][2][H][NGR]
+    unsigned long long* hop;  // halo snapshot granules [pair][nwg][2][nblk][NGR]
     size_t hop_pair;          // granules per pair
-    uint32_t* key2;  // [pair][H][W] disp2 keys (minS << 16 | 0xFFFF - X), preset to ~0
-    int16_t* disp;   // [pair][H][W] WTA output before the LR check (domain columns only)
-    uint32_t* err;   // bit 0: a boundary poll timed out
+    uint32_t* rec;   // [pair][H][W] WTA winners (minS << 16 | best, ~0 rejected), domain columns only
+    uint32_t* nb;    // [pair][H][W] S[best-1] | S[best+1] << 16 (sub-pixel inputs)
+    uint32_t* err;   // bit 0: a halo poll timed out
     int H, W, W1, D, minD, minX1, P1, P2, uniq;
     int nwg;
     uint32_t epoch;  // 1..65535, distinct from the previous launches on the same hop buffer
-    int dbg;         // timing ablations only: 1 no waiting in the boundary polls, 2 no polls
+    int dbg;         // timing ablations only: 1 no waiting in the halo polls, 2 no polls
 };
 
 
 struct SweepInfo {
-    int cw;             // columns per workgroup (strip width)
-    int ngr;            // boundary granules per (strip, direction, row)
-    int blocks_per_cu;  // occupancy API answer for 256-thread blocks
+    int cw;             // own columns per workgroup (strip width)
+    int hb;             // rows per halo block
+    int ngr;            // halo granules per (strip, direction, block)
+    int threads;        // threads per workgroup
+    int blocks_per_cu;  // occupancy API answer for that block size
 };
 
 template <typename CT, int MODE, class F>
@@ -40,7 +42,7 @@ hipError_t with_d(int D, F& f);
 hipError_t sweep_info_m0(int D, int ct_bytes, int device, SweepInfo* out);
 hipError_t sweep_info_m1(int D, int ct_bytes, int device, SweepInfo* out);
 hipError_t sweep_info_m2(int D, int ct_bytes, int device, SweepInfo* out);
-// grid (a.nwg, npairs), 256 threads
+// grid (a.nwg, npairs), SweepInfo::threads threads
 hipError_t sweep_launch_m0(int D, int ct_bytes, const SweepArgs& a, int npairs, hipStream_t stream);
 hipError_t sweep_launch_m1(int D, int ct_bytes, const SweepArgs& a, int npairs, hipStream_t stream);
 hipError_t sweep_launch_m2(int D, int ct_bytes, const SweepArgs& a, int npairs, hipStream_t stream);
@@ -57,7 +59,8 @@ inline hipError_t sweep_launch(int D, int ct_bytes, int mode, const SweepArgs& a
          : mode == 1 ? sweep_launch_m1(D, ct_bytes, a, npairs, stream)
                      : sweep_launch_m2(D, ct_bytes, a, npairs, stream);
 }
-hipError_t lr_check_launch(const int16_t* pre, const uint32_t* key2, int16_t* out, int G, int H, int W, int minD,
-                           int minX1, int maxX1, int disp12, hipStream_t stream);
+// sub-pixel + disp2 + disp12MaxDiff check from the WTA sweep's records, one row per workgroup
+hipError_t lr_rows_launch(const uint32_t* rec, const uint32_t* nb, int16_t* out, int G, int H, int W, int D, int minD,
+                          int minX1, int maxX1, int disp12, hipStream_t stream);
 
 }  // namespace smk
