@@ -43,6 +43,9 @@ def parse():
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--row", action="store_true",
                     help="experimental fused row kernel (E/W paths + WTA) instead of k_wta (D %% 64 == 0)")
+    ap.add_argument("--engine", default="auto", choices=["auto", "perdir", "sweep"],
+                    help="auto: fused sweeps for 5 paths, per-direction volumes for 8 paths (measured faster); "
+                         "perdir / sweep force one engine (DESIGN.md §4)")
     ap.add_argument("--cpu-baseline-pairs", type=int, default=8,
                     help="pairs timed on the host C port per thread (rank 0, N=1 only); 0 = skip")
     ap.add_argument("--cpu-threads", type=int, default=16,
@@ -111,8 +114,10 @@ def main():
     eng = _lib.Engine(local_rank)
     stream = torch.cuda.current_stream(dev)
     eng.set_stream(stream.cuda_stream)
-    if args.row:
-        eng.set_debug_flags(32)
+    flags = 32 if args.row else 0
+    flags |= {"auto": 0, "perdir": 4096, "sweep": 16384}[args.engine]
+    if flags:
+        eng.set_debug_flags(flags)
 
     def step():
         if full:
@@ -186,8 +191,17 @@ def main():
         kern = {"paths": ("k_sgm_paths (vertical family)" if row_mode else "k_sgm_paths (all directions)",
                           paths_bytes),
                 "wta": (wta_name, wta_bytes)}
-        # dominant kernel = the stage with the larger device time
-        dom = max(("paths", "wta"), key=lambda k: stages[k][0])
+        cands = ("paths", "wta")
+        if stages["sweep_wta"][1] > 0:  # fused-sweep engine (sm_sweep.hpp): its kernels have stages of their own
+            rec_b = 8 * H * width1  # WTA winner record + sub-pixel inputs per pixel
+            kern = {"horizontal": ("k_sgm_paths (E/W lines only)", 4 * vol * eb),
+                    "sweep": ("k_sweep down (S+SE+SW -> u16 partial)", vol * eb + 2 * vol),
+                    "sweep_wta": ("k_sweep " + ("up (N+NE+NW" if P_dirs == 8 else "down (S+SE+SW")
+                                  + " + E + W" + (" + partial" if P_dirs == 8 else "") + " + WTA)",
+                                  3 * vol * eb + (2 * vol if P_dirs == 8 else 0) + rec_b)}
+            cands = tuple(k for k in ("horizontal", "sweep", "sweep_wta") if stages[k][1] > 0)
+        # dominant kernel = the stage with the largest device time
+        dom = max(cands, key=lambda k: stages[k][0])
         dom_ms, dom_launches, dom_pairs = stages[dom]
         paths_avg_s = dom_ms / 1e3 / max(dom_launches, 1)
         pairs_per_launch = dom_pairs / max(dom_launches, 1)
@@ -235,6 +249,8 @@ def main():
             "data": "synthetic random-dot pairs (no dataset in the image)"
                     + ("; f32 cost = 3x3-smoothed |L-R|/255 volume per pair" if volume else ""),
             "config": {
+                "engine": {"auto": "sweeps (5 paths) / per-direction (8 paths)", "perdir": "per-direction",
+                           "sweep": "fused sweeps"}[args.engine],
                 "workload": f"{args.config} {W}x{H} D={D} "
                             + {"census8": "census9x7 + 8-path SGM", "sgbm5": "OpenCV-SGBM 5-path",
                                "volume8": "f32 cost volume (mc-cnn) + 8-path SGM",

@@ -27,7 +27,12 @@ hipError_t with_d(int D, F& f)
     case d: return f.template run<8, d / 8, CT, MODE>();
 #define SW16(d) \
     case d: return f.template run<16, d / 16, CT, MODE>();
-        SW8(16) SW8(32) SW8(48) SW8(64) SW16(80) SW16(96) SW16(112) SW16(128)
+        SW8(16) SW8(32) SW8(48) SW8(64) SW16(80) SW16(96) SW16(112)
+#ifdef SWEEP_VL8_128
+        SW8(128)
+#else
+        SW16(128)
+#endif
         SW16(144) SW16(160) SW16(176) SW16(192) SW16(208) SW16(224) SW16(240) SW16(256)
 #undef SW8
 #undef SW16

@@ -24,8 +24,13 @@ for k, d in vals.items():
     wr = ws * 1024 if ws is not None else None
     summary["kernels"][k] = {"fetch_size_kb": fs, "write_size_kb": ws, "read_bytes_corrected": rd,
                              "write_bytes": wr, "hbm_bytes": (rd or 0) + (wr or 0)}
-    stage = ("paths" if "k_sgm_paths" in k else "wta" if ("k_wta" in k or "k_row_wta" in k)
-             else "cost" if any(c in k for c in ("k_census9x7", "k_sgbm_cost(", "k_cost_volume_f32")) else None)
+    sweep = any("k_sweep" in n for n in vals)  # fused-sweep engine: k_sgm_paths runs the E/W lines only
+    if "k_sweep" in k:  # template argument list ends with the sweep mode (0 = down partial, 1/2 = with WTA)
+        stage = "sweep" if k.split(">")[0].rstrip().endswith(" 0") else "sweep_wta"
+    else:
+        stage = (("horizontal" if sweep else "paths") if "k_sgm_paths" in k
+                 else "wta" if ("k_wta" in k or "k_row_wta" in k)
+                 else "cost" if any(c in k for c in ("k_census9x7", "k_sgbm_cost(", "k_cost_volume_f32")) else None)
     if stage:
         summary.setdefault("stages", {})[stage] = {"kernel": k, "hbm_bytes_per_launch": (rd or 0) + (wr or 0),
                                                    "read_bytes": rd, "write_bytes": wr}
