@@ -116,6 +116,7 @@ __device__ __forceinline__ uint32_t sweep_step(const uint32_t (&Lp)[DPL], uint32
     return group_min<VL>(mn);
 }
 
+
 // DPL u16 values of one lane in LDS (little-endian pairs), widest aligned chunks
 template <int DPL>
 __device__ __forceinline__ void lds_put(uint16_t* p, const uint32_t (&v)[DPL])
@@ -312,8 +313,7 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL>::THREADS)) k_sweep(SweepArg
         rrec = make_rsrc(a.rec + (size_t)pair * H * a.W, (uint64_t)H * a.W * 4);
         rnb = make_rsrc(a.nb + (size_t)pair * H * a.W, (uint64_t)H * a.W * 4);
     }
-    // uniqueness: S*(100-u) < 100*minS  <=>  S < ceil(100*minS / (100-u)) when 100-u > 0
-    const int ku = 100 - a.uniq;
+    const int ku = 100 - a.uniq;  // uniqueness: S*(100-u) < 100*minS
     if constexpr (MODE != 1) rp = make_rsrc((const uint8_t*)a.part + (size_t)pair * a.part_pair, cells * 2);
     const rsrc_t rhop = make_rsrc(hopp, (uint64_t)a.hop_pair * 8);
     constexpr uint32_t NONE = 0xFFFFFFFFu;
@@ -450,10 +450,11 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL>::THREADS)) k_sweep(SweepArg
                     // far entries (|d - best| > 1) below the uniqueness threshold
                     uint32_t far = 0;
                     const int gb = g * DPL - best + 1;  // d - best + 1 of element 0
-                    if (ku > 0) {
-                        const uint32_t T = (100u * minS + (uint32_t)ku - 1u) / (uint32_t)ku;
+                    if (ku > 0) {  // S, minS < 2^15, ku <= 100: 24-bit multiplies are exact (full rate)
+                        const uint32_t lim = __umul24(minS, 100u);
 #pragma unroll
-                        for (int i = 0; i < DPL; i++) far = max(far, S[i] < T ? (uint32_t)(gb + i) : 0u);
+                        for (int i = 0; i < DPL; i++)
+                            far = max(far, __umul24(S[i], (uint32_t)ku) < lim ? (uint32_t)(gb + i) : 0u);
                     } else {  // uniquenessRatio >= 100: the product form (rare)
 #pragma unroll
                         for (int i = 0; i < DPL; i++)
