@@ -263,8 +263,12 @@ long long sm_debug_fetch(sm_ctx* ctx, int what, void* host, size_t bytes);
  * instead of reading the precomputed u8 cost volume, bit 11 only in the
  * horizontal family; bit 12 (valid results) uses the per-direction engine
  * (one path volume per direction + WTA kernel) instead of the fused sweeps,
- * so that sm_debug_fetch(1) has every direction; bits 16-19: launch-group
- * size cap (0 = none).
+ * so that sm_debug_fetch(1) has every direction; bit 13 (valid results) one
+ * pair per fused-sweep launch; bit 14 (valid results) the fused sweeps for 8
+ * paths too; bit 15 (valid results, 8 paths) the hybrid engine: the down
+ * sweep on a second stream beside a per-direction launch of the other five
+ * directions; bits 16-19: launch-group size cap (0 = none); bits 24-27:
+ * fused-sweep timing ablations (results become wrong).
  * 0 = normal operation. */
 int sm_set_debug_flags(sm_ctx* ctx, int flags);
 

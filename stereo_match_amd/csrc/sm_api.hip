@@ -68,7 +68,7 @@ struct BufSet {
 // debug flags (sm_set_debug_flags); 1 skip horizontal, 2 skip vertical and 4 drop stores are read in-kernel
 constexpr int DBG_VL16 = 8, DBG_STORE_W = 16, DBG_ROW = 32, DBG_OVERLAP = 64, DBG_H64 = 512, DBG_NO_C8 = 1024;
 // 4096: per-direction engine (one path volume per direction + k_wta) instead of the fused sweeps
-constexpr int DBG_LEGACY = 4096, DBG_SWEEP1 = 8192, DBG_SWEEP8 = 16384;
+constexpr int DBG_LEGACY = 4096, DBG_SWEEP1 = 8192, DBG_SWEEP8 = 16384, DBG_HYBRID = 32768;
 
 }  // namespace
 
@@ -243,6 +243,7 @@ size_t elem_bytes(const Norm& n) { return n.cost == SM_COST_CENSUS ? 1 : 2; }  /
 // Output slots: 0 E, 1 W (horizontal family), 2 SE, 3 S, 4 SW (MODE_SGBM adds
 // these three), 5 NE, 6 N, 7 NW (MODE_HH / 8-path adds these three).
 const int kVdx[6] = {1, 0, -1, 1, 0, -1};
+enum { DIRS_ALL = 0, DIRS_EW = 1, DIRS_EW_UP = 2 };
 const int kVdy[6] = {1, 1, 1, -1, -1, -1};
 
 constexpr size_t kSetBudget = size_t(12) << 30;  // bytes of path volumes per buffer set
@@ -268,7 +269,8 @@ struct Src {  // where a launch group's pairs come from (device pointers)
 struct Geo {  // per-group geometry shared by the launches
     int H, W, stride, G;
     size_t vol, slot_bytes, L_pair, census_pair, cost_pair;
-    bool sweep;  // fused-sweep engine (sm_sweep.hpp) instead of per-direction volumes
+    bool sweep;   // fused-sweep engine (sm_sweep.hpp) instead of per-direction volumes
+    bool hybrid;  // 8 paths: down sweep (u16 partial) beside a per-direction launch of E, W, NE, N, NW
 };
 
 bool row_mode(const sm_ctx* ctx, const Norm& n) { return (ctx->dbg_flags & DBG_ROW) && n.D % 64 == 0; }
@@ -284,7 +286,7 @@ hipStream_t stream_b(const sm_ctx* ctx) { return overlap(ctx) ? ctx->side : ctx-
 
 // ---- stream A: path aggregation -------------------------------------------
 template <int DPLV, bool CENSUS, int VL, bool H16 = false>
-int launch_paths_t(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs, bool horiz_only)
+int launch_paths_t(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs, int dirset)
 {
     using LT = typename std::conditional<CENSUS, uint8_t, uint16_t>::type;
     constexpr int D = 16 * DPLV;
@@ -316,21 +318,31 @@ int launch_paths_t(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs, bool ho
     pa.dbg = ctx->dbg_flags;
     const int lines_per_wg = 4 * (64 / LANESH);
     pa.hblocks = row_mode(ctx, n) ? 0 : (g.H + lines_per_wg - 1) / lines_per_wg;
-    pa.nv = horiz_only ? 0 : n.ndirs - 2;  // sweep engine: E and W only
+    // DIRS_ALL: every direction; DIRS_EW: E and W only (sweep engine); DIRS_EW_UP:
+    // E, W and the up family NE, N, NW (hybrid engine, slots 2..4)
+    pa.nv = dirset == DIRS_ALL ? n.ndirs - 2 : dirset == DIRS_EW ? 0 : 3;
+    const int k0 = dirset == DIRS_EW_UP ? 3 : 0;
     int blocks = 0;
     constexpr int LPWV = 64 / VL;
     for (int k = 0; k < pa.nv; k++) {
-        pa.v_dx[k] = kVdx[k];
-        pa.v_dy[k] = kVdy[k];
+        const int dx = kVdx[k0 + k];
+        pa.v_dx[k] = dx;
+        pa.v_dy[k] = kVdy[k0 + k];
         pa.v_slot[k] = 2 + k;
-        pa.v_line_lo[k] = kVdx[k] > 0 ? -(g.H - 1) : 0;
-        pa.v_nlines[k] = kVdx[k] == 0 ? n.width1 : n.width1 + g.H - 1;
+        pa.v_line_lo[k] = dx > 0 ? -(g.H - 1) : 0;
+        pa.v_nlines[k] = dx == 0 ? n.width1 : n.width1 + g.H - 1;
         pa.v_blk_start[k] = blocks;
         // waves come in groups of 8 covering 8*LPW lines (lines w + 8*kl)
         blocks += ((pa.v_nlines[k] + 8 * LPWV - 1) / (8 * LPWV)) * 2;
     }
     for (int k = pa.nv; k <= 6; k++) pa.v_blk_start[k] = blocks;
-    StageTimer t(ctx, ctx->stream, horiz_only ? SM_STAGE_HORIZONTAL : SM_STAGE_PATHS, g.G);
+    if (pa.dbg & (1 << 21)) {  // interleaved directions: every direction padded to the largest count
+        int mx = 0;
+        for (int k = 0; k < pa.nv; k++) mx = std::max(mx, pa.v_blk_start[k + 1] - pa.v_blk_start[k]);
+        blocks = mx * pa.nv;
+    }
+    if (g.G % 8) pa.dbg &= ~(1 << 20);  // XCD-aware pair mapping needs whole XCD rounds
+    StageTimer t(ctx, ctx->stream, dirset == DIRS_EW ? SM_STAGE_HORIZONTAL : SM_STAGE_PATHS, g.G);
     hipLaunchKernelGGL((smk::k_sgm_paths<VL, DPLV * 16 / VL, LANESH, DPLH, CENSUS, LT>),
                        dim3(2 * pa.hblocks + blocks, g.G), dim3(256), 0, ctx->stream, pa);
     HIP_TRY(ctx, hipGetLastError());
@@ -380,7 +392,9 @@ int launch_wta_t(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs)
     wa.L = (const uint8_t*)bs.L.p;
     wa.slot_bytes = g.slot_bytes;
     wa.L_pair_bytes = g.L_pair;
-    wa.nslots = n.ndirs;
+    wa.nslots = g.hybrid ? 5 : n.ndirs;
+    wa.part = g.hybrid ? (const uint16_t*)bs.part.p : nullptr;  // hybrid: S + SE + SW partial
+    wa.part_pair = g.vol;
     wa.H = g.H;
     wa.W = g.W;
     wa.width1 = n.width1;
@@ -396,30 +410,30 @@ int launch_wta_t(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs)
 }
 
 template <int DPLV, bool CENSUS>
-int launch_paths_dpl(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs, bool horiz_only)
+int launch_paths_dpl(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs, int dirset)
 {
     // horizontal lines: 16 lanes (4 rows per wave); 64-lane lines (one row per
     // wave, the round-1 layout for D % 64 == 0) with the ablation flag
     if constexpr ((16 * DPLV) % 64 == 0) {
         if (ctx->dbg_flags & DBG_H64) {
             if (DPLV == 8 && !(ctx->dbg_flags & DBG_VL16))
-                return launch_paths_t<DPLV, CENSUS, 8>(ctx, n, g, bs, horiz_only);
-            return launch_paths_t<DPLV, CENSUS, 16>(ctx, n, g, bs, horiz_only);
+                return launch_paths_t<DPLV, CENSUS, 8>(ctx, n, g, bs, dirset);
+            return launch_paths_t<DPLV, CENSUS, 16>(ctx, n, g, bs, dirset);
         }
     }
     // 8-lane vertical lines at D = 128 (16-lane with the ablation flag)
     if constexpr (DPLV == 8) {
-        if (!(ctx->dbg_flags & DBG_VL16)) return launch_paths_t<DPLV, CENSUS, 8, true>(ctx, n, g, bs, horiz_only);
+        if (!(ctx->dbg_flags & DBG_VL16)) return launch_paths_t<DPLV, CENSUS, 8, true>(ctx, n, g, bs, dirset);
     }
-    return launch_paths_t<DPLV, CENSUS, 16, true>(ctx, n, g, bs, horiz_only);
+    return launch_paths_t<DPLV, CENSUS, 16, true>(ctx, n, g, bs, dirset);
 }
 
-enum { DISPATCH_PATHS = 0, DISPATCH_WTA = 1, DISPATCH_HORIZONTAL = 2 };
+enum { DISPATCH_PATHS = 0, DISPATCH_WTA = 1, DISPATCH_HORIZONTAL = 2, DISPATCH_HYBRID = 3 };
 
 int dispatch(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs, int what)
 {
     const bool census = n.cost == SM_COST_CENSUS;
-    const bool h = what == DISPATCH_HORIZONTAL;
+    const int h = what == DISPATCH_HORIZONTAL ? DIRS_EW : what == DISPATCH_HYBRID ? DIRS_EW_UP : DIRS_ALL;
     switch (n.dpl) {
 #define CASE(k)                                                                                               \
     case k:                                                                                                   \
@@ -435,6 +449,18 @@ int dispatch(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs, int what)
 
 // ---- fused-sweep engine (sm_sweep.hpp) -----------------------------------------
 int ensure_event(sm_ctx* ctx, hipEvent_t& e);
+bool use_sweep(const sm_ctx* ctx, const Norm& n, int H);
+
+// 8 paths: the down sweep (S + SE + SW -> one u16 partial, VALU-bound) runs on
+// the side stream beside ONE per-direction launch of E, W, NE, N, NW
+// (HBM-bound); k_wta then sums 5 volumes + the partial (21 instead of 25 B/cell)
+bool use_hybrid(const sm_ctx* ctx, const Norm& n, int H)
+{
+    if (n.ndirs != 8 || !(ctx->dbg_flags & DBG_HYBRID) || (ctx->dbg_flags & (DBG_LEGACY | DBG_SWEEP8))) return false;
+    sm_ctx tmp = *ctx;
+    tmp.dbg_flags = (ctx->dbg_flags & ~DBG_HYBRID) | DBG_SWEEP8;  // same preconditions as the sweeps
+    return use_sweep(&tmp, n, H);
+}
 
 bool use_sweep(const sm_ctx* ctx, const Norm& n, int H)
 {
@@ -583,6 +609,38 @@ int run_sweep(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs)
     return SM_OK;
 }
 
+// hybrid 8-path aggregation (see use_hybrid); leaves per-direction slots 0..4 and bs.part for k_wta
+int run_hybrid(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs)
+{
+    const int G = g.G;
+    int rc;
+    SweepJob j{};
+    j.cost = (const uint8_t*)bs.cost.p;
+    j.cost_pair = g.vol * elem_bytes(n);
+    j.G = G;
+    if ((rc = ensure(ctx, bs.part, (size_t)G * g.vol * 2)) != SM_OK) return rc;
+    j.part = (uint16_t*)bs.part.p;
+    j.part_pair = g.vol * 2;
+    if ((rc = ensure_event(ctx, ctx->ev_fork)) != SM_OK) return rc;
+    if ((rc = ensure_event(ctx, ctx->ev_join)) != SM_OK) return rc;
+    StageTimer t(ctx, ctx->stream, SM_STAGE_PATHS, G);
+    // the sweep first (its strips must become co-resident), then the per-direction launch
+    HIP_TRY(ctx, hipEventRecord(ctx->ev_fork, ctx->stream));
+    HIP_TRY(ctx, hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
+    const hipStream_t main = ctx->stream;
+    ctx->stream = ctx->side;
+    {
+        StageTimer ts(ctx, ctx->stream, SM_STAGE_SWEEP, G);
+        rc = sweep_pass(ctx, n, g, j, 0);
+    }
+    ctx->stream = main;
+    if (rc != SM_OK) return rc;
+    HIP_TRY(ctx, hipEventRecord(ctx->ev_join, ctx->side));
+    if ((rc = dispatch(ctx, n, g, bs, DISPATCH_HYBRID)) != SM_OK) return rc;
+    HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
+    return SM_OK;
+}
+
 // device-side error word of the sweep engine (boundary poll timeout); clears it
 int check_sweep_errors(sm_ctx* ctx)
 {
@@ -596,11 +654,14 @@ int check_sweep_errors(sm_ctx* ctx)
     return SM_OK;
 }
 
-int group_size(const sm_ctx* ctx, const Norm& n, int H, int npairs, bool sweep)
+int group_size(const sm_ctx* ctx, const Norm& n, int H, int npairs, bool sweep, bool hybrid)
 {
     const size_t cells = (size_t)H * std::max(n.width1, 1) * n.D;
-    // sweep engine: E + W volumes (+ the u16 partial at 8 paths); else one volume per direction
-    const size_t per = sweep ? cells * (2 * elem_bytes(n) + (n.ndirs == 8 ? 2 : 0)) : cells * elem_bytes(n) * n.ndirs;
+    // sweep engine: E + W volumes (+ the u16 partial at 8 paths); hybrid: 5 volumes + the
+    // partial; else one volume per direction
+    const size_t per = sweep    ? cells * (2 * elem_bytes(n) + (n.ndirs == 8 ? 2 : 0))
+                       : hybrid ? cells * (5 * elem_bytes(n) + 2)
+                                : cells * elem_bytes(n) * n.ndirs;
     const size_t g = std::max<size_t>(1, kSetBudget / std::max<size_t>(per, 1));
     // at least two groups per call when possible, so WTA(g) overlaps paths(g+1)
     const size_t half = overlap(ctx) ? std::max(1, (npairs + 1) / 2) : kMaxGroup;
@@ -771,6 +832,8 @@ int run_group(sm_ctx* ctx, const Src& src, const Geo& g, const Norm& n, int16_t*
     }
     if (g.sweep) {
         if ((rc = run_sweep(ctx, n, g, bs)) != SM_OK) return rc;
+    } else if (g.hybrid) {
+        if ((rc = run_hybrid(ctx, n, g, bs)) != SM_OK) return rc;
     } else if ((rc = dispatch(ctx, n, g, bs, DISPATCH_PATHS)) != SM_OK) {
         return rc;
     }
@@ -818,11 +881,13 @@ int run_pairs(sm_ctx* ctx, const Src& src, int npairs, int H, int W, int stride,
     g.vol = (size_t)H * std::max(n.width1, 0) * n.D;
     g.slot_bytes = (g.vol * elem_bytes(n) + 255) & ~size_t(255);
     g.sweep = use_sweep(ctx, n, H);
-    g.L_pair = g.slot_bytes * (g.sweep ? 2 : n.ndirs);  // sweep engine keeps only the E and W volumes
+    g.hybrid = !g.sweep && use_hybrid(ctx, n, H);
+    // sweep engine keeps only the E and W volumes, the hybrid E, W, NE, N, NW
+    g.L_pair = g.slot_bytes * (g.sweep ? 2 : g.hybrid ? 5 : n.ndirs);
     g.census_pair = (size_t)H * W;
     g.cost_pair = n.cost == SM_COST_CENSUS ? 0 : g.vol;
-    ctx->last_ndirs = g.sweep ? 2 : n.ndirs;
-    const int G = group_size(ctx, n, H, npairs, g.sweep);
+    ctx->last_ndirs = g.sweep ? 2 : g.hybrid ? 5 : n.ndirs;
+    const int G = group_size(ctx, n, H, npairs, g.sweep, g.hybrid);
     int rc = SM_OK;
     {
         StageTimer total(ctx, ctx->stream, SM_STAGE_TOTAL, npairs);

@@ -88,11 +88,11 @@ for _i in range(36):
                       d12=int(_rng.choice([1, 2, 1000000])), seed=int(_rng.integers(0, 1 << 30))))
 
 
-@pytest.mark.parametrize("flags", [0, 16384], ids=["default", "sweep8"])
+@pytest.mark.parametrize("flags", [0, 16384, 32768], ids=["default", "sweep8", "hybrid8"])
 @pytest.mark.parametrize("c", CASES, ids=lambda c: "H{H}W{W}D{D}m{minD}c{cost}p{mode}".format(**c))
 def test_random_shapes_vs_c_oracle(eng, c, flags):
     """Default engines, then the fused sweeps for 8 paths too (16384; 5 paths
-    run on the sweeps by default)."""
+    run on the sweeps by default) and the hybrid 8-path engine (32768)."""
     if flags and c["mode"] != 8:
         pytest.skip("5 paths already run on the sweeps by default")
     eng.set_debug_flags(flags)
@@ -120,7 +120,9 @@ def _random_case(eng, c):
                                                   ("kitti", 1, 5, 0), ("mccnn", 1, 8, 0), ("kitti", 1, 8, 32),
                                                   ("kitti", 1, 8, 1024), ("kitti", 1, 8, 512),
                                                   ("kitti", 1, 8, 16384), ("kitti", 0, 8, 16384),
-                                                  ("kitti", 0, 5, 4096), ("mccnn", 1, 8, 16384)])
+                                                  ("kitti", 0, 5, 4096), ("mccnn", 1, 8, 16384),
+                                                  ("kitti", 1, 8, 32768), ("kitti", 0, 8, 32768),
+                                                  ("mccnn", 1, 8, 32768)])
 def test_full_size_bit_exact(eng, name, cost, mode, flags):
     H, W, D = synthetic.CONFIGS[name]
     left, right, gt = synthetic.random_dot_pair(H, W, D, seed=42)
@@ -181,13 +183,13 @@ def test_batch_device_matches_single(eng):
         assert np.array_equal(got[i], ref_c.compute(a, b, q))
 
 
-@pytest.mark.parametrize("flags", [0, 32, 64, 96, 4096, 8192, 16384, 16384 | 8192])
+@pytest.mark.parametrize("flags", [0, 32, 64, 96, 4096, 8192, 16384, 16384 | 8192, 32768, 32768 | 64])
 def test_batch_pipeline_groups(eng, flags):
     """Batches through the normal pipeline (fused sweeps), the fused row kernel
     (32), the two-stream overlap (64: 7 pairs -> launch groups of 4 + 3 on
     alternating buffer sets, WTA of group g on the second stream beside paths
-    of group g+1), the per-direction engine (4096) and one pair per sweep
-    launch (8192); then a call with a different geometry reuses (and regrows)
+    of group g+1), the per-direction engine (4096), one pair per sweep
+    launch (8192) and the hybrid 8-path engine (32768); then a call with a different geometry reuses (and regrows)
     the sets."""
     import torch
 

@@ -39,6 +39,8 @@ def main():
     for _ in range(2):
         eng.compute_batch_device(dL.data_ptr(), dR.data_ptr(), P, H * W, H, W, W, prm, out.data_ptr())
     torch.cuda.synchronize()
+    ref = out.clone()
+    same = {f: True for f in flags}
     for r in range(args.rounds):
         for f in flags:
             eng.set_debug_flags(f)
@@ -48,11 +50,14 @@ def main():
                 eng.compute_batch_device(dL.data_ptr(), dR.data_ptr(), P, H * W, H, W, W, prm, out.data_ptr())
             t = eng.timing()
             eng.set_timing(False)
+            torch.cuda.synchronize()
+            same[f] = same[f] and bool(torch.equal(out, ref))
             res[f].append({k: v[0] * 1e3 / max(v[2], 1) for k, v in t.items()})
     eng.set_debug_flags(0)
     for f in flags:
         med = {k: float(np.median([x[k] for x in res[f]])) for k in res[f][0]}
-        print(json.dumps({"flags": f, "us_per_pair": {k: round(v, 1) for k, v in med.items()}}))
+        print(json.dumps({"flags": f, "same_as_0": same[f],
+                          "us_per_pair": {k: round(v, 1) for k, v in med.items()}}))
 
 
 if __name__ == "__main__":
