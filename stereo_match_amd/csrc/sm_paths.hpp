@@ -416,6 +416,8 @@ struct WtaArgs {
     int nslots;
     int H, W, width1, D, minD, minX1, uniq, disp12;
     int16_t* disp;  // [pair][H][W] pre-median
+    const uint16_t* part;  // hybrid engine: u16 S + SE + SW sums [pair][H][width1][D], or null
+    size_t part_pair;      // elements
 };
 
 template <int DPL, typename LT, int NT>
@@ -485,6 +487,12 @@ __global__ void __launch_bounds__(NT) k_wta(WtaArgs a)
 #pragma unroll
                 for (int i = 0; i < DPL; i++) S[i] += t[i];
             }
+        }
+        if (a.part) {  // wave-uniform
+            uint32_t t[DPL];
+            load_n<DPL>(a.part + (size_t)pair * a.part_pair + off + g * DPL, t);
+#pragma unroll
+            for (int i = 0; i < DPL; i++) S[i] += t[i];
         }
         uint32_t key = 0xFFFFFFFFu;
 #pragma unroll
