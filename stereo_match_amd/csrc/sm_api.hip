@@ -69,6 +69,7 @@ struct BufSet {
 constexpr int DBG_VL16 = 8, DBG_STORE_W = 16, DBG_ROW = 32, DBG_OVERLAP = 64, DBG_H64 = 512, DBG_NO_C8 = 1024;
 // 4096: per-direction engine (one path volume per direction + k_wta) instead of the fused sweeps
 constexpr int DBG_LEGACY = 4096, DBG_SWEEP1 = 8192, DBG_SWEEP8 = 16384, DBG_HYBRID = 32768;
+constexpr int DBG_COST_TILE = 1 << 22;
 
 }  // namespace
 
@@ -654,6 +655,58 @@ int check_sweep_errors(sm_ctx* ctx)
     return SM_OK;
 }
 
+// SGBM cost volume, streaming form (sm_cost.hpp k_sgbm_cost2): one workgroup per
+// (TX-column strip, band of rows, pair)
+template <int S, int CPT>
+int launch_cost2_s(sm_ctx* ctx, const Norm& n, const Geo& g, const smk::SgbmCostArgs& sc)
+{
+    const int NP = n.D / 2, CG = std::max(1, 256 / NP), bd = NP * CG, TX = CG * CPT, NHC = TX + 2 * S;
+    const int rpairs = TX + 2 * S + n.D - 1;
+    if (NP > 256 || NHC > 4 * bd || rpairs > 4 * bd)
+        return fail(ctx, SM_E_UNSUPPORTED, "sgbm cost: numDisparities %d not built", n.D);
+    const bool one = NHC <= bd && rpairs <= bd;  // one prefetch slot per thread (fewer VGPRs)
+    const int rph = (rpairs + 1) / 2;
+    const size_t lds = (size_t)NHC * 16 + (size_t)((NHC + 1) & ~1) * 8 + (size_t)2 * rph * 24 + (size_t)(NHC | 1) * NP * 4;
+    smk::SgbmCost2Args c2{};
+    c2.planes = sc.planes;
+    c2.C = sc.C;
+    c2.C_pair = sc.C_pair;
+    c2.H = sc.H;
+    c2.W = sc.W;
+    c2.width1 = sc.width1;
+    c2.D = sc.D;
+    c2.minD = sc.minD;
+    c2.minX1 = sc.minX1;
+    c2.Yc = sc.Yc;
+    const int strips = (n.width1 + TX - 1) / TX;
+    // enough workgroups to fill the chip; bands at least 8 rows (warm-up 2S rows each)
+    const int want = std::max(1, 2048 / std::max(1, strips * g.G));
+    const int tune = (ctx->dbg_flags >> 28) & 7;  // tuning: band height 8 * (bits 28-30)
+    c2.band = tune ? 8 * tune : std::max({(sc.Yc + want - 1) / want, 8, 4 * S});
+    const int bands = (sc.Yc + c2.band - 1) / c2.band;
+    if (one)
+        hipLaunchKernelGGL((smk::k_sgbm_cost2<S, CPT, 1>), dim3(strips, bands, g.G), dim3(bd), lds, ctx->stream, c2);
+    else
+        hipLaunchKernelGGL((smk::k_sgbm_cost2<S, CPT, 4>), dim3(strips, bands, g.G), dim3(bd), lds, ctx->stream, c2);
+    HIP_TRY(ctx, hipGetLastError());
+    return SM_OK;
+}
+
+int launch_sgbm_cost2(sm_ctx* ctx, const Norm& n, const Geo& g, const smk::SgbmCostArgs& sc)
+{
+    if (ctx->dbg_flags & DBG_COST_TILE) return SM_OK;
+    // 8 columns per thread: 16 measured slower (fewer waves: the register ring is 2S+1 x CPT)
+    switch (n.bs / 2) {
+    case 0: return launch_cost2_s<0, 8>(ctx, n, g, sc);
+    case 1: return launch_cost2_s<1, 8>(ctx, n, g, sc);
+    case 2: return launch_cost2_s<2, 8>(ctx, n, g, sc);
+    case 3: return launch_cost2_s<3, 8>(ctx, n, g, sc);
+    case 4: return launch_cost2_s<4, 8>(ctx, n, g, sc);
+    case 5: return launch_cost2_s<5, 8>(ctx, n, g, sc);
+    default: return fail(ctx, SM_E_UNSUPPORTED, "blockSize %d not built", n.bs);
+    }
+}
+
 int group_size(const sm_ctx* ctx, const Norm& n, int H, int npairs, bool sweep, bool hybrid)
 {
     const size_t cells = (size_t)H * std::max(n.width1, 1) * n.D;
@@ -811,8 +864,11 @@ int run_group(sm_ctx* ctx, const Src& src, const Geo& g, const Norm& n, int16_t*
             sc.SW2 = n.bs / 2;
             sc.SH2 = n.bs / 2;
             sc.Yc = std::max(1, H - n.bs / 2);
+            // streaming box sums (k_sgbm_cost2); flag 1<<22 restores the tiled kernel
+            if ((rc = launch_sgbm_cost2(ctx, n, g, sc)) != SM_OK) return rc;
             // 64-column tiles up to blockSize 7; 32-column tiles keep blockSize 9..11 within 64 KB of LDS
-            if (n.bs <= 7)
+            if (!(ctx->dbg_flags & DBG_COST_TILE)) {
+            } else if (n.bs <= 7)
                 hipLaunchKernelGGL((smk::k_sgbm_cost<64, 3>),
                                    dim3((n.width1 + 63) / 64, (sc.Yc + smk::SC_TY - 1) / smk::SC_TY, G), dim3(256), 0,
                                    ctx->stream, sc);
@@ -823,9 +879,9 @@ int run_group(sm_ctx* ctx, const Src& src, const Geo& g, const Norm& n, int16_t*
             HIP_TRY(ctx, hipGetLastError());
             if (sc.Yc < H) {
                 const size_t row = (size_t)n.width1 * n.D;
-                for (int i = 0; i < G; i++)
-                    hipLaunchKernelGGL(smk::k_sgbm_cost_tail, dim3(grid_for((size_t)(H - sc.Yc) * row / 8)), dim3(256), 0,
-                                       ctx->stream, sc.C + (size_t)i * g.vol, H, sc.Yc, row, (int)(n.mode == SM_MODE_HH));
+                hipLaunchKernelGGL(smk::k_sgbm_cost_tail,
+                                   dim3(std::max(1, grid_for((size_t)(H - sc.Yc) * row / 8) / G), G), dim3(256), 0,
+                                   ctx->stream, sc.C, g.vol, H, sc.Yc, row, (int)(n.mode == SM_MODE_HH));
                 HIP_TRY(ctx, hipGetLastError());
             }
         }

@@ -385,10 +385,197 @@ __global__ void __launch_bounds__(256) k_sgbm_cost(SgbmCostArgs a)
     }
 }
 
+// Streaming form of the same box sum: one workgroup per (strip of TX
+// columns, band of rows, pair), ALL disparities, walking its band row by row.
+// Thread (p, cg) owns the disparity pair (2p, 2p+1) of CPT adjacent columns;
+// per input row it computes the BT costs of its share of the strip + 2S halo
+// columns once (u16 pairs in LDS), a running horizontal sum along its columns
+// (2 LDS reads per output), and a running vertical sum with the last 2S+1
+// rows' horizontal sums in a register ring — no recomputation of vertical
+// halo rows, and a wave stores whole 256-byte d-rows (NP = D/2 lanes per
+// column).  Sums are u16 pairs in u32 lanes: every subtracted term was added
+// before, so no borrow crosses lanes.  Bands start 2S rows early (warm-up).
+struct SgbmCost2Args {
+    const uint2* planes;  // packed, [pair][view][H][W]
+    uint16_t* C;          // [pair][H][width1][D]
+    size_t C_pair;
+    int H, W, width1, D, minD, minX1, Yc, band;
+};
+
+template <int S, int CPT, int NLR>
+__global__ void __launch_bounds__(256) k_sgbm_cost2(SgbmCost2Args a)
+{
+    constexpr int R = 2 * S + 1;
+    extern __shared__ __attribute__((aligned(16))) uint32_t dsm[];
+    const int D = a.D, NP = D >> 1, CG = blockDim.x / NP, TX = CG * CPT, NHC = TX + 2 * S;
+    const int W = a.W, W1 = a.width1;
+    const int tid = threadIdx.x, p = tid % NP, cg = tid / NP;
+    const int x0 = blockIdx.x * TX, pair = blockIdx.z;
+    const int xlo = max(x0 - S, 0), xhi = min(x0 + TX + S - 1, W1 - 1);
+    const int rpairs = xhi - xlo + D - 1;   // right column pairs (k, k+1)
+    const int rph = (rpairs + 1) >> 1;      // per parity
+    const int rb = xlo + a.minX1 - a.minD - (D - 1);  // right column of pair index 0
+    // LDS: left quantities broadcast form [NHC] (uint4 + uint2), right pairs split by
+    // parity [2][rph] (uint4 + uint2), BT costs [NP][PP] (u16 pairs, column fastest,
+    // odd pitch PP: lanes p hit distinct banks; a thread's columns are contiguous)
+    uint4* Ua = reinterpret_cast<uint4*>(dsm);
+    uint2* Ub = reinterpret_cast<uint2*>(Ua + NHC);
+    uint4* Qa = reinterpret_cast<uint4*>(Ub + ((NHC + 1) & ~1));
+    uint2* Qb = reinterpret_cast<uint2*>(Qa + 2 * rph);
+    const int PP = NHC | 1;
+    uint32_t* pix = reinterpret_cast<uint32_t*>(Qb + 2 * rph) + p * PP;
+    const uint2* Lp = a.planes + (size_t)(pair * 2) * a.H * W;
+    const uint2* Rp = Lp + (size_t)a.H * W;
+    const rsrc_t rc = make_rsrc(a.C + pair * a.C_pair, (uint64_t)a.H * W1 * D * 2);
+
+    const int yb0 = blockIdx.y * a.band, yb1 = min(yb0 + a.band, a.Yc);
+    const int r0 = yb0 - S, nsteps = yb1 + S - r0;  // input rows r0 .. yb1-1+S
+
+    // register prefetch of one input row's planes: left halo columns, right column pairs
+    constexpr int NL = NLR, NR = NLR;  // host: NHC, rpairs <= NLR * blockDim
+    uint2 pl[NL], pr0[NR], pr1[NR];
+    auto load_row = [&](int r) {
+        const int y = min(max(r, 0), a.H - 1);
+        const uint2* lrow = Lp + (size_t)y * W + a.minX1;
+        const uint2* rrow = Rp + (size_t)y * W + rb;
+#pragma unroll
+        for (int i = 0; i < NL; i++) {
+            const int c = tid + i * (int)blockDim.x;
+            if (c < NHC) pl[i] = lrow[min(max(x0 - S + c, 0), W1 - 1)];
+        }
+#pragma unroll
+        for (int i = 0; i < NR; i++) {
+            const int k = tid + i * (int)blockDim.x;
+            if (k < rpairs) {
+                pr0[i] = rrow[k];
+                pr1[i] = rrow[k + 1];
+            }
+        }
+    };
+    auto stage_row = [&]() {
+#pragma unroll
+        for (int i = 0; i < NL; i++) {
+            const int c = tid + i * (int)blockDim.x;
+            if (c < NHC) {
+                const uint2 L = pl[i];
+                Ua[c] = make_uint4(__builtin_amdgcn_perm(0, L.x, 0x0c000c00u), __builtin_amdgcn_perm(0, L.x, 0x0c010c01u),
+                                   __builtin_amdgcn_perm(0, L.x, 0x0c020c02u), __builtin_amdgcn_perm(0, L.x, 0x0c030c03u));
+                Ub[c] = make_uint2(__builtin_amdgcn_perm(0, L.y, 0x0c000c00u), __builtin_amdgcn_perm(0, L.y, 0x0c010c01u));
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < NR; i++) {
+            const int k = tid + i * (int)blockDim.x;
+            if (k < rpairs) {
+                const uint2 c0 = pr0[i], c1 = pr1[i];
+                const int q = (k & 1) * rph + (k >> 1);
+                // u16 pair (col k+1 | col k << 16): lanes (d, d+1) of one column
+                Qa[q] = make_uint4(__builtin_amdgcn_perm(c1.x, c0.x, 0x0c000c04u), __builtin_amdgcn_perm(c1.x, c0.x, 0x0c010c05u),
+                                   __builtin_amdgcn_perm(c1.x, c0.x, 0x0c020c06u), __builtin_amdgcn_perm(c1.x, c0.x, 0x0c030c07u));
+                Qb[q] = make_uint2(__builtin_amdgcn_perm(c1.y, c0.y, 0x0c000c04u), __builtin_amdgcn_perm(c1.y, c0.y, 0x0c010c05u));
+            }
+        }
+    };
+
+    uint32_t ring[R][CPT], vs[CPT];
+#pragma unroll
+    for (int q = 0; q < R; q++)
+#pragma unroll
+        for (int i = 0; i < CPT; i++) ring[q][i] = 0;
+#pragma unroll
+    for (int i = 0; i < CPT; i++) vs[i] = 0;
+    const int hx0 = cg * CPT;  // first own column, halo index minus S
+    // valid halo columns (inside [0, W1)): [hlo, hhi]; strips at the image edges clamp
+    const int hlo = max(0, S - x0), hhi = min(NHC - 1, W1 - 1 - x0 + S);
+    const bool edge = hlo > 0 || hhi < NHC - 1;
+    // BT work split: thread cg computes halo columns [hb0, hb1) of its pair p
+    const int per = (NHC + CG - 1) / CG;
+    const int hb0 = max(cg * per, hlo), hb1 = min(cg * per + per, hhi + 1);
+    // right pair index of column hb0 (and hb0 + 1) -> parity-split LDS slots
+    const int kk0 = (x0 - S + hb0) - xlo + D - 2 - 2 * p;
+    const int q0 = (kk0 & 1) * rph + (kk0 >> 1), q1 = ((kk0 + 1) & 1) * rph + ((kk0 + 1) >> 1);
+
+    load_row(r0);
+    for (int s0 = 0; s0 < nsteps; s0 += R) {
+#pragma unroll
+        for (int q = 0; q < R; q++) {
+            const int st = s0 + q;
+            if (st < nsteps) {  // workgroup-uniform
+                __syncthreads();  // previous row done with Ua/Qa and pix
+                stage_row();
+                if (st + 1 < nsteps) load_row(r0 + st + 1);
+                __syncthreads();
+                // BT costs of this thread's contiguous run of valid halo columns, pair p
+                {
+                    int hc = hb0;
+                    const uint4* ua = Ua + hc;
+                    const uint2* ub = Ub + hc;
+                    const uint4* qa0 = Qa + q0;
+                    const uint2* qb0 = Qb + q0;
+                    const uint4* qa1 = Qa + q1;
+                    const uint2* qb1 = Qb + q1;
+                    auto bt = [&](uint4 uA, uint2 uB, uint4 qa, uint2 qb) -> uint32_t {
+                        const u16x2 U0 = as_u16x2(uA.x), U1 = as_u16x2(uA.y), U2 = as_u16x2(uA.z);
+                        const u16x2 U3 = as_u16x2(uA.w), U4 = as_u16x2(uB.x), U5 = as_u16x2(uB.y);
+                        const u16x2 V0 = as_u16x2(qa.x), V1 = as_u16x2(qa.y), V2 = as_u16x2(qa.z);
+                        const u16x2 V3 = as_u16x2(qa.w), V4 = as_u16x2(qb.x), V5 = as_u16x2(qb.y);
+                        const u16x2 g = __builtin_elementwise_min(__builtin_elementwise_max(subsat(U0, V2), subsat(V1, U0)),
+                                                                  __builtin_elementwise_max(subsat(V0, U2), subsat(U1, V0)));
+                        const u16x2 rr = __builtin_elementwise_min(__builtin_elementwise_max(subsat(U3, V5), subsat(V4, U3)),
+                                                                   __builtin_elementwise_max(subsat(V3, U5), subsat(U4, V3)));
+                        return as_u32(g + (rr >> (u16x2)2));
+                    };
+                    // consecutive columns alternate the parity of their right pair index
+                    for (; hc + 1 < hb1; hc += 2) {
+                        const uint32_t e0 = bt(ua[0], ub[0], *qa0, *qb0);
+                        const uint32_t e1 = bt(ua[1], ub[1], *qa1, *qb1);
+                        pix[hc] = e0;
+                        pix[hc + 1] = e1;
+                        ua += 2;
+                        ub += 2;
+                        qa0++;
+                        qb0++;
+                        qa1++;
+                        qb1++;
+                    }
+                    if (hc < hb1) pix[hc] = bt(ua[0], ub[0], *qa0, *qb0);
+                }
+                __syncthreads();
+                // running horizontal sum along the thread's CPT columns (halo columns past
+                // the image edge repeat the edge column), then the vertical ring
+                uint32_t v[CPT + 2 * S];
+                if (edge) {
+#pragma unroll
+                    for (int j = 0; j < CPT + 2 * S; j++) v[j] = pix[min(max(hx0 + j, hlo), hhi)];
+                } else {
+#pragma unroll
+                    for (int j = 0; j < CPT + 2 * S; j++) v[j] = pix[hx0 + j];
+                }
+                uint32_t h = 0;
+#pragma unroll
+                for (int j = 0; j < 2 * S + 1; j++) h += v[j];
+                const int y = r0 + st - S;  // output row of this step (valid when st >= 2S)
+                const uint32_t ob = (((uint32_t)max(y, 0) * W1 + x0 + hx0) * D + 2 * p) * 2;
+                const int nval = st >= 2 * S ? W1 - (x0 + hx0) : 0;
+#pragma unroll
+                for (int i = 0; i < CPT; i++) {
+                    if (i) h += v[i + 2 * S] - v[i - 1];
+                    vs[i] += h;
+                    ring[q][i] = h;
+                    // column step as the scalar offset: one voffset for all CPT stores
+                    if (i < nval) __builtin_amdgcn_raw_buffer_store_b32(vs[i], rc, ob, i * 2 * D, 0);
+                    vs[i] -= ring[(q + 1) % R][i];  // row r - 2S leaves the window
+                }
+            }
+        }
+    }
+}
+
 // Rows y >= Yc: MODE_SGBM reuses one C row, so they stay equal to row Yc-1;
 // MODE_HH keeps one C row per y that is never updated (P2 seed only: C_true = 0).
-__global__ void __launch_bounds__(256) k_sgbm_cost_tail(uint16_t* C, int H, int Yc, size_t row_elems, int hh)
+__global__ void __launch_bounds__(256) k_sgbm_cost_tail(uint16_t* C, size_t C_pair, int H, int Yc, size_t row_elems, int hh)
 {
+    C += blockIdx.y * C_pair;  // one launch for the group's pairs
     const size_t n = (size_t)(H - Yc) * row_elems / 8;
     const uint4* src = reinterpret_cast<const uint4*>(C + (size_t)(Yc - 1) * row_elems);
     uint4* dst = reinterpret_cast<uint4*>(C + (size_t)Yc * row_elems);

@@ -116,13 +116,26 @@ def _random_case(eng, c):
     assert np.array_equal(out, expected), f"{np.sum(out != expected)} px differ"
 
 
+@pytest.mark.parametrize("bs,D,minD", [(9, 16, 0), (11, 48, -5), (9, 144, 3), (11, 80, 0), (1, 256, 0), (3, 160, -20)])
+def test_sgbm_cost_block_sizes(eng, bs, D, minD):
+    """The streaming SGBM cost kernel at every blockSize radius and odd /
+    small column-group counts (D = 144, 160: 3 column groups per workgroup)."""
+    left, right, _ = synthetic.random_dot_pair(45, 330, D, seed=bs * 1000 + D)
+    p = dict(synthetic.parity_params(D), minDisparity=minD, blockSize=bs, P1=8 * bs * bs, P2=32 * bs * bs)
+    if bs >= 9:
+        p["preFilterCap"] = 15  # int16-exact domain: bs^2 * (2 * cap + 63) + P2 <= 16383
+    for mode in (5, 8):
+        q = dict(p, mode=mode)
+        assert np.array_equal(run(eng, left, right, q), ref_c.compute(left, right, q)), (bs, D, minD, mode)
+
+
 @pytest.mark.parametrize("name,cost,mode,flags", [("kitti", 1, 8, 0), ("kitti", 0, 5, 0), ("kitti", 0, 8, 0),
                                                   ("kitti", 1, 5, 0), ("mccnn", 1, 8, 0), ("kitti", 1, 8, 32),
                                                   ("kitti", 1, 8, 1024), ("kitti", 1, 8, 512),
                                                   ("kitti", 1, 8, 16384), ("kitti", 0, 8, 16384),
                                                   ("kitti", 0, 5, 4096), ("mccnn", 1, 8, 16384),
                                                   ("kitti", 1, 8, 32768), ("kitti", 0, 8, 32768),
-                                                  ("mccnn", 1, 8, 32768)])
+                                                  ("mccnn", 1, 8, 32768), ("kitti", 0, 5, 1 << 22)])
 def test_full_size_bit_exact(eng, name, cost, mode, flags):
     H, W, D = synthetic.CONFIGS[name]
     left, right, gt = synthetic.random_dot_pair(H, W, D, seed=42)
