@@ -555,8 +555,18 @@ int sweep_pass(sm_ctx* ctx, const Norm& n, const Geo& g, const SweepJob& j, int 
     return SM_OK;
 }
 
-// E/W volumes -> [down sweep partial] -> WTA sweep -> LR check into bs.raw
-int run_sweep(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs)
+// launches of a scope go to another stream (restored on every exit path)
+struct StreamSwap {
+    sm_ctx* c;
+    hipStream_t old;
+    StreamSwap(sm_ctx* c_, hipStream_t s) : c(c_), old(c_->stream) { c->stream = s; }
+    ~StreamSwap() { c->stream = old; }
+};
+
+// E/W volumes -> [down sweep partial] -> WTA sweep -> LR check into bs.raw.  With
+// wta_stream != ctx->stream (5 paths, two-stream overlap) the WTA sweep and the
+// LR pass run there, beside the next launch group's cost + E/W on ctx->stream.
+int run_sweep(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs, hipStream_t wta_stream)
 {
     const int G = g.G;
     int rc;
@@ -600,6 +610,11 @@ int run_sweep(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs)
             return rc;
         }
     }
+    if (wta_stream != ctx->stream) {
+        HIP_TRY(ctx, hipEventRecord(bs.paths_done, ctx->stream));
+        HIP_TRY(ctx, hipStreamWaitEvent(wta_stream, bs.paths_done, 0));
+    }
+    StreamSwap sw(ctx, wta_stream);
     StageTimer t(ctx, ctx->stream, SM_STAGE_WTA, G);
     {
         StageTimer ts(ctx, ctx->stream, SM_STAGE_SWEEP_WTA, G);
@@ -887,7 +902,10 @@ int run_group(sm_ctx* ctx, const Src& src, const Geo& g, const Norm& n, int16_t*
         }
     }
     if (g.sweep) {
-        if ((rc = run_sweep(ctx, n, g, bs)) != SM_OK) return rc;
+        // 5 paths: the WTA sweep of this group overlaps the next group's cost + E/W
+        // (the 8-path sweeps keep the second stream for their E/W fork)
+        const hipStream_t ws = n.ndirs == 5 ? stream_b(ctx) : ctx->stream;
+        if ((rc = run_sweep(ctx, n, g, bs, ws)) != SM_OK) return rc;
     } else if (g.hybrid) {
         if ((rc = run_hybrid(ctx, n, g, bs)) != SM_OK) return rc;
     } else if ((rc = dispatch(ctx, n, g, bs, DISPATCH_PATHS)) != SM_OK) {

@@ -97,7 +97,10 @@ __device__ __forceinline__ void horz_impl(const PathsArgs& a, int pair, int hb, 
     if constexpr (CENSUS) {
         if (a.cost8 && !(a.dbg & 2048)) {  // costs from the precomputed u8 volume (same [H][W1][D] layout as L)
             // ring of PF loads in flight: step s uses ring[s % PF], then refills it with step s + PF
-            constexpr int PF = 8;
+#ifndef HPF8
+#define HPF8 8
+#endif
+            constexpr int PF = HPF8;
             const rsrc_t rc = make_rsrc(a.cost8 + (size_t)pair * a.cost_pair, (uint64_t)H * W1 * D);
             RawBytes<DPL> ring[PF];
 #pragma unroll
@@ -174,7 +177,10 @@ __device__ __forceinline__ void horz_impl(const PathsArgs& a, int pair, int hb, 
     } else {
         // u16 cost volume; ring of PF loads in flight (the serial chain of one
         // line is short of independent work, so the loads are issued PF steps ahead)
-        constexpr int PF = 4;
+#ifndef HPF16
+#define HPF16 4
+#endif
+        constexpr int PF = HPF16;
         const rsrc_t rc = make_rsrc(a.cost + (size_t)pair * a.cost_pair, (uint64_t)H * W1 * D * 2);
         const int coff0 = off0 / (int)sizeof(LT) * 2, cstep = step_bytes / (int)sizeof(LT) * 2;
         RawU16<DPL> ring[PF];
