@@ -470,6 +470,9 @@ bool use_sweep(const sm_ctx* ctx, const Norm& n, int H)
     // it there; flag 16384 selects the sweeps for 8 paths too
     if (n.ndirs == 8 && !(ctx->dbg_flags & DBG_SWEEP8)) return false;
     if (n.cost == SM_COST_CENSUS && !use_cost8(ctx, n)) return false;  // the sweeps read the u8 cost volume
+    // packed u16 recurrence (sm_sweep.hpp): every L must stay <= 16383 (SGBM costs: normalize's domain check)
+    const int cmax = n.cost == SM_COST_CENSUS ? 64 : n.cost == SM_COST_VOLUME ? smk::VOL_CMAX : 0;
+    if (cmax + n.P2 > 16383) return false;
     if (H > 65535 || n.width1 <= 0) return false;                      // row index lives in 16 tag bits
     if ((size_t)n.maxX1 * 6 + 16 > 65536) return false;                 // k_lr_rows keeps a row in LDS
     return (uint64_t)H * n.width1 * n.D * 2 <= smk::kMaxRecords;

@@ -242,7 +242,10 @@ template <typename T, int N>
 __device__ __forceinline__ void pack_words(const uint32_t (&in)[N], uint32_t (&w)[(N * sizeof(T) + 3) / 4])
 {
     constexpr int NW = (N * (int)sizeof(T) + 3) / 4;
-    if constexpr (sizeof(T) == 1) {
+    if constexpr (sizeof(T) == 4) {  // words already packed (u16 pairs of the packed sweeps)
+#pragma unroll
+        for (int k = 0; k < NW; k++) w[k] = in[k];
+    } else if constexpr (sizeof(T) == 1) {
 #pragma unroll
         for (int k = 0; k < NW; k++) {
             const uint32_t a = in[4 * k];

@@ -104,15 +104,29 @@ __device__ __forceinline__ void horz_impl(const PathsArgs& a, int pair, int hb, 
             const rsrc_t rc = make_rsrc(a.cost8 + (size_t)pair * a.cost_pair, (uint64_t)H * W1 * D);
             RawBytes<DPL> ring[PF];
 #pragma unroll
-            for (int k = 0; k < PF; k++) ring[k].load(rc, k < W1 ? (uint32_t)(off0 + k * step_bytes) : kOOB);
+            for (int k = 0; k < PF; k++) {
+                ring[k].load(rc, k < W1 ? (uint32_t)(off0 + k * step_bytes) : kOOB);
+                // issue order = slot order: the loop-head wait is the max over entry
+                // paths, and slot 0 issued last would make it vmcnt(0) every round
+                asm volatile("" ::: "memory");
+            }
             int off = off0;
             for (int s0 = 0; s0 < W1; s0 += PF) {
 #pragma unroll
                 for (int k = 0; k < PF; k++) {
                     const int s = s0 + k;
                     uint32_t C[DPL], Ln[DPL];
+                    // the slot is read only after the previous step (no hoisted unpacks,
+                    // whose waits would cover the younger slots too)
+#pragma unroll
+                    for (int j = 0; j < RawBytes<DPL>::WORDS; j++) asm volatile("" : "+v"(ring[k].w[j]) : "v"(minLp));
 #pragma unroll
                     for (int i = 0; i < DPL; i++) C[i] = ring[k].template get<uint8_t>(i);
+                    // materialise the slot's values before its refill is issued: otherwise
+                    // hipcc keeps both, rotates the ring with moves at the back-edge and
+                    // those wait (vmcnt) for the loads just issued (no prefetch left)
+#pragma unroll
+                    for (int i = 0; i < DPL; i++) asm volatile("" : "+v"(C[i])::"memory");
                     ring[k].load(rc, s + PF < W1 ? (uint32_t)(off + PF * step_bytes) : kOOB);
                     const uint32_t mn = sgm_step<LANES, DPL>(Lp, minLp, C, P1, P2, Ln);
                     bstore_n<LT, DPL>(rout, (line_ok && s < W1) ? (uint32_t)off : kOOB, Ln);
@@ -185,14 +199,21 @@ __device__ __forceinline__ void horz_impl(const PathsArgs& a, int pair, int hb, 
         const int coff0 = off0 / (int)sizeof(LT) * 2, cstep = step_bytes / (int)sizeof(LT) * 2;
         RawU16<DPL> ring[PF];
 #pragma unroll
-        for (int k = 0; k < PF; k++) ring[k].load(rc, k < W1 ? (uint32_t)(coff0 + k * cstep) : kOOB);
+        for (int k = 0; k < PF; k++) {
+            ring[k].load(rc, k < W1 ? (uint32_t)(coff0 + k * cstep) : kOOB);
+            asm volatile("" ::: "memory");  // issue order = slot order (see the u8 ring)
+        }
         int off = off0, coff = coff0;
         for (int s0 = 0; s0 < W1; s0 += PF) {
 #pragma unroll
             for (int k = 0; k < PF; k++) {
                 const int s = s0 + k;
                 uint32_t C[DPL], Ln[DPL];
+#pragma unroll
+                for (int j = 0; j < RawU16<DPL>::WORDS; j++) asm volatile("" : "+v"(ring[k].w[j]) : "v"(minLp));
                 ring[k].unpack(C);
+#pragma unroll
+                for (int i = 0; i < DPL; i++) asm volatile("" : "+v"(C[i])::"memory");  // see the u8 ring
                 ring[k].load(rc, s + PF < W1 ? (uint32_t)(coff + PF * cstep) : kOOB);
                 coff += cstep;
                 const uint32_t mn = sgm_step<LANES, DPL>(Lp, minLp, C, P1, P2, Ln);

@@ -49,6 +49,11 @@ typedef __attribute__((address_space(1))) unsigned long long gu64;
 
 constexpr uint32_t SW_SPIN_LIMIT = 1u << 19;
 
+// build-time switch back to the u32 recurrence for every DPL (comparison builds)
+#ifndef SWEEP_U32
+#define SWEEP_U32 0
+#endif
+
 template <int VL, int DPL>
 struct SweepGeo {
     static constexpr int LPW = 64 / VL;             // columns per wave
@@ -116,6 +121,92 @@ __device__ __forceinline__ uint32_t sweep_step(const uint32_t (&Lp)[DPL], uint32
     return group_min<VL>(mn);
 }
 
+// ---- packed form (even DPL): a lane's L vector as NP = DPL/2 u16 pairs
+// (d even in the low half), two disparities per VOP3P instruction.  Every
+// intermediate fits 16 bits: L <= max cost + P2 <= 16383 (host domain checks),
+// the edge value is OpenCV's MAX_COST 0x7FFF, partial sums of three paths stay
+// below 2^16 and the WTA sums saturate before the 32767 clamp.
+typedef unsigned short pk16 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ pk16 pkv(uint32_t w) { return __builtin_bit_cast(pk16, w); }
+__device__ __forceinline__ uint32_t pkw(pk16 v) { return __builtin_bit_cast(uint32_t, v); }
+__device__ __forceinline__ uint32_t pk_min(uint32_t a, uint32_t b) { return pkw(__builtin_elementwise_min(pkv(a), pkv(b))); }
+__device__ __forceinline__ uint32_t pk_add(uint32_t a, uint32_t b) { return pkw(pkv(a) + pkv(b)); }
+__device__ __forceinline__ uint32_t pk_sub(uint32_t a, uint32_t b) { return pkw(pkv(a) - pkv(b)); }
+__device__ __forceinline__ uint32_t pk_adds(uint32_t a, uint32_t b)
+{
+    return pkw(__builtin_elementwise_add_sat(pkv(a), pkv(b)));
+}
+
+template <int VL, int NP>
+__device__ __forceinline__ uint32_t sweep_step_pk(const uint32_t (&Lp)[NP], uint32_t minLp, const uint32_t (&C)[NP],
+                                                  uint32_t P1p, uint32_t P2, uint32_t (&Ln)[NP])
+{
+    constexpr uint32_t EDGE = kBig | (kBig << 16);
+    const uint32_t lm = Line<VL>::prev(EDGE, Lp[NP - 1]);  // its high half is d - 1 of element 0
+    const uint32_t lq = Line<VL>::next(EDGE, Lp[0]);       // its low half is d + 1 of the last element
+    const uint32_t mm = minLp * 0x10001u, dl = (minLp + P2) * 0x10001u;
+    uint32_t mn = 0xFFFFFFFFu;
+    uint32_t a1 = __builtin_amdgcn_alignbit(Lp[0], lm, 16);  // (d-1, d) neighbours of pair 0
+#pragma unroll
+    for (int k = 0; k < NP; k++) {
+        const uint32_t a2 = __builtin_amdgcn_alignbit(k + 1 < NP ? Lp[k + 1] : lq, Lp[k], 16);  // (d+1, d+2)
+        uint32_t v = pk_min(pk_add(pk_min(a1, a2), P1p), Lp[k]);
+        v = pk_min(v, dl);
+        Ln[k] = pk_add(C[k], pk_sub(v, mm));
+        mn = pk_min(mn, Ln[k]);
+        a1 = a2;
+    }
+    return group_min<VL>(::min(mn & 0xFFFFu, mn >> 16));
+}
+
+// NP packed words of one lane <-> LDS (widest aligned chunks)
+template <int NP>
+__device__ __forceinline__ void lds_get_pk(const uint16_t* p, uint32_t (&v)[NP])
+{
+    if constexpr (NP % 4 == 0) {
+#pragma unroll
+        for (int k = 0; k < NP / 4; k++) {
+            const uint4 q = reinterpret_cast<const uint4*>(p)[k];
+            v[4 * k] = q.x; v[4 * k + 1] = q.y; v[4 * k + 2] = q.z; v[4 * k + 3] = q.w;
+        }
+    } else if constexpr (NP % 2 == 0) {
+#pragma unroll
+        for (int k = 0; k < NP / 2; k++) {
+            const uint2 q = reinterpret_cast<const uint2*>(p)[k];
+            v[2 * k] = q.x; v[2 * k + 1] = q.y;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < NP; k++) v[k] = reinterpret_cast<const uint32_t*>(p)[k];
+    }
+}
+
+template <int NP>
+__device__ __forceinline__ void lds_put_pk(uint16_t* p, const uint32_t (&v)[NP])
+{
+    if constexpr (NP % 4 == 0) {
+#pragma unroll
+        for (int k = 0; k < NP / 4; k++)
+            reinterpret_cast<uint4*>(p)[k] = make_uint4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
+    } else if constexpr (NP % 2 == 0) {
+#pragma unroll
+        for (int k = 0; k < NP / 2; k++) reinterpret_cast<uint2*>(p)[k] = make_uint2(v[2 * k], v[2 * k + 1]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < NP; k++) reinterpret_cast<uint32_t*>(p)[k] = v[k];
+    }
+}
+
+// raw cost / E / W bytes of one lane -> NP packed pairs (u16 already pairs; u8 widened)
+template <typename CT, int DPL>
+__device__ __forceinline__ void unpack_ct_pk(const RawBytes<DPL * (int)sizeof(CT)>& r, uint32_t (&C)[DPL / 2])
+{
+#pragma unroll
+    for (int k = 0; k < DPL / 2; k++) {
+        if constexpr (sizeof(CT) == 2) C[k] = r.w[k];
+        else C[k] = __builtin_amdgcn_perm(0u, r.w[k >> 1], (k & 1) ? 0x0c030c02u : 0x0c010c00u);
+    }
+}
 
 // DPL u16 values of one lane in LDS (little-endian pairs), widest aligned chunks
 template <int DPL>
@@ -347,6 +438,142 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL>::THREADS)) k_sweep(SweepArg
     };
 #pragma unroll
     for (int k = 0; k < PF; k++) issue(k, k);
+
+    if constexpr (DPL % 2 == 0 && !SWEEP_U32) {
+        // ---- packed u16-pair form (same steps as the u32 loop below)
+        constexpr int NP = DPL / 2;
+        const uint32_t P1p = P1 * 0x10001u;
+        uint32_t LVp[NP];
+#pragma unroll
+        for (int i = 0; i < NP; i++) LVp[i] = 0;
+        for (int b = 0; b < nblk; b++) {
+#pragma unroll
+            for (int j = 0; j < HB; j++) {
+                const int k = j % PF;
+                const int s = b * HB + j;
+                const bool live = s < H;
+                const int y = UP ? H - 1 - s : s;
+                const int rb = (s + 1) & 1, wb = s & 1;
+                const uint32_t e = live ? cell(y) : NONE;
+                uint32_t C[NP], Ein[NP], Win[NP], Pin[NP];
+                unpack_ct_pk<CT, DPL>(rc_[k], C);
+                if constexpr (WTA) {
+                    unpack_ct_pk<CT, DPL>(re_[k], Ein);
+                    unpack_ct_pk<CT, DPL>(rw_[k], Win);
+                }
+                if constexpr (MODE == 2) unpack_ct_pk<uint16_t, DPL>(rp_[k], Pin);
+#pragma unroll
+                for (int i = 0; i < NP; i++) {  // before the refill (see the u32 loop)
+                    asm volatile("" : "+v"(C[i])::"memory");
+                    if constexpr (WTA) asm volatile("" : "+v"(Ein[i]), "+v"(Win[i])::"memory");
+                    if constexpr (MODE == 2) asm volatile("" : "+v"(Pin[i])::"memory");
+                }
+                issue(k, s + PF);
+
+                uint32_t nA[NP], nB[NP];
+                uint32_t mnA = 0, mnB = 0;
+                if (!halo_r) {
+                    uint32_t LA[NP];
+                    lds_get_pk<NP>(&lv[rb][0][c][g * DPL], LA);
+                    mnA = sweep_step_pk<VL, NP>(LA, lmin[rb][0][c], C, P1p, P2, nA);
+                    if (wave_ragged) {
+#pragma unroll
+                        for (int i = 0; i < NP; i++) nA[i] = active ? nA[i] : 0u;
+                        mnA = active ? mnA : 0u;
+                    }
+                    lds_put_pk<NP>(&lv[wb][0][c + 1][g * DPL], nA);
+                    if (g == 0) lmin[wb][0][c + 1] = mnA;
+                }
+                if (!halo_l) {
+                    uint32_t LB[NP];
+                    lds_get_pk<NP>(&lv[rb][1][c + 2][g * DPL], LB);
+                    mnB = sweep_step_pk<VL, NP>(LB, lmin[rb][1][c + 2], C, P1p, P2, nB);
+                    if (wave_ragged) {
+#pragma unroll
+                        for (int i = 0; i < NP; i++) nB[i] = active ? nB[i] : 0u;
+                        mnB = active ? mnB : 0u;
+                    }
+                    lds_put_pk<NP>(&lv[wb][1][c + 1][g * DPL], nB);
+                    if (g == 0) lmin[wb][1][c + 1] = mnB;
+                }
+                if (j == HB - 1 && b + 1 < nblk) {
+                    const bool pa = wave == NCW - 2 && has_right, pb = wave == 1 && has_left;
+                    if (pa || pb) {
+                        const uint32_t tag = tag0 | (uint32_t)(b + 1);
+                        const uint32_t o = (uint32_t)((gbase(wg, pa ? 0 : 1, b) + (size_t)(kl * VL + g) * NG) * 8);
+#pragma unroll
+                        for (int q = 0; q < NG; q++)
+                            __builtin_amdgcn_raw_buffer_store_b64(u32x2{pa ? nA[q] : nB[q], tag}, rhop, o + 8 * q, 0, 16);
+                    }
+                }
+
+                uint32_t out[NP];
+#pragma unroll
+                for (int i = 0; i < NP; i++) out[i] = 0;
+                uint32_t recw = 0, nbw = 0;
+                bool wpx = false;
+                if (own) {
+                    uint32_t nV[NP];
+                    const uint32_t mnV = sweep_step_pk<VL, NP>(LVp, mV, C, P1p, P2, nV);
+#pragma unroll
+                    for (int i = 0; i < NP; i++) LVp[i] = nV[i];
+                    mV = mnV;
+                    if constexpr (MODE == 0) {
+#pragma unroll
+                        for (int i = 0; i < NP; i++) out[i] = pk_add(pk_add(nV[i], nA[i]), nB[i]);
+                    } else {
+                        uint32_t Sp[NP], S[DPL];
+                        uint32_t key = 0xFFFFFFFFu;
+#pragma unroll
+                        for (int i = 0; i < NP; i++) {
+                            uint32_t t = pk_adds(pk_adds(pk_adds(pk_adds(nV[i], nA[i]), nB[i]), Ein[i]), Win[i]);
+                            if constexpr (MODE == 2) t = pk_adds(t, Pin[i]);
+                            t = pk_min(t, 0x7FFF7FFFu);  // min(sum, 32767) (census sums stay below 2^11)
+                            Sp[i] = t;
+                            S[2 * i] = t & 0xFFFFu;
+                            S[2 * i + 1] = t >> 16;
+                            key = min(key, min((t << 16) | (uint32_t)(g * DPL + 2 * i),
+                                               (t & 0xFFFF0000u) | (uint32_t)(g * DPL + 2 * i + 1)));
+                        }
+                        lds_put_pk<NP>(&srow[(wave - 1) % (NCW - 2)][kl][g * DPL], Sp);
+                        key = group_min<VL>(key);
+                        const uint32_t minS = key >> 16;
+                        const int best = (int)(key & 0xFFFF);
+                        uint32_t far = 0;
+                        const int gb = g * DPL - best + 1;
+                        if (ku > 0) {
+                            const uint32_t lim = __umul24(minS, 100u);
+#pragma unroll
+                            for (int i = 0; i < DPL; i++)
+                                far = max(far, __umul24(S[i], (uint32_t)ku) < lim ? (uint32_t)(gb + i) : 0u);
+                        } else {
+#pragma unroll
+                            for (int i = 0; i < DPL; i++)
+                                far = max(far, (int)S[i] * ku < (int)minS * 100 ? (uint32_t)(gb + i) : 0u);
+                        }
+                        far = group_max<VL>(far);
+                        const bool ok = far <= 2u && minS < 32767u;
+                        const int bm = max(best - 1, 0), bq = min(best + 1, D - 1);
+                        const uint32_t Sm = srow[(wave - 1) % (NCW - 2)][kl][bm];
+                        const uint32_t Sq = srow[(wave - 1) % (NCW - 2)][kl][bq];
+                        recw = ok ? ((minS << 16) | (uint32_t)best) : 0xFFFFFFFFu;
+                        nbw = Sm | (Sq << 16);
+                        wpx = g == 0 && active && live;
+                    }
+                }
+                if constexpr (MODE == 0) {
+                    bstore_n<uint32_t, NP>(rp, own ? boff(e, 2) : kOOB, out);
+                } else {
+                    const uint32_t px = (uint32_t)y * (uint32_t)a.W + (uint32_t)(x1 + a.minX1);
+                    __builtin_amdgcn_raw_buffer_store_b32(recw, rrec, wpx ? px * 4 : kOOB, 0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b32(nbw, rnb, wpx ? px * 4 : kOOB, 0, 0);
+                }
+                lds_barrier();
+            }
+            if (b + 1 < nblk) lds_barrier();
+        }
+        return;
+    }
 
     for (int b = 0; b < nblk; b++) {
 #pragma unroll
