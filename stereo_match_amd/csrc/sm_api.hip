@@ -550,6 +550,7 @@ int sweep_pass(sm_ctx* ctx, const Norm& n, const Geo& g, const SweepJob& j, int 
         a.P1 = n.P1;
         a.P2 = n.P2;
         a.uniq = n.uniq;
+        a.inv_ku = n.uniq < 100 ? 1.0f / (float)(100 - n.uniq) : 0.f;
         a.nwg = nwg;
         a.epoch = ctx->hop_epoch;
         a.dbg = (ctx->dbg_flags >> 24) & 15;  // timing ablations (results wrong): 1 no polls

@@ -57,7 +57,10 @@ constexpr uint32_t SW_SPIN_LIMIT = 1u << 19;
 template <int VL, int DPL>
 struct SweepGeo {
     static constexpr int LPW = 64 / VL;             // columns per wave
-    static constexpr int NCW = 7;                   // compute waves: left halo, 5 own, right halo
+#ifndef SWEEP_NCW
+#define SWEEP_NCW 7
+#endif
+    static constexpr int NCW = SWEEP_NCW;           // compute waves: left halo, NCW-2 own, right halo
     static constexpr int THREADS = (NCW + 1) * 64;  // + the poller wave
     static constexpr int HB = LPW;                  // rows per block = halo width
     static constexpr int NCOL = NCW * LPW;          // columns held by the compute waves
@@ -87,6 +90,16 @@ __device__ __forceinline__ uint32_t group_min(uint32_t v)
     v = ::min(v, perm_dpp<DPP_QP_XOR2>(v));
     if constexpr (N >= 8) v = ::min(v, perm_dpp<DPP_ROW_HALF_MIRROR>(v));
     if constexpr (N >= 16) v = ::min(v, perm_dpp<DPP_ROW_MIRROR>(v));
+    return v;
+}
+
+template <int N>
+__device__ __forceinline__ uint32_t group_sum(uint32_t v)
+{
+    v += perm_dpp<DPP_QP_XOR1>(v);
+    v += perm_dpp<DPP_QP_XOR2>(v);
+    if constexpr (N >= 8) v += perm_dpp<DPP_ROW_HALF_MIRROR>(v);
+    if constexpr (N >= 16) v += perm_dpp<DPP_ROW_MIRROR>(v);
     return v;
 }
 
@@ -539,23 +552,40 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL>::THREADS)) k_sweep(SweepArg
                         key = group_min<VL>(key);
                         const uint32_t minS = key >> 16;
                         const int best = (int)(key & 0xFFFF);
-                        uint32_t far = 0;
-                        const int gb = g * DPL - best + 1;
-                        if (ku > 0) {
-                            const uint32_t lim = __umul24(minS, 100u);
-#pragma unroll
-                            for (int i = 0; i < DPL; i++)
-                                far = max(far, __umul24(S[i], (uint32_t)ku) < lim ? (uint32_t)(gb + i) : 0u);
-                        } else {
-#pragma unroll
-                            for (int i = 0; i < DPL; i++)
-                                far = max(far, (int)S[i] * ku < (int)minS * 100 ? (uint32_t)(gb + i) : 0u);
-                        }
-                        far = group_max<VL>(far);
-                        const bool ok = far <= 2u && minS < 32767u;
                         const int bm = max(best - 1, 0), bq = min(best + 1, D - 1);
                         const uint32_t Sm = srow[(wave - 1) % (NCW - 2)][kl][bm];
                         const uint32_t Sq = srow[(wave - 1) % (NCW - 2)][kl][bq];
+                        bool ok;
+                        if (ku > 0) {
+                            // uniqueness: S*ku < 100*minS  <=>  S < T = ceil(100*minS / ku); the
+                            // pixel passes iff only best-1, best, best+1 are below T, so count
+                            // the entries below T (packed) and compare with that window's count
+                            const uint32_t lim = minS * 100u;
+                            uint32_t T = 0xFFFFu;
+                            if (lim <= 0xFFFFu * (uint32_t)ku) {  // T < 2^16: float quotient, exact fix-up
+                                T = (uint32_t)((float)lim * a.inv_ku);
+                                T += __umul24(T, (uint32_t)ku) < lim ? 1u : 0u;
+                                T -= (T > 0 && __umul24(T - 1, (uint32_t)ku) >= lim) ? 1u : 0u;
+                            }
+                            const uint32_t Tp = T * 0x10001u;
+                            uint32_t cp = 0;
+#pragma unroll
+                            for (int i = 0; i < NP; i++)
+                                cp = pk_add(cp, pk_min(pkw(__builtin_elementwise_sub_sat(pkv(Tp), pkv(Sp[i]))), 0x10001u));
+                            const uint32_t cnt = group_sum<VL>((cp & 0xFFFFu) + (cp >> 16));
+                            const uint32_t win = (minS < T ? 1u : 0u) + (best > 0 && Sm < T ? 1u : 0u) +
+                                                 (best < D - 1 && Sq < T ? 1u : 0u);
+                            ok = cnt == win;
+                        } else {
+                            uint32_t far = 0;
+                            const int gb = g * DPL - best + 1;
+#pragma unroll
+                            for (int i = 0; i < DPL; i++)
+                                far = max(far, (int)S[i] * ku < (int)minS * 100 ? (uint32_t)(gb + i) : 0u);
+                            far = group_max<VL>(far);
+                            ok = far <= 2u;
+                        }
+                        ok = ok && minS < 32767u;
                         recw = ok ? ((minS << 16) | (uint32_t)best) : 0xFFFFFFFFu;
                         nbw = Sm | (Sq << 16);
                         wpx = g == 0 && active && live;

@@ -21,6 +21,7 @@ struct SweepArgs {
     uint32_t* nb;    // [pair][H][W] S[best-1] | S[best+1] << 16 (sub-pixel inputs)
     uint32_t* err;   // bit 0: a halo poll timed out
     int H, W, W1, D, minD, minX1, P1, P2, uniq;
+    float inv_ku;  // 1 / (100 - uniq) (uniqueness threshold estimate; exact fix-up on the device)
     int nwg;
     uint32_t epoch;  // 1..65535, distinct from the previous launches on the same hop buffer
     int dbg;         // timing ablations only: 1 no waiting in the halo polls, 2 no polls
