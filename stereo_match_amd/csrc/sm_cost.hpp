@@ -168,51 +168,58 @@ struct PrefilterArgs {
     int H, W, stride, ftzero;
 };
 
-__device__ __forceinline__ int sobel_clip(const uint8_t* img, int stride, int H, int W, int y, int x, int ftzero)
-{
-    if (x <= 0 || x >= W - 1) return ftzero;
-    const uint8_t* r = img + (size_t)y * stride;
-    const uint8_t* rn = img + (size_t)max(y - 1, 0) * stride;
-    const uint8_t* rs = img + (size_t)min(y + 1, H - 1) * stride;
-    int v = (r[x + 1] - r[x - 1]) * 2 + rn[x + 1] - rn[x - 1] + rs[x + 1] - rs[x - 1];
-    return min(max(v, -ftzero), ftzero) + ftzero;
-}
-
-__device__ __forceinline__ int raw_px(const uint8_t* img, int stride, int W, int y, int x, int ftzero)
-{
-    if (x <= 0 || x >= W - 1) return ftzero;
-    return img[(size_t)y * stride + x];
-}
-
 // Packed per-pixel planes for the BT cost: one uint2 per pixel per view,
 // bytes [g, g_min, g_max, raw, raw_min, raw_max, 0, 0] (g = clipped Sobel-x,
 // min/max over the half-pixel neighbours as calcPixelCostBT); blockIdx.z =
 // 2*pair + view.
 __global__ void __launch_bounds__(256) k_sgbm_prefilter(PrefilterArgs a)
 {
-    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y, im = blockIdx.z & 1, pair = blockIdx.z >> 1;
-    if (x >= a.W) return;
+    // one workgroup per (256 columns, row, view): the three image rows (+2 halo
+    // columns each side) and the clipped Sobel of columns x0-1 .. x0+256 in LDS
+    __shared__ uint8_t rows[3][260];
+    __shared__ int gs[258];
+    const int x0 = blockIdx.x * 256, y = blockIdx.y, im = blockIdx.z & 1, pair = blockIdx.z >> 1;
+    const int W = a.W, H = a.H, ft = a.ftzero, tid = threadIdx.x;
     const uint8_t* img = a.img[im] + (size_t)pair * a.in_pair;
-    uint32_t b[6];
-    for (int ch = 0; ch < 2; ch++) {
-        int v, vl, vr;
-        if (ch == 0) {
-            v = sobel_clip(img, a.stride, a.H, a.W, y, x, a.ftzero);
-            vl = x > 0 ? (v + sobel_clip(img, a.stride, a.H, a.W, y, x - 1, a.ftzero)) / 2 : v;
-            vr = x < a.W - 1 ? (v + sobel_clip(img, a.stride, a.H, a.W, y, x + 1, a.ftzero)) / 2 : v;
-        } else {
-            v = raw_px(img, a.stride, a.W, y, x, a.ftzero);
-            vl = x > 0 ? (v + raw_px(img, a.stride, a.W, y, x - 1, a.ftzero)) / 2 : v;
-            vr = x < a.W - 1 ? (v + raw_px(img, a.stride, a.W, y, x + 1, a.ftzero)) / 2 : v;
+    for (int i = tid; i < 3 * 260; i += 256) {
+        const int r = i / 260, c = i - r * 260;
+        rows[r][c] = img[(size_t)min(max(y - 1 + r, 0), H - 1) * a.stride + min(max(x0 - 2 + c, 0), W - 1)];
+    }
+    __syncthreads();
+    for (int i = tid; i < 258; i += 256) {  // column xx = x0 - 1 + i sits at rows[.][i + 1]
+        const int xx = x0 - 1 + i, c = i + 1;
+        int v = ft;
+        if (xx > 0 && xx < W - 1) {
+            v = (rows[1][c + 1] - rows[1][c - 1]) * 2 + rows[0][c + 1] - rows[0][c - 1] + rows[2][c + 1] - rows[2][c - 1];
+            v = min(max(v, -ft), ft) + ft;
         }
-        b[3 * ch] = (uint32_t)v;
-        b[3 * ch + 1] = (uint32_t)min(min(vl, vr), v);
-        b[3 * ch + 2] = (uint32_t)max(max(vl, vr), v);
+        gs[i] = v;
+    }
+    __syncthreads();
+    const int x = x0 + tid;
+    if (x >= W) return;
+    auto raw = [&](int xx) { return (xx <= 0 || xx >= W - 1) ? ft : (int)rows[1][xx - x0 + 2]; };
+    uint32_t b[6];
+    {
+        const int v = gs[tid + 1];
+        const int vl = x > 0 ? (v + gs[tid]) / 2 : v;
+        const int vr = x < W - 1 ? (v + gs[tid + 2]) / 2 : v;
+        b[0] = (uint32_t)v;
+        b[1] = (uint32_t)min(min(vl, vr), v);
+        b[2] = (uint32_t)max(max(vl, vr), v);
+    }
+    {
+        const int v = raw(x);
+        const int vl = x > 0 ? (v + raw(x - 1)) / 2 : v;
+        const int vr = x < W - 1 ? (v + raw(x + 1)) / 2 : v;
+        b[3] = (uint32_t)v;
+        b[4] = (uint32_t)min(min(vl, vr), v);
+        b[5] = (uint32_t)max(max(vl, vr), v);
     }
     uint2 w;
     w.x = b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
     w.y = b[4] | (b[5] << 8);
-    reinterpret_cast<uint2*>(a.planes)[((size_t)(pair * 2 + im) * a.H + y) * a.W + x] = w;
+    reinterpret_cast<uint2*>(a.planes)[((size_t)(pair * 2 + im) * H + y) * W + x] = w;
 }
 
 // C_true[y][x1][d] for the rows OpenCV's incremental box filter actually
