@@ -430,7 +430,8 @@ __global__ void __launch_bounds__(256) k_sgbm_cost2(SgbmCost2Args a)
     uint4* Qa = reinterpret_cast<uint4*>(Ub + ((NHC + 1) & ~1));
     uint2* Qb = reinterpret_cast<uint2*>(Qa + 2 * rph);
     const int PP = NHC | 1;
-    uint32_t* pix = reinterpret_cast<uint32_t*>(Qb + 2 * rph) + p * PP;
+    // two row buffers: BT of row r+1 may start while slower threads still sum row r
+    uint32_t* const pix2 = reinterpret_cast<uint32_t*>(Qb + 2 * rph) + p * PP;
     const uint2* Lp = a.planes + (size_t)(pair * 2) * a.H * W;
     const uint2* Rp = Lp + (size_t)a.H * W;
     const rsrc_t rc = make_rsrc(a.C + pair * a.C_pair, (uint64_t)a.H * W1 * D * 2);
@@ -508,7 +509,9 @@ __global__ void __launch_bounds__(256) k_sgbm_cost2(SgbmCost2Args a)
         for (int q = 0; q < R; q++) {
             const int st = s0 + q;
             if (st < nsteps) {  // workgroup-uniform
-                __syncthreads();  // previous row done with Ua/Qa and pix
+                // Ua/Qa were last read by the previous row's BT, which every thread
+                // finished before the previous row's second barrier: no barrier here
+                uint32_t* const pix = pix2 + (st & 1) * (NP * PP);
                 stage_row();
                 if (st + 1 < nsteps) load_row(r0 + st + 1);
                 __syncthreads();
