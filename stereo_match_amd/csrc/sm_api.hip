@@ -834,7 +834,9 @@ int run_group(sm_ctx* ctx, const Src& src, const Geo& g, const Norm& n, int16_t*
                 c8.D = n.D;
                 c8.minD = n.minD;
                 c8.minX1 = n.minX1;
-                hipLaunchKernelGGL(smk::k_census_cost8, dim3((n.width1 + smk::C8_TX - 1) / smk::C8_TX, H, G), dim3(256),
+                hipLaunchKernelGGL(smk::k_census_cost8,
+                                   dim3((n.width1 + smk::C8_TX - 1) / smk::C8_TX, (H + smk::C8_RY - 1) / smk::C8_RY, G),
+                                   dim3(256),
                                    0, ctx->stream, c8);
                 HIP_TRY(ctx, hipGetLastError());
             }

@@ -76,11 +76,12 @@ __global__ void __launch_bounds__(256) k_census9x7(CensusArgs a)
     }
 }
 
-// Census Hamming cost volume for the path kernels' vertical family:
-// C[pair][y][x1][d] = popcount(cl[y][X] ^ cr[y][X-minD-d]) (u8), X = x1 + minX1.
-// One workgroup per (64 columns, row, pair): the 64 left codes and the
-// 64+D-1 right codes they need staged in LDS; a thread writes 16 disparities
-// (one 16-byte store) of one column, consecutive threads consecutive columns.
+// Census Hamming cost volume for the path kernels (u8):
+// C[pair][y][x1][d] = popcount(cl[y][X] ^ cr[y][X-minD-d]), X = x1 + minX1.
+// One workgroup per (64 columns, C8_RY rows, pair); per row the 64 left codes
+// and the 64+D-1 right codes they need are staged in LDS.  Thread (x, c0)
+// computes 16-disparity chunks c0, c0+4, ... of column x (no index division),
+// then the tile's nx*D contiguous bytes leave as coalesced 16-byte stores.
 struct Cost8Args {
     const uint64_t* cl;
     const uint64_t* cr;
@@ -90,43 +91,49 @@ struct Cost8Args {
     int H, W, width1, D, minD, minX1;
 };
 
-constexpr int C8_TX = 64;
+constexpr int C8_TX = 64, C8_RY = 4;
 
 __global__ void __launch_bounds__(256) k_census_cost8(Cost8Args a)
 {
     __shared__ uint64_t lc[C8_TX];
     __shared__ uint64_t rc[C8_TX + 256];
     __shared__ uint4 tile[C8_TX * 17];  // [x][D/16 + 1] 16-byte chunks (padded pitch)
-    const int x0 = blockIdx.x * C8_TX, y = blockIdx.y, pair = blockIdx.z;
+    const int x0 = blockIdx.x * C8_TX, pair = blockIdx.z, tid = threadIdx.x;
     const int nx = min(C8_TX, a.width1 - x0), D = a.D;
-    const uint64_t* cl = a.cl + pair * a.census_pair + (size_t)y * a.W;
-    const uint64_t* cr = a.cr + pair * a.census_pair + (size_t)y * a.W;
     const int X0 = x0 + a.minX1;
     const int rlo = X0 - a.minD - (D - 1);  // right column of rc[0]
-    for (int i = threadIdx.x; i < nx; i += 256) lc[i] = cl[X0 + i];
-    for (int i = threadIdx.x; i < nx + D - 1; i += 256) rc[i] = cr[rlo + i];
-    __syncthreads();
     const int chunks = D / 16, pitch = chunks + 1;
-    for (int i = threadIdx.x; i < nx * chunks; i += 256) {
-        // consecutive lanes take consecutive columns: conflict-free LDS reads
-        const int ch = i / nx, x = i - ch * nx;
-        const uint64_t l = lc[x];
-        // disparity d = 16*ch + j reads right column X - minD - d = rc[x + D - 1 - d]
-        const uint64_t* r = rc + x + D - 1 - 16 * ch;
-        uint32_t w[4];
+    // i / chunks for i < 64 * 16 as a multiply-shift (exact: the error stays below 1/64)
+    const uint32_t M = (65536u + (uint32_t)chunks - 1) / (uint32_t)chunks;
+    const int xl = tid & 63, c0 = tid >> 6;
+    for (int r = 0; r < C8_RY; r++) {
+        const int y = blockIdx.y * C8_RY + r;
+        if (y >= a.H) break;  // workgroup-uniform
+        const uint64_t* cl = a.cl + pair * a.census_pair + (size_t)y * a.W;
+        const uint64_t* cr = a.cr + pair * a.census_pair + (size_t)y * a.W;
+        if (tid < nx) lc[tid] = cl[X0 + tid];
+        for (int i = tid; i < nx + D - 1; i += 256) rc[i] = cr[rlo + i];
+        __syncthreads();  // also: the previous row's stores have read the tile
+        if (xl < nx) {
+            const uint64_t l = lc[xl];
+            for (int ch = c0; ch < chunks; ch += 4) {
+                // disparity d = 16*ch + j reads right column X - minD - d = rc[x + D - 1 - d]
+                const uint64_t* rr = rc + xl + D - 1 - 16 * ch;
+                uint32_t w[4];
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            w[q] = (uint32_t)__popcll(l ^ r[-4 * q]) | ((uint32_t)__popcll(l ^ r[-4 * q - 1]) << 8) |
-                   ((uint32_t)__popcll(l ^ r[-4 * q - 2]) << 16) | ((uint32_t)__popcll(l ^ r[-4 * q - 3]) << 24);
+                for (int q = 0; q < 4; q++) {
+                    w[q] = (uint32_t)__popcll(l ^ rr[-4 * q]) | ((uint32_t)__popcll(l ^ rr[-4 * q - 1]) << 8) |
+                           ((uint32_t)__popcll(l ^ rr[-4 * q - 2]) << 16) | ((uint32_t)__popcll(l ^ rr[-4 * q - 3]) << 24);
+                }
+                tile[xl * pitch + ch] = make_uint4(w[0], w[1], w[2], w[3]);
+            }
         }
-        tile[x * pitch + ch] = make_uint4(w[0], w[1], w[2], w[3]);
-    }
-    __syncthreads();
-    // the tile's nx*D bytes are contiguous in C: coalesced 16-byte stores
-    uint4* out = reinterpret_cast<uint4*>(a.C + pair * a.C_pair + ((size_t)y * a.width1 + x0) * D);
-    for (int i = threadIdx.x; i < nx * chunks; i += 256) {
-        const int x = i / chunks, ch = i - x * chunks;
-        out[i] = tile[x * pitch + ch];
+        __syncthreads();
+        uint4* out = reinterpret_cast<uint4*>(a.C + pair * a.C_pair + ((size_t)y * a.width1 + x0) * D);
+        for (int i = tid; i < nx * chunks; i += 256) {
+            const int x = (int)(((uint32_t)i * M) >> 16), ch = i - x * chunks;
+            out[i] = tile[x * pitch + ch];
+        }
     }
 }
 
