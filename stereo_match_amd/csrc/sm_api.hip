@@ -267,6 +267,8 @@ struct Src {  // where a launch group's pairs come from (device pointers)
     }
 };
 
+int hybrid_slots(const Norm& n);  // per-direction volumes kept by the hybrid engine
+
 struct Geo {  // per-group geometry shared by the launches
     int H, W, stride, G;
     size_t vol, slot_bytes, L_pair, census_pair, cost_pair;
@@ -393,7 +395,7 @@ int launch_wta_t(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs)
     wa.L = (const uint8_t*)bs.L.p;
     wa.slot_bytes = g.slot_bytes;
     wa.L_pair_bytes = g.L_pair;
-    wa.nslots = g.hybrid ? 5 : n.ndirs;
+    wa.nslots = g.hybrid ? hybrid_slots(n) : n.ndirs;
     wa.part = g.hybrid ? (const uint16_t*)bs.part.p : nullptr;  // hybrid: S + SE + SW partial
     wa.part_pair = g.vol;
     wa.H = g.H;
@@ -452,12 +454,16 @@ int dispatch(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs, int what)
 int ensure_event(sm_ctx* ctx, hipEvent_t& e);
 bool use_sweep(const sm_ctx* ctx, const Norm& n, int H);
 
-// 8 paths: the down sweep (S + SE + SW -> one u16 partial, VALU-bound) runs on
-// the side stream beside ONE per-direction launch of E, W, NE, N, NW
-// (HBM-bound); k_wta then sums 5 volumes + the partial (21 instead of 25 B/cell)
+// Hybrid engine: the down sweep (S + SE + SW -> one u16 partial, latency-bound) runs
+// on the side stream beside ONE per-direction launch of the other directions (8
+// paths: E, W, NE, N, NW; 5 paths: E, W); k_wta then sums those volumes + the
+// partial (8 paths: 21 instead of 25 B/cell)
+int hybrid_slots(const Norm& n) { return n.ndirs == 8 ? 5 : 2; }
+
 bool use_hybrid(const sm_ctx* ctx, const Norm& n, int H)
 {
-    if (n.ndirs != 8 || !(ctx->dbg_flags & DBG_HYBRID) || (ctx->dbg_flags & (DBG_LEGACY | DBG_SWEEP8))) return false;
+    if ((n.ndirs != 8 && n.ndirs != 5) || !(ctx->dbg_flags & DBG_HYBRID) || (ctx->dbg_flags & (DBG_LEGACY | DBG_SWEEP8)))
+        return false;
     sm_ctx tmp = *ctx;
     tmp.dbg_flags = (ctx->dbg_flags & ~DBG_HYBRID) | DBG_SWEEP8;  // same preconditions as the sweeps
     return use_sweep(&tmp, n, H);
@@ -656,7 +662,7 @@ int run_hybrid(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs)
     ctx->stream = main;
     if (rc != SM_OK) return rc;
     HIP_TRY(ctx, hipEventRecord(ctx->ev_join, ctx->side));
-    if ((rc = dispatch(ctx, n, g, bs, DISPATCH_HYBRID)) != SM_OK) return rc;
+    if ((rc = dispatch(ctx, n, g, bs, n.ndirs == 8 ? DISPATCH_HYBRID : DISPATCH_HORIZONTAL)) != SM_OK) return rc;
     HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
     return SM_OK;
 }
@@ -732,7 +738,7 @@ int group_size(const sm_ctx* ctx, const Norm& n, int H, int npairs, bool sweep, 
     // sweep engine: E + W volumes (+ the u16 partial at 8 paths); hybrid: 5 volumes + the
     // partial; else one volume per direction
     const size_t per = sweep    ? cells * (2 * elem_bytes(n) + (n.ndirs == 8 ? 2 : 0))
-                       : hybrid ? cells * (5 * elem_bytes(n) + 2)
+                       : hybrid ? cells * (hybrid_slots(n) * elem_bytes(n) + 2)
                                 : cells * elem_bytes(n) * n.ndirs;
     const size_t g = std::max<size_t>(1, kSetBudget / std::max<size_t>(per, 1));
     // at least two groups per call when possible, so WTA(g) overlaps paths(g+1)
@@ -960,13 +966,13 @@ int run_pairs(sm_ctx* ctx, const Src& src, int npairs, int H, int W, int stride,
     g.stride = stride;
     g.vol = (size_t)H * std::max(n.width1, 0) * n.D;
     g.slot_bytes = (g.vol * elem_bytes(n) + 255) & ~size_t(255);
-    g.sweep = use_sweep(ctx, n, H);
-    g.hybrid = !g.sweep && use_hybrid(ctx, n, H);
-    // sweep engine keeps only the E and W volumes, the hybrid E, W, NE, N, NW
-    g.L_pair = g.slot_bytes * (g.sweep ? 2 : g.hybrid ? 5 : n.ndirs);
+    g.hybrid = use_hybrid(ctx, n, H);
+    g.sweep = !g.hybrid && use_sweep(ctx, n, H);
+    // sweep engine keeps only the E and W volumes, the hybrid E, W (+ NE, N, NW at 8 paths)
+    g.L_pair = g.slot_bytes * (g.sweep ? 2 : g.hybrid ? hybrid_slots(n) : n.ndirs);
     g.census_pair = (size_t)H * W;
     g.cost_pair = n.cost == SM_COST_CENSUS ? 0 : g.vol;
-    ctx->last_ndirs = g.sweep ? 2 : g.hybrid ? 5 : n.ndirs;
+    ctx->last_ndirs = g.sweep ? 2 : g.hybrid ? hybrid_slots(n) : n.ndirs;
     const int G = group_size(ctx, n, H, npairs, g.sweep, g.hybrid);
     int rc = SM_OK;
     {

@@ -92,8 +92,8 @@ for _i in range(36):
 @pytest.mark.parametrize("c", CASES, ids=lambda c: "H{H}W{W}D{D}m{minD}c{cost}p{mode}".format(**c))
 def test_random_shapes_vs_c_oracle(eng, c, flags):
     """Default engines, then the fused sweeps for 8 paths too (16384; 5 paths
-    run on the sweeps by default) and the hybrid 8-path engine (32768)."""
-    if flags and c["mode"] != 8:
+    run on the sweeps by default) and the hybrid engine (32768, 5 and 8 paths)."""
+    if flags == 16384 and c["mode"] != 8:
         pytest.skip("5 paths already run on the sweeps by default")
     eng.set_debug_flags(flags)
     try:
@@ -135,7 +135,8 @@ def test_sgbm_cost_block_sizes(eng, bs, D, minD):
                                                   ("kitti", 1, 8, 16384), ("kitti", 0, 8, 16384),
                                                   ("kitti", 0, 5, 4096), ("mccnn", 1, 8, 16384),
                                                   ("kitti", 1, 8, 32768), ("kitti", 0, 8, 32768),
-                                                  ("mccnn", 1, 8, 32768), ("kitti", 0, 5, 1 << 22)])
+                                                  ("mccnn", 1, 8, 32768), ("kitti", 0, 5, 32768),
+                                                  ("kitti", 0, 5, 1 << 22)])
 def test_full_size_bit_exact(eng, name, cost, mode, flags):
     H, W, D = synthetic.CONFIGS[name]
     left, right, gt = synthetic.random_dot_pair(H, W, D, seed=42)
