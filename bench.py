@@ -249,7 +249,7 @@ def main():
             "data": "synthetic random-dot pairs (no dataset in the image)"
                     + ("; f32 cost = 3x3-smoothed |L-R|/255 volume per pair" if volume else ""),
             "config": {
-                "engine": {"auto": "sweeps (5 paths) / per-direction (8 paths)", "perdir": "per-direction",
+                "engine": {"auto": "per-direction (census 8 paths) / fused sweeps (otherwise)", "perdir": "per-direction",
                            "sweep": "fused sweeps"}[args.engine],
                 "workload": f"{args.config} {W}x{H} D={D} "
                             + {"census8": "census9x7 + 8-path SGM", "sgbm5": "OpenCV-SGBM 5-path",

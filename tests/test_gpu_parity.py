@@ -88,12 +88,13 @@ for _i in range(36):
                       d12=int(_rng.choice([1, 2, 1000000])), seed=int(_rng.integers(0, 1 << 30))))
 
 
-@pytest.mark.parametrize("flags", [0, 16384, 32768], ids=["default", "sweep8", "hybrid8"])
+@pytest.mark.parametrize("flags", [0, 4096, 16384, 32768], ids=["default", "perdir", "sweep8", "hybrid"])
 @pytest.mark.parametrize("c", CASES, ids=lambda c: "H{H}W{W}D{D}m{minD}c{cost}p{mode}".format(**c))
 def test_random_shapes_vs_c_oracle(eng, c, flags):
-    """Default engines, then the fused sweeps for 8 paths too (16384; 5 paths
-    run on the sweeps by default) and the hybrid engine (32768, 5 and 8 paths)."""
-    if flags == 16384 and c["mode"] != 8:
+    """Default engines, the per-direction engine (4096), the fused sweeps for
+    census 8 paths too (16384; the other configurations run on the sweeps by
+    default) and the hybrid engine (32768, 5 and 8 paths)."""
+    if flags == 16384 and (c["mode"] != 8 or not c["cost"]):
         pytest.skip("5 paths already run on the sweeps by default")
     eng.set_debug_flags(flags)
     try:
@@ -136,7 +137,7 @@ def test_sgbm_cost_block_sizes(eng, bs, D, minD):
                                                   ("kitti", 0, 5, 4096), ("mccnn", 1, 8, 16384),
                                                   ("kitti", 1, 8, 32768), ("kitti", 0, 8, 32768),
                                                   ("mccnn", 1, 8, 32768), ("kitti", 0, 5, 32768),
-                                                  ("kitti", 0, 5, 1 << 22)])
+                                                  ("kitti", 0, 5, 1 << 22), ("kitti", 0, 8, 4096)])
 def test_full_size_bit_exact(eng, name, cost, mode, flags):
     H, W, D = synthetic.CONFIGS[name]
     left, right, gt = synthetic.random_dot_pair(H, W, D, seed=42)
@@ -324,14 +325,19 @@ def test_volume_random_shapes_vs_c_oracle(eng, c):
     assert np.array_equal(out, ref_c.compute_volume(vol, p, 0.0, synthetic.VOLUME_SCALE))
 
 
-@pytest.mark.parametrize("mode", [8, 5])
-def test_volume_full_size_mccnn(eng, mode):
-    """Config C: (1, 192, 375, 1242) float32 |L-R| volume of the KITTI-size pair."""
+@pytest.mark.parametrize("mode,flags", [(8, 0), (5, 0), (8, 4096)])
+def test_volume_full_size_mccnn(eng, mode, flags):
+    """Config C: (1, 192, 375, 1242) float32 |L-R| volume of the KITTI-size pair
+    (default engine = fused sweeps; 4096 = per-direction engine)."""
     H, W, D = synthetic.CONFIGS["mccnn"]
     left, right, gt = synthetic.random_dot_pair(H, W, D, seed=7)
     vol = synthetic.absdiff_volume(left, right, D)
     p = dict(synthetic.cost_volume_params(D), mode=mode)
-    out = eng.aggregate_cost_f32(vol, synthetic.to_sm_params(p), 0.0, synthetic.VOLUME_SCALE)
+    eng.set_debug_flags(flags)
+    try:
+        out = eng.aggregate_cost_f32(vol, synthetic.to_sm_params(p), 0.0, synthetic.VOLUME_SCALE)
+    finally:
+        eng.set_debug_flags(0)
     assert np.array_equal(out, ref_c.compute_volume(vol, p, 0.0, synthetic.VOLUME_SCALE))
     valid = out >= 0
     assert valid.mean() > 0.7

@@ -26,6 +26,8 @@ def main():
     from stereo_match_amd import _lib, synthetic
     H, W, D = synthetic.CONFIGS[args.config]
     p = synthetic.headline_params(D) if args.mode == "census8" else synthetic.parity_params(D)
+    if args.mode == "sgbm8":  # OpenCV BT cost, 8 paths (MODE_HH)
+        p = dict(p, mode=8)
     prm = synthetic.to_sm_params(p)
     P = args.pairs
     ls, rs = zip(*[synthetic.random_dot_pair(H, W, D, seed=i)[:2] for i in range(P)])
