@@ -35,8 +35,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default=None, choices=["kitti", "middlebury", "tsukuba", "mccnn"],
                     help="default: kitti (mccnn for --mode volume8)")
-    ap.add_argument("--mode", default="census8", choices=["census8", "sgbm5", "volume8", "disparity5", "bm"],
-                    help="census8 = headline; sgbm5 = OpenCV parity mode; volume8 = mc-cnn f32 cost volume; "
+    ap.add_argument("--mode", default="census8", choices=["census8", "sgbm5", "sgbm8", "volume8", "disparity5", "bm"],
+                    help="census8 = headline; sgbm5 = OpenCV parity mode; sgbm8 = OpenCV cost + 8 paths; "
+                         "volume8 = mc-cnn f32 cost volume; "
                          "disparity5 = the reference's whole compute_disparity (left + right SGBM + WLS); "
                          "bm = StereoBM(numDisparities=D, blockSize=21), the method='BM' matcher")
     ap.add_argument("--pairs-per-gpu", type=int, default=8)
@@ -83,6 +84,8 @@ def main():
         p = synthetic.cost_volume_params(D)
     else:
         p = synthetic.parity_params(D)
+        if args.mode == "sgbm8":  # OpenCV cost, 8 paths (MODE_HH)
+            p = dict(p, mode=8)
     prm = synthetic.to_sm_params(p)
     if bm:
         prm = _lib.SmBmParams()
@@ -244,7 +247,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": {"census8": "u8", "sgbm5": "i16", "volume8": "f32->u16", "disparity5": "i16+f32",
+            "dtype": {"census8": "u8", "sgbm5": "i16", "sgbm8": "i16", "volume8": "f32->u16", "disparity5": "i16+f32",
                       "bm": "i32"}[args.mode],
             "data": "synthetic random-dot pairs (no dataset in the image)"
                     + ("; f32 cost = 3x3-smoothed |L-R|/255 volume per pair" if volume else ""),
@@ -253,6 +256,7 @@ def main():
                            "sweep": "fused sweeps"}[args.engine],
                 "workload": f"{args.config} {W}x{H} D={D} "
                             + {"census8": "census9x7 + 8-path SGM", "sgbm5": "OpenCV-SGBM 5-path",
+                               "sgbm8": "OpenCV-SGBM 8-path (MODE_HH)",
                                "volume8": "f32 cost volume (mc-cnn) + 8-path SGM",
                                "disparity5": "compute_disparity: left+right OpenCV-SGBM 5-path + WLS",
                                "bm": "OpenCV StereoBM blockSize 21 (X-Sobel prefilter)"}[args.mode],
