@@ -25,6 +25,6 @@ step bench 400 python -u bench.py --traffic-file "$OUT/census8_traffic.json"
 step bench_sgbm5 400 python -u bench.py --mode sgbm5 --traffic-file "$OUT/sgbm5_traffic.json"
 step bench_census8_sweep 300 python -u bench.py --engine sweep --cpu-baseline-pairs 0
 step bench_sgbm5_perdir 300 python -u bench.py --mode sgbm5 --engine perdir --cpu-baseline-pairs 0
-for m in volume8 disparity5 bm; do step bench_$m 400 python -u bench.py --mode $m; done
+for m in sgbm8 volume8 disparity5 bm; do step bench_$m 400 python -u bench.py --mode $m; done
 step bench_middlebury 400 python -u bench.py --config middlebury --pairs-per-gpu 4 --cpu-baseline-pairs 0
 echo done
