@@ -2,21 +2,35 @@
 """Benchmark: stereo pairs/s (+ Mpix·disp/s) on the BASELINE.json headline
 workload — KITTI 1242×375, D=128, Census 9×7 + 8-path SGM, WTA + uniqueness
 + sub-pixel + left/right check + 3×3 median — on 1..8 MI355X, one process per
-GPU (launched by torch.distributed.run for N > 1).
+GPU.
 
-A step = every rank runs the hot path over its batch of ``--pairs-per-gpu``
-synthetic pairs already resident in HBM, then (N > 1) the int16 disparity
-maps are gathered to rank 0 over RCCL/xGMI (BASELINE config 4).  Weak
-scaling: per-GPU work is fixed as N grows.  Timed region: barrier +
-device sync on both sides, K steps, max over ranks.
+``python bench.py --gpus N`` with N > 1 and no ``WORLD_SIZE`` in the
+environment starts ``torch.distributed.run`` with N ranks as a CHILD process
+(nothing here touches the GPU before that) and exits with its status; the
+driver's own ``torch.distributed.run ... bench.py --gpus N`` lands directly in
+the per-rank path.  ``--gpus`` must equal the world size.
 
-Prints ONE JSON line on rank 0 (see DESIGN.md §6 for every field).
+A step = every rank runs the hot path over its block of ``--pairs-per-gpu``
+synthetic pairs (``batch.shard_range`` of the global batch) already resident
+in HBM, then (N > 1) the int16 disparity maps are gathered to rank 0 over
+RCCL/xGMI (BASELINE config 4).  Weak scaling: per-GPU work is fixed as N
+grows.  Timed region: barrier + device sync on both sides, K steps, max over
+ranks; the gather's share is timed separately with events on the same stream.
+
+Prints ONE JSON line on rank 0 (DESIGN.md §6 lists every field).  The
+roofline figure follows SURVEY.md §8(d): the model's bytes attributable to
+the dominant kernel (see ``model_stage_bytes``) over that kernel's average
+launch time; the engine's own bytes are reported beside it.
 """
 from __future__ import annotations
 
 import argparse
+import glob
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -26,6 +40,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+METRIC = "stereo pairs/sec + Mpix·disp/sec, KITTI 1242×375 D=128 SGM, 1/2/4/8 GPU"
 
 
 def parse():
@@ -42,32 +57,127 @@ def parse():
                          "bm = StereoBM(numDisparities=D, blockSize=21), the method='BM' matcher")
     ap.add_argument("--pairs-per-gpu", type=int, default=8)
     ap.add_argument("--no-gather", action="store_true")
-    ap.add_argument("--row", action="store_true",
-                    help="experimental fused row kernel (E/W paths + WTA) instead of k_wta (D %% 64 == 0)")
     ap.add_argument("--engine", default="auto", choices=["auto", "perdir", "sweep"],
-                    help="auto: fused sweeps for 5 paths, per-direction volumes for 8 paths (measured faster); "
-                         "perdir / sweep force one engine (DESIGN.md §4)")
+                    help="auto: the library's default per configuration; perdir / sweep force one engine "
+                         "(DESIGN.md §4)")
     ap.add_argument("--cpu-baseline-pairs", type=int, default=8,
                     help="pairs timed on the host C port per thread (rank 0, N=1 only); 0 = skip")
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="host threads for the multi-core CPU baseline (the box's CPU share is 16)")
+    ap.add_argument("--host-surface-calls", type=int, default=20,
+                    help="rank 0, N=1: timed calls of the reference surface compute_disparity (host numpy in/out, "
+                         "settings.ini, KITTI size); 0 = skip")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
+    ap.add_argument("--selftest-cpu", action="store_true",
+                    help="launcher self-test: gloo on CPU, a stand-in step (no disparity computed, not a measurement)")
     return ap.parse_args()
 
 
+# ---------------------------------------------------------------------------
+# launcher
+# ---------------------------------------------------------------------------
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int) -> int:
+    """Run this script under torch.distributed.run with n ranks (a child
+    process: the parent never initialises the GPU and never execs)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
+
+
+def source_hash() -> str:
+    """Hash of the kernel + C-ABI sources (stamps PMC traffic files)."""
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(ROOT, "stereo_match_amd", "csrc", "*.hip"))
+                   + glob.glob(os.path.join(ROOT, "stereo_match_amd", "csrc", "*.hpp"))
+                   + glob.glob(os.path.join(ROOT, "include", "*.h")))
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+# ---------------------------------------------------------------------------
+# SURVEY.md §8(d) byte model, attributed to the engine's stages
+# ---------------------------------------------------------------------------
+def model_pair_bytes(mode: str, H: int, W: int, D: int, P: int) -> int:
+    """§8(d) algorithmic bytes per pair (per matcher call)."""
+    cells = H * W * D
+    if mode == "volume8":
+        return cells * (4 * P + 8)
+    if mode == "bm":
+        return H * W * (2 + 2 * 2 + 2 + 4)
+    return cells * (1 + P + 4) + 2 * H * W + 2 * H * W * 2
+
+
+def model_stage_bytes(stage: str, mode: str, H: int, W: int, D: int, P: int, sweep: bool) -> int:
+    """Share of ``model_pair_bytes`` owned by one engine stage, per pair.
+
+    Model terms per cell: cost volume written once (1 B; f32 volume read once,
+    4 B), read once per path (P x 1 B; 4 B for f32), S written once and read
+    once (2 + 2 B); per pixel: 2 images in (2 B), 2 int16 maps out (4 B).
+    A stage owns the terms of the work it does: the cost stage the volume
+    write and the image reads; each aggregation kernel the reads of the paths
+    it aggregates (+ the S write when it completes S); the WTA stage the S
+    read and the outputs.  Summed over the stages this is exactly
+    ``model_pair_bytes``.
+    """
+    cells, px = H * W * D, H * W
+    if mode == "bm":
+        return model_pair_bytes(mode, H, W, D, P) if stage in ("wta", "paths") else 0
+    vol = mode == "volume8"
+    cw, r = (4, 4) if vol else (1, 1)
+    io_in, io_out = (0, 0) if vol else (2, 4)
+    if stage == "cost":
+        return cells * cw + px * io_in
+    if not sweep:
+        if stage == "paths":
+            return cells * (P * r + 2)
+        if stage == "wta":
+            return cells * 2 + px * io_out
+        return 0
+    # fused-sweep engine: E/W lines, [down sweep S+SE+SW -> partial], last sweep (+ S write/read) + WTA
+    if stage == "horizontal":
+        return cells * 2 * r
+    if stage == "sweep":
+        return cells * 3 * r if P == 8 else 0
+    if stage == "sweep_wta":
+        return cells * (3 * r + 2 + 2) + px * io_out
+    return 0
+
+
+# ---------------------------------------------------------------------------
 def main():
     args = parse()
     if args.config is None:
         args.config = "mccnn" if args.mode == "volume8" else "kitti"
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    world = int(world_env or "1")
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} (launch N ranks for --gpus N)")
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.selftest_cpu:
+        return selftest_cpu(args, world, rank)
+
     import torch
     import torch.distributed as dist
 
     from stereo_match_amd import _lib, synthetic
-    from stereo_match_amd.batch import gather_to_root
+    from stereo_match_amd.batch import gather_to_root, shard_range
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
@@ -90,12 +200,12 @@ def main():
     if bm:
         prm = _lib.SmBmParams()
         _lib.load().sm_bm_default_params(D, 21, prm)
-    P = args.pairs_per_gpu
-    gpairs = P * world
+    gpairs = args.pairs_per_gpu * world
+    first, P = shard_range(gpairs, rank, world)
 
-    # synthetic inputs for this rank's pairs, resident in HBM before timing
+    # synthetic inputs for this rank's block of pairs, resident in HBM before timing
     lefts, rights = [], []
-    for i in range(rank * P, rank * P + P):
+    for i in range(first, first + P):
         l, r, _ = synthetic.random_dot_pair(H, W, D, seed=1000 + i)
         lefts.append(l)
         rights.append(r)
@@ -117,12 +227,13 @@ def main():
     eng = _lib.Engine(local_rank)
     stream = torch.cuda.current_stream(dev)
     eng.set_stream(stream.cuda_stream)
-    flags = 32 if args.row else 0
-    flags |= {"auto": 0, "perdir": 4096, "sweep": 16384}[args.engine]
+    flags = {"auto": 0, "perdir": 4096, "sweep": 16384}[args.engine]
     if flags:
         eng.set_debug_flags(flags)
+    gather = world > 1 and not args.no_gather
+    gather_events = []
 
-    def step():
+    def step(timed=False):
         if full:
             eng.compute_disparity_batch_device(dL.data_ptr(), dR.data_ptr(), P, H * W, H, W, W, prm, wprm,
                                                dOut.data_ptr(), dOutR.data_ptr(), dFilt.data_ptr())
@@ -133,35 +244,43 @@ def main():
                                           dOut.data_ptr())
         else:
             eng.compute_batch_device(dL.data_ptr(), dR.data_ptr(), P, H * W, H, W, W, prm, dOut.data_ptr())
-        if world > 1 and not args.no_gather:
+        if gather:
+            if timed:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
             gather_to_root(dOut, gpairs)
+            if timed:
+                e1 = torch.cuda.Event(enable_timing=True)
+                e1.record(stream)
+                gather_events.append((e0, e1))
 
     for _ in range(args.warmup):
         step()
+    eng.synchronize()  # device-side failures (sweep hand-off timeouts) fail the run here
     torch.cuda.synchronize(dev)
     eng.set_timing(True)
     eng.reset_timing()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    ev0.record(stream)
     for _ in range(args.steps):
-        step()
-    ev1.record(stream)
+        step(timed=True)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
+    eng.synchronize()
     elapsed = t1 - t0
     stages = eng.timing()
     eng.set_timing(False)
+    gather_ms = sum(a.elapsed_time(b) for a, b in gather_events)
     if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed, gather_ms], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed, gather_ms_max = float(t[0].item()), float(t[1].item())
+    else:
+        gather_ms_max = 0.0
 
     # correctness spot check of the last step (cheap, outside the timed region)
     out0 = dOut[0].cpu().numpy()
@@ -169,75 +288,27 @@ def main():
 
     if rank == 0:
         K = args.steps
-        pairs_total = gpairs * K
-        value = pairs_total / elapsed
+        value = gpairs * K / elapsed
         cells = H * W * D
-        width1 = W - D
-        vol = H * width1 * D
         P_dirs = 5 if args.mode in ("sgbm5", "disparity5") else 8
-        eb = 1 if args.mode == "census8" else 2  # bytes per path element
-        row_mode = args.row and D % 64 == 0  # both horizontal paths fused into the row/WTA kernel
-        # census mode: the path kernel reads the precomputed u8 Hamming cost volume
-        # once per direction (k_census_cost8), like the u16 cost volume in SGBM mode
-        census_b = 0
-        if row_mode:
-            # paths launch: vertical family only; row kernel: E (+W) paths + WTA
-            paths_bytes = (P_dirs - 2) * vol * eb + (census_b or (P_dirs - 2) * vol * eb)
-            wta_bytes = vol * eb + (P_dirs - 1) * vol * eb + (census_b or 2 * vol * 2) + 2 * H * W
-            wta_name = "k_row_wta (E/W paths + WTA + disp2/LR, one wave per row)"
-        else:
-            paths_bytes = P_dirs * vol * eb + (census_b or P_dirs * vol * eb)
-            wta_bytes = P_dirs * vol * eb + 2 * H * W
-            wta_name = "k_wta"
-        if bm:  # SAD kernel reads the two prefiltered views, writes disparity (+ int32 cost)
-            wta_name, wta_bytes = "k_bm_sad (column sums in LDS + WTA)", H * W * (2 + 2 + 4)
-        kern = {"paths": ("k_sgm_paths (vertical family)" if row_mode else "k_sgm_paths (all directions)",
-                          paths_bytes),
-                "wta": (wta_name, wta_bytes)}
-        cands = ("paths", "wta")
-        if stages["sweep_wta"][1] > 0:  # fused-sweep engine (sm_sweep.hpp): its kernels have stages of their own
-            rec_b = 8 * H * width1  # WTA winner record + sub-pixel inputs per pixel
-            kern = {"horizontal": ("k_sgm_paths (E/W lines only)", 4 * vol * eb),
-                    "sweep": ("k_sweep down (S+SE+SW -> u16 partial)", vol * eb + 2 * vol),
-                    "sweep_wta": ("k_sweep " + ("up (N+NE+NW" if P_dirs == 8 else "down (S+SE+SW")
-                                  + " + E + W" + (" + partial" if P_dirs == 8 else "") + " + WTA)",
-                                  3 * vol * eb + (2 * vol if P_dirs == 8 else 0) + rec_b)}
-            cands = tuple(k for k in ("horizontal", "sweep", "sweep_wta") if stages[k][1] > 0)
+        sweep = stages["sweep_wta"][1] > 0  # fused-sweep engine ran (its stages have launches)
+        kern, cands = design_kernels(args, stages, H, W, D, p, P_dirs, sweep, bm)
         # dominant kernel = the stage with the largest device time
         dom = max(cands, key=lambda k: stages[k][0])
         dom_ms, dom_launches, dom_pairs = stages[dom]
-        paths_avg_s = dom_ms / 1e3 / max(dom_launches, 1)
+        launch_s = dom_ms / 1e3 / max(dom_launches, 1)
         pairs_per_launch = dom_pairs / max(dom_launches, 1)
-        alg_bytes_paths = kern[dom][1] * pairs_per_launch
-        achieved = alg_bytes_paths / paths_avg_s / 1e9 if paths_avg_s > 0 else None
-        traffic = None
-        if os.path.exists(args.traffic_file):
-            try:
-                with open(args.traffic_file) as f:
-                    tr = json.load(f)
-                if tr.get("config") == args.config and tr.get("mode") == args.mode:
-                    st = tr.get("stages", {}).get(dom, {})
-                    # per launch of the same pairs-per-launch as this run
-                    if st and tr.get("pairs_per_launch", pairs_per_launch) == pairs_per_launch:
-                        traffic = st.get("hbm_bytes_per_launch")
-            except (OSError, ValueError):
-                traffic = None
-        # SURVEY.md §8(d) whole-pipeline model: H·W·D·(1+P+4) + 2HW + 4HW per pair
-        # (mc-cnn f32 volume: H·W·D·(4·P + 8))
-        if volume:
-            survey_bytes = cells * (4 * P_dirs + 8)
-        elif bm:  # no volume: images in, prefiltered views, disparity + cost out
-            survey_bytes = H * W * (2 + 2 * 2 + 2 + 4)
-        elif full:  # two matcher runs (left, right) per pair; WLS traffic is O(H·W)
-            survey_bytes = 2 * (cells * (1 + P_dirs + 4) + 2 * H * W + 4 * H * W)
-        else:
-            survey_bytes = cells * (1 + P_dirs + 4) + 2 * H * W + 4 * H * W
+        alg_bytes = model_stage_bytes(dom, args.mode, H, W, D, P_dirs, sweep) * pairs_per_launch
+        design_bytes = kern[dom][1] * pairs_per_launch
+        achieved = alg_bytes / launch_s / 1e9 if launch_s > 0 else None
+        traffic, traffic_note = read_traffic(args, dom, kern[dom][0], pairs_per_launch, sweep)
+        survey_bytes = model_pair_bytes(args.mode, H, W, D, P_dirs) * (2 if full else 1)
         tot_ms, _, tot_pairs = stages["total"]
         pair_s = tot_ms / 1e3 / max(tot_pairs, 1)
         if full:  # per reference pair: two matcher calls + the WLS filter
             pair_s = (tot_ms + stages["wls"][0]) / 1e3 / max(stages["wls"][2], 1)
         line = {
-            "metric": "stereo pairs/sec + Mpix·disp/sec, KITTI 1242×375 D=128 SGM, 1/2/4/8 GPU",
+            "metric": METRIC,
             "value": value,
             "unit": "pairs/s",
             "n_gpus": world,
@@ -252,16 +323,15 @@ def main():
             "data": "synthetic random-dot pairs (no dataset in the image)"
                     + ("; f32 cost = 3x3-smoothed |L-R|/255 volume per pair" if volume else ""),
             "config": {
-                "engine": {"auto": "per-direction (census 8 paths) / fused sweeps (otherwise)", "perdir": "per-direction",
-                           "sweep": "fused sweeps"}[args.engine],
+                "engine": "fused sweeps" if sweep else "per-direction",
                 "workload": f"{args.config} {W}x{H} D={D} "
                             + {"census8": "census9x7 + 8-path SGM", "sgbm5": "OpenCV-SGBM 5-path",
                                "sgbm8": "OpenCV-SGBM 8-path (MODE_HH)",
                                "volume8": "f32 cost volume (mc-cnn) + 8-path SGM",
                                "disparity5": "compute_disparity: left+right OpenCV-SGBM 5-path + WLS",
                                "bm": "OpenCV StereoBM blockSize 21 (X-Sobel prefilter)"}[args.mode],
-                "pairs_per_gpu": P, "global_batch": gpairs, "H": H, "W": W, "D": D,
-                "gather": world > 1 and not args.no_gather, "parallelism": f"pairs/dp{world}",
+                "pairs_per_gpu": args.pairs_per_gpu, "global_batch": gpairs, "H": H, "W": W, "D": D,
+                "gather": gather, "parallelism": f"pairs/dp{world}",
             },
             "mpix_disp_per_s": value * cells / 1e6,
             "roofline": {
@@ -272,9 +342,14 @@ def main():
                 "unit": "GB/s",
                 "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                 "traffic": traffic,
-                "alg_bytes_per_launch": alg_bytes_paths,
+                "alg_bytes_per_launch": alg_bytes,
+                "alg_model": "SURVEY §8d bytes owned by this stage (bench.model_stage_bytes)",
+                "design_bytes_per_launch": design_bytes,
+                "design_achieved_GBs": design_bytes / launch_s / 1e9 if launch_s > 0 else None,
+                "traffic_over_alg": (traffic / alg_bytes) if traffic and alg_bytes else None,
+                "traffic_note": traffic_note,
                 "pairs_per_launch": pairs_per_launch,
-                "avg_launch_us": paths_avg_s * 1e6,
+                "avg_launch_us": launch_s * 1e6,
             },
             "pipeline_roofline": {
                 "model": "SURVEY §8d " + ("H·W·D·(4P+8)" if volume else "H·W·(2+4+2+4) (no volume)" if bm
@@ -288,22 +363,144 @@ def main():
             "stage_us_per_pair": {k: v[0] * 1e3 / max(v[2], 1) for k, v in stages.items()},
             "valid_frac_pair0": valid_frac,
         }
+        if world > 1:
+            line["distributed"] = {
+                "backend": dist.get_backend(), "world_size": dist.get_world_size(),
+                "gather_ms_per_step_rank0": gather_ms / K, "gather_ms_per_step_max": gather_ms_max / K,
+                "gather_bytes_to_root": gpairs * H * W * 2,
+                "compute_ms_per_step": (elapsed * 1e3 - gather_ms) / K,
+            }
+        if world == 1 and args.host_surface_calls > 0 and args.config == "kitti":
+            line["host_surface"] = host_surface(args, local_rank)
         if world == 1 and args.cpu_baseline_pairs > 0:
-            line["cpu_baseline"] = cpu_baseline(args, H, W, D, p, lefts, rights, out0, volume, full)
+            line["cpu_baseline"] = cpu_baseline(args, H, W, D, p, lefts, rights, out0, volume, full,
+                                                line.get("host_surface"))
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
-def cpu_baseline(args, H, W, D, p, lefts, rights, out0, volume, full=False):
+def design_kernels(args, stages, H, W, D, p, P_dirs, sweep, bm):
+    """The engine's own bytes per pair for each timed stage (what the kernels
+    move by design), and the stages that can be the dominant kernel."""
+    width1 = W - D  # minDisparity 0
+    vol = H * width1 * D
+    eb = 1 if args.mode == "census8" else 2  # bytes per path element
+    if bm:  # SAD kernel reads the two prefiltered views, writes disparity (+ int32 cost)
+        return {"paths": ("k_bm_sad (column sums in LDS + WTA)", H * W * (2 + 2 + 4)),
+                "wta": ("k_bm_sad (column sums in LDS + WTA)", H * W * (2 + 2 + 4))}, ("wta",)
+    if sweep:
+        rec_b = 8 * H * width1  # WTA winner record + sub-pixel inputs per pixel
+        kern = {"horizontal": ("k_sgm_paths (E/W lines only)", 4 * vol * eb),
+                "sweep": ("k_sweep down (S+SE+SW -> u16 partial)", vol * eb + 2 * vol),
+                "sweep_wta": ("k_sweep " + ("up (N+NE+NW" if P_dirs == 8 else "down (S+SE+SW")
+                              + " + E + W" + (" + partial" if P_dirs == 8 else "") + " + WTA)",
+                              3 * vol * eb + (2 * vol if P_dirs == 8 else 0) + rec_b)}
+        return kern, tuple(k for k in ("horizontal", "sweep", "sweep_wta") if stages[k][1] > 0)
+    # per-direction engine: one path volume per direction written, cost volume read per direction
+    kern = {"paths": ("k_sgm_paths (all directions)", 2 * P_dirs * vol * eb),
+            "wta": ("k_wta", P_dirs * vol * eb + 2 * H * W)}
+    return kern, ("paths", "wta")
+
+
+def read_traffic(args, dom, kernel_label, pairs_per_launch, sweep):
+    """HBM bytes per launch of the dominant kernel from a PMC summary
+    (tools/traffic.sh), used only when it was collected on the same sources,
+    configuration, mode and engine as this run."""
+    if not os.path.exists(args.traffic_file):
+        return None, "no traffic file"
+    try:
+        with open(args.traffic_file) as f:
+            tr = json.load(f)
+    except (OSError, ValueError):
+        return None, "unreadable traffic file"
+    want = {"config": args.config, "mode": args.mode, "engine": "sweep" if sweep else "perdir",
+            "src_sha16": source_hash(), "pairs_per_launch": pairs_per_launch}
+    for k, v in want.items():
+        if tr.get(k) != v:
+            return None, f"traffic file {os.path.relpath(args.traffic_file, ROOT)} is for {k}={tr.get(k)!r}, " \
+                         f"this run has {v!r}: dropped"
+    st = tr.get("stages", {}).get(dom)
+    if not st:
+        return None, f"traffic file has no stage {dom!r}"
+    return st.get("hbm_bytes_per_launch"), f"PMC FETCH_SIZE/WRITE_SIZE, {os.path.relpath(args.traffic_file, ROOT)}"
+
+
+def host_surface(args, device):
+    """The reference's own surface (stereo_vision/stereo_vision.py:132-184):
+    ``compute_disparity(gray_l, gray_r, settings)`` with host numpy in and
+    out, one pair per call, settings.ini values (window_size 5 -> P1 600 /
+    P2 2400, numDisparities 160, blockSize 5, lambda 80000, sigma 1.2) at KITTI
+    size: left SGBM + right SGBM + WLS, each call synchronous.  Also the
+    one-call C-ABI form (sm_compute_disparity) with its host<->device copies
+    timed apart."""
+    from stereo_match_amd import _lib, compute_disparity, settings, synthetic
+
+    s = dict(settings.DEFAULT_SETTINGS, window_size=5)  # /root/reference/settings.ini:3-23
+    H, W = synthetic.CONFIGS["kitti"][:2]
+    D = s["num_disparities"]
+    gl, gr, _ = synthetic.random_dot_pair(H, W, D, seed=77)
+    n = args.host_surface_calls
+    e = _lib.engine(device)
+    for _ in range(2):
+        compute_disparity(gl, gr, s, device=device)
+    e.set_timing(True)
+    e.reset_timing()
+    ts = []
+    for _ in range(n):
+        t0 = time.perf_counter()
+        displ, filt = compute_disparity(gl, gr, s, device=device)
+        ts.append(time.perf_counter() - t0)
+    st = e.timing()
+    e.set_timing(False)
+    # one-call C-ABI form
+    from stereo_match_amd.stereo_vision import matcher_from_settings
+    from stereo_match_amd import wls as _wls
+    lm = matcher_from_settings(s, device=device)
+    prm = lm.params()  # before createDisparityWLSFilter mutates the matcher (sm_compute_disparity applies it)
+    wf = _wls.createDisparityWLSFilter(lm)
+    wf.setLambda(s["lmbda"])
+    wf.setSigmaColor(s["sigma"])
+    wp = wf.params(H, W)
+    e.compute_disparity(gl, gr, prm, wp)
+    e.set_timing(True)
+    e.reset_timing()
+    ts1 = []
+    for _ in range(n):
+        t0 = time.perf_counter()
+        d1, f1 = e.compute_disparity(gl, gr, prm, wp)
+        ts1.append(time.perf_counter() - t0)
+    st1 = e.timing()
+    e.set_timing(False)
+    med, med1 = float(np.median(ts)), float(np.median(ts1))
+    return {
+        "what": "stereo_match_amd.compute_disparity(gray_l, gray_r, settings) = reference "
+                "stereo_vision.py:132-184: left + right SGBM (5 paths) + WLS, host numpy in/out, one pair per call",
+        "workload": f"kitti {W}x{H} D={D} settings.ini (window_size 5, blockSize 5, lambda 80000, sigma 1.2)",
+        "calls": n,
+        "value": 1.0 / med, "unit": "pairs/s", "ms_per_call_median": med * 1e3,
+        "ms_per_call_mean": float(np.mean(ts)) * 1e3,
+        "h2d_ms_per_call": st["h2d"][0] / n, "d2h_ms_per_call": st["d2h"][0] / n,
+        "device_ms_per_call": (st["total"][0] + st["wls"][0]) / n,
+        "one_call_abi": {"entry": "sm_compute_disparity", "value": 1.0 / med1, "ms_per_call_median": med1 * 1e3,
+                         "h2d_ms_per_call": st1["h2d"][0] / n, "d2h_ms_per_call": st1["d2h"][0] / n,
+                         "device_ms_per_call": (st1["total"][0] + st1["wls"][0]) / n,
+                         "same_as_python_surface": bool(np.array_equal(d1, displ) and np.array_equal(f1, filt))},
+        "_pair": (gl, gr, s, displ, filt),
+    }
+
+
+def cpu_baseline(args, H, W, D, p, lefts, rights, out0, volume, full=False, hs=None):
     """The C restatement (oracle/sgm_ref.c, -O3) on a bounded sample of the
     same workload: ``--cpu-threads`` host threads each running
     ``--cpu-baseline-pairs`` pairs concurrently (ctypes releases the GIL; the
     port is single-threaded per pair, the pairs are independent), plus the
-    one-thread rate.  Also re-checks pair 0 bit for bit."""
+    one-thread rate.  Also re-checks pair 0 bit for bit; the numpy oracle on
+    Tsukuba (BASELINE.md CPU plan step 2); and the host-surface pair through
+    the C port + numpy WLS."""
     import threading
 
-    from oracle import ref_c
+    from oracle import ref_c, sgm_np, wls_np
     from stereo_match_amd import synthetic
 
     n = args.cpu_baseline_pairs
@@ -322,11 +519,9 @@ def cpu_baseline(args, H, W, D, p, lefts, rights, out0, volume, full=False):
         def one(i):
             return bm_np.stereo_bm(lefts[i % len(lefts)], rights[i % len(rights)], bp)
     elif full:  # compute_disparity: C port for both matchers + the numpy WLS restatement
-        from oracle import sgm_np, wls_np
         lp = dict(p, uniquenessRatio=0, disp12MaxDiff=1000000)
         rp = sgm_np.right_matcher_params(p)
-        wp = dict(lmbda=80000.0, sigma=1.2, radius=(p["blockSize"] + 1) // 2, min_disp=p["minDisparity"],
-                  left_offset=max(0, p["minDisparity"] + D), right_offset=max(0, -p["minDisparity"]))
+        wp = _wls_oracle_params(p, D)
         n = max(1, n // 4)
 
         def one(i):
@@ -358,7 +553,7 @@ def cpu_baseline(args, H, W, D, p, lefts, rights, out0, volume, full=False):
         t.join()
     dtT = time.perf_counter() - t0
     what = "f32 cost volumes" if volume else ("pairs (left+right C port + numpy WLS)" if full else "pairs")
-    return {
+    out = {
         "value": T * n / dtT,
         "unit": "pairs/s",
         "cores": T,
@@ -370,6 +565,86 @@ def cpu_baseline(args, H, W, D, p, lefts, rights, out0, volume, full=False):
         "host_cpus_visible": os.cpu_count(),
         "gpu_matches_port_pair0": bool(np.array_equal(first, out0)),
     }
+    # BASELINE.md CPU plan step 2: the numpy oracle on Tsukuba (config 1), median of 5 after 1 warm-up
+    tl, tr, _ = synthetic.random_dot_pair(*synthetic.CONFIGS["tsukuba"], seed=5)
+    tp = synthetic.parity_params(16)
+    sgm_np.compute(tl, tr, tp)
+    tt = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        sgm_np.compute(tl, tr, tp)
+        tt.append(time.perf_counter() - t0)
+    out["numpy_tsukuba"] = {"value": 1.0 / float(np.median(tt)), "unit": "pairs/s", "cores": 1,
+                            "sample": "oracle/sgm_np.py, 384x288 D=16 OpenCV-SGBM 5-path (settings.ini), "
+                                      "median of 5 after 1 warm-up"}
+    if hs is not None:  # host surface: the same pair through the C port (both matchers) + numpy WLS
+        gl, gr, s, displ, filt = hs.pop("_pair")
+        Dh = s["num_disparities"]
+        hp = synthetic.parity_params(Dh, s["window_size"])
+        lp = dict(hp, uniquenessRatio=0, disp12MaxDiff=1000000)
+        t0 = time.perf_counter()
+        dl = ref_c.compute(gl, gr, lp)
+        dr = ref_c.compute(gr, gl, sgm_np.right_matcher_params(hp))
+        fl = wls_np.wls_filter(dl, gl, dr, _wls_oracle_params(hp, Dh))
+        dt = time.perf_counter() - t0
+        out["host_surface_port"] = {
+            "value": 1.0 / dt, "unit": "pairs/s", "cores": 1,
+            "sample": f"1 KITTI pair D={Dh}: oracle/sgm_ref.c left + right + oracle/wls_np.py WLS, {dt:.1f} s",
+            "gpu_matches_port": bool(np.array_equal(dl, displ) and np.array_equal(fl, filt)),
+        }
+    return out
+
+
+def _wls_oracle_params(p, D):
+    """createDisparityWLSFilter(left) defaults for the numpy WLS restatement."""
+    return dict(lmbda=80000.0, sigma=1.2, radius=(p["blockSize"] + 1) // 2, min_disp=p["minDisparity"],
+                left_offset=max(0, p["minDisparity"] + D), right_offset=max(0, -p["minDisparity"]))
+
+
+# ---------------------------------------------------------------------------
+def selftest_cpu(args, world, rank):
+    """The multi-rank plumbing of ``main`` on CPU (gloo): same sharding, same
+    gather, same max-over-ranks timing and JSON keys; the step is a stand-in
+    (left image widened to int16), so nothing here is a measurement."""
+    import torch
+    import torch.distributed as dist
+
+    from stereo_match_amd import synthetic
+    from stereo_match_amd.batch import gather_to_root, shard_range
+
+    if world > 1:
+        dist.init_process_group("gloo")
+    H, W, D = synthetic.CONFIGS[args.config]
+    gpairs = args.pairs_per_gpu * world
+    first, P = shard_range(gpairs, rank, world)
+    dL = torch.stack([torch.full((H, W), i % 251, dtype=torch.uint8) for i in range(first, first + P)])
+    gathered = None
+    gather_s = 0.0
+    for k in range(args.warmup + args.steps):
+        out = dL.to(torch.int16) * 16
+        if world > 1 and not args.no_gather:
+            tg = time.perf_counter()
+            gathered = gather_to_root(out, gpairs)
+            if k >= args.warmup:
+                gather_s += time.perf_counter() - tg
+    if world > 1:
+        dist.barrier()
+    ok = True
+    if rank == 0 and gathered is not None:
+        want = torch.stack([torch.full((H, W), (i % 251) * 16, dtype=torch.int16) for i in range(gpairs)])
+        ok = bool(torch.equal(gathered, want))
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "pairs/s", "n_gpus": world,
+                          "steps": args.steps, "warmup": args.warmup, "higher_is_better": True, "scaling": "weak",
+                          "data": "launcher self-test: gloo on CPU, stand-in step (no disparity computed)",
+                          "config": {"workload": args.config, "pairs_per_gpu": args.pairs_per_gpu,
+                                     "global_batch": gpairs, "parallelism": f"pairs/dp{world}"},
+                          "distributed": {"backend": dist.get_backend() if world > 1 else None,
+                                          "world_size": dist.get_world_size() if world > 1 else 1,
+                                          "gather_ms_per_step_rank0": gather_s * 1e3 / max(args.steps, 1),
+                                          "gathered_in_pair_order": ok}}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

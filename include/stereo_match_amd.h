@@ -213,10 +213,24 @@ int sm_compute_batch(sm_ctx** ctxs, int ngpu, const uint8_t* const* left, const 
  * (reference call: stereo_vision/stereo_vision.py:171). */
 int sm_right_matcher_params(const sm_params* left, sm_params* right_out);
 
-/* Wait for all work enqueued on the context stream; reports (and clears) a
- * device-side failure of the fused-sweep engine (a strip-boundary hand-off
- * that timed out) as SM_E_HIP.  Synchronous entry points check it themselves. */
+/* Wait for all work enqueued on the context stream.  The fused-sweep engine's
+ * strips wait on their neighbours; when one gives up (its neighbours could not
+ * be resident, e.g. other work held the CUs), the launch group is recomputed on
+ * the device by the per-direction engine, so results stay exact and the call
+ * succeeds (counted by sm_get_counters).  Only the opt-in hybrid engine reports
+ * such a give-up as SM_E_HIP here (and synchronous entry points check it). */
 int sm_synchronize(sm_ctx* ctx);
+
+/* Counters since sm_create: launch groups the fused sweeps handed to the
+ * guarded per-direction fallback.  Synchronises the context stream. */
+int sm_get_counters(sm_ctx* ctx, long long* sweep_fallbacks);
+
+/* Restrict the context's own streams (the default stream and its internal
+ * second stream) to a CU subset: mask = nwords 32-bit words, bit i = CU i
+ * (hipExtStreamCreateWithCUMask); nwords = 0 restores unmasked streams.  The
+ * fused sweeps size their co-resident launches from the CUs the stream can
+ * reach.  Waits for queued work; resets sm_set_stream to the own stream. */
+int sm_set_cu_mask(sm_ctx* ctx, const uint32_t* mask, int nwords);
 
 /* Per-stage device timing with hipEvents on the context stream.
  * stage: 0 cost, 1 path aggregation, 2 WTA+LR, 3 median, 4 whole matcher
@@ -234,7 +248,14 @@ int sm_synchronize(sm_ctx* ctx);
 #define SM_STAGE_HORIZONTAL 7
 #define SM_STAGE_SWEEP 8
 #define SM_STAGE_SWEEP_WTA 9
-#define SM_NUM_STAGES 10
+/* host-pointer entry points: host->device copies of the images, device->host
+ * copies of the maps (kept out of every other stage) */
+#define SM_STAGE_H2D 10
+#define SM_STAGE_D2H 11
+/* guarded per-direction recomputation after the fused sweeps (near zero unless a
+ * sweep strip gave up waiting for its neighbours; see sm_get_counters) */
+#define SM_STAGE_FALLBACK 12
+#define SM_NUM_STAGES 13
 int sm_set_timing(sm_ctx* ctx, int enable);
 int sm_get_timing(sm_ctx* ctx, int stage, double* total_ms, long long* launches, long long* pairs);
 int sm_reset_timing(sm_ctx* ctx);

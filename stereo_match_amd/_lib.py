@@ -21,7 +21,8 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "stereo_match_amd.
 SM_OK, SM_E_ARG, SM_E_HIP, SM_E_UNSUPPORTED = 0, -1, -2, -4
 SM_COST_SGBM, SM_COST_CENSUS, SM_COST_VOLUME = 0, 1, 2
 SM_MODE_SGBM, SM_MODE_HH = 5, 8
-STAGES = ("cost", "paths", "wta", "median", "total", "wls", "speckle", "horizontal", "sweep", "sweep_wta")
+STAGES = ("cost", "paths", "wta", "median", "total", "wls", "speckle", "horizontal", "sweep", "sweep_wta", "h2d",
+          "d2h", "fallback")
 
 
 class SmParams(ctypes.Structure):
@@ -106,6 +107,8 @@ _SIGS = {
                                     _c.c_void_p]),
     "sm_right_matcher_params": (_c.c_int, [_c.POINTER(SmParams), _c.POINTER(SmParams)]),
     "sm_synchronize": (_c.c_int, [_c.c_void_p]),
+    "sm_get_counters": (_c.c_int, [_c.c_void_p, _c.POINTER(_c.c_longlong)]),
+    "sm_set_cu_mask": (_c.c_int, [_c.c_void_p, _c.POINTER(_c.c_uint32), _c.c_int]),
     "sm_set_timing": (_c.c_int, [_c.c_void_p, _c.c_int]),
     "sm_get_timing": (_c.c_int, [_c.c_void_p, _c.c_int, _c.POINTER(_c.c_double), _c.POINTER(_c.c_longlong),
                                  _c.POINTER(_c.c_longlong)]),
@@ -369,6 +372,23 @@ class Engine:
 
     def synchronize(self):
         self._check(self._lib.sm_synchronize(self.ctx))
+
+    def counters(self) -> dict:
+        """{"sweep_fallbacks": launch groups recomputed by the guarded fallback}"""
+        n = ctypes.c_longlong()
+        self._check(self._lib.sm_get_counters(self.ctx, ctypes.byref(n)))
+        return {"sweep_fallbacks": n.value}
+
+    def set_cu_mask(self, cus):
+        """Restrict the context's streams to the CU indices in ``cus`` (None: all)."""
+        if cus is None:
+            self._check(self._lib.sm_set_cu_mask(self.ctx, None, 0))
+            return
+        nwords = (max(cus) // 32 + 1) if cus else 1
+        words = (ctypes.c_uint32 * nwords)()
+        for c in cus:
+            words[c // 32] |= 1 << (c % 32)
+        self._check(self._lib.sm_set_cu_mask(self.ctx, words, nwords))
 
     # -- timing ---------------------------------------------------------------
     def set_timing(self, on: bool):

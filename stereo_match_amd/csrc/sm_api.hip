@@ -70,6 +70,15 @@ constexpr int DBG_VL16 = 8, DBG_STORE_W = 16, DBG_ROW = 32, DBG_OVERLAP = 64, DB
 // 4096: per-direction engine (one path volume per direction + k_wta) instead of the fused sweeps
 constexpr int DBG_LEGACY = 4096, DBG_SWEEP1 = 8192, DBG_SWEEP8 = 16384, DBG_HYBRID = 32768;
 constexpr int DBG_COST_TILE = 1 << 22;
+// 1 << 23 (valid results): raise every fused-sweep group's give-up flag, so the
+// guarded per-direction fallback recomputes the group (tests the recovery path)
+constexpr int DBG_FORCE_FALLBACK = 1 << 23;
+// words of ctx->sweep_err: per-buffer-set group flags (set by a sweep strip that gave
+// up waiting; cleared by the host before each group), the sticky error of the
+// (unguarded) hybrid engine, and the count of fallback recomputations
+constexpr int ERR_GROUP0 = 0, ERR_STICKY = 32, ERR_FALLBACKS = 48;
+// timing ablation: no guarded fallback launches after the sweeps
+constexpr int DBG_NO_FALLBACK = (int)0x80000000u;
 
 }  // namespace
 
@@ -81,8 +90,12 @@ struct sm_ctx {
     DevBuf img[2], planes, out, dbg, volbuf, sp_parent, sp_count, rp_in, rp_out, rp_min, bm_pre[2], bm_cost;
     DevBuf wls_num, wls_den, wls_inter, wls_w, wls_disp[2], wls_out;  // WLS scratch
     DevBuf hop, sweep_err;  // sweep engine: strip-boundary granules, device error word
+    void* pin = nullptr;    // page-locked host staging of the host-pointer entry points (HostStage)
+    size_t pin_n = 0;
     uint32_t hop_epoch = 0;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;  // sweep engine: E/W kernel on the side stream
+    const uint32_t* fb_guard = nullptr;  // set while enqueuing a group's guarded per-direction fallback
+    hipStream_t wta_override = nullptr;  // stream of the WTA launch when it is not stream_b()
     BufSet set[2];
     int next_set = 0;
     // geometry of the last computation (for sm_debug_fetch): its last pair
@@ -233,6 +246,71 @@ void harvest_timing(sm_ctx* ctx)
     ctx->pending.clear();
 }
 
+// Page-locked staging for the host-pointer entry points: inputs are packed row
+// by row into pinned memory and cross PCIe as one DMA each (a pageable
+// hipMemcpy2D moves one row per transfer: ~3 ms for a KITTI image); outputs
+// land in pinned memory and are copied out once the stream has synchronised.
+// The whole call's bytes are reserved up front, so the buffer never moves
+// while a DMA of this call is queued (host entry points are synchronous, so
+// nothing of a previous call is in flight either).
+struct HostStage {
+    struct Out {
+        void* dst;
+        size_t off, bytes;
+    };
+    sm_ctx* ctx;
+    size_t used = 0;
+    std::vector<Out> outs;
+    explicit HostStage(sm_ctx* c) : ctx(c) {}
+    int reserve(size_t bytes)
+    {
+        if (ctx->pin_n >= bytes && ctx->pin) return SM_OK;
+        if (ctx->pin) {
+            HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+            (void)hipHostFree(ctx->pin);
+            ctx->pin = nullptr;
+            ctx->pin_n = 0;
+        }
+        HIP_TRY(ctx, hipHostMalloc(&ctx->pin, bytes, hipHostMallocDefault));
+        ctx->pin_n = bytes;
+        return SM_OK;
+    }
+    uint8_t* take(size_t bytes)
+    {
+        uint8_t* p = (uint8_t*)ctx->pin + used;
+        used += (bytes + 255) & ~size_t(255);
+        return p;
+    }
+    // rows x row_bytes from host (pitch src_pitch) -> contiguous device buffer
+    int in(void* dev, const void* src, size_t rows, size_t row_bytes, size_t src_pitch)
+    {
+        uint8_t* p = take(rows * row_bytes);
+        if (src_pitch == row_bytes)
+            std::memcpy(p, src, rows * row_bytes);
+        else
+            for (size_t r = 0; r < rows; r++) std::memcpy(p + r * row_bytes, (const uint8_t*)src + r * src_pitch, row_bytes);
+        StageTimer t(ctx, ctx->stream, SM_STAGE_H2D, 1);
+        HIP_TRY(ctx, hipMemcpyAsync(dev, p, rows * row_bytes, hipMemcpyHostToDevice, ctx->stream));
+        return SM_OK;
+    }
+    int out(void* dst, const void* dev, size_t bytes)
+    {
+        uint8_t* p = take(bytes);
+        outs.push_back({dst, (size_t)(p - (uint8_t*)ctx->pin), bytes});
+        StageTimer t(ctx, ctx->stream, SM_STAGE_D2H, 1);
+        HIP_TRY(ctx, hipMemcpyAsync(p, dev, bytes, hipMemcpyDeviceToHost, ctx->stream));
+        return SM_OK;
+    }
+    int finish()
+    {
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        for (const Out& o : outs) std::memcpy(o.dst, (const uint8_t*)ctx->pin + o.off, o.bytes);
+        return SM_OK;
+    }
+};
+// staged bytes of n buffers of `bytes` each (256-byte slots)
+inline size_t stage_bytes(size_t bytes, int n = 1) { return (size_t)n * ((bytes + 255) & ~size_t(255)); }
+
 int grid_for(size_t n)
 {
     size_t g = (n + 255) / 256;
@@ -285,7 +363,10 @@ bool use_cost8(const sm_ctx* ctx, const Norm& n)
 {
     return n.cost == SM_COST_CENSUS && !(ctx->dbg_flags & DBG_NO_C8) && n.D <= 256;
 }
-hipStream_t stream_b(const sm_ctx* ctx) { return overlap(ctx) ? ctx->side : ctx->stream; }
+hipStream_t stream_b(const sm_ctx* ctx)
+{
+    return ctx->wta_override ? ctx->wta_override : overlap(ctx) ? ctx->side : ctx->stream;
+}
 
 // ---- stream A: path aggregation -------------------------------------------
 template <int DPLV, bool CENSUS, int VL, bool H16 = false>
@@ -345,9 +426,22 @@ int launch_paths_t(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs, int dir
         blocks = mx * pa.nv;
     }
     if (g.G % 8) pa.dbg &= ~(1 << 20);  // XCD-aware pair mapping needs whole XCD rounds
-    StageTimer t(ctx, ctx->stream, dirset == DIRS_EW ? SM_STAGE_HORIZONTAL : SM_STAGE_PATHS, g.G);
-    hipLaunchKernelGGL((smk::k_sgm_paths<VL, DPLV * 16 / VL, LANESH, DPLH, CENSUS, LT>),
-                       dim3(2 * pa.hblocks + blocks, g.G), dim3(256), 0, ctx->stream, pa);
+    dim3 grid(2 * pa.hblocks + blocks, g.G);
+    if (ctx->fb_guard) {  // guarded fallback: a small grid that walks every block if the sweep gave up
+        pa.dbg &= ~((1 << 20) | (1 << 21));
+        pa.guard = ctx->fb_guard;
+        pa.nblocks = (int)grid.x;
+        pa.npairs = g.G;
+        grid = dim3(std::min<unsigned>(grid.x * g.G, 512u), 1);
+    }
+    StageTimer t(ctx, ctx->stream,
+                 ctx->fb_guard ? SM_STAGE_FALLBACK : dirset == DIRS_EW ? SM_STAGE_HORIZONTAL : SM_STAGE_PATHS, g.G);
+    if (ctx->fb_guard)
+        hipLaunchKernelGGL((smk::k_sgm_paths<VL, DPLV * 16 / VL, LANESH, DPLH, CENSUS, LT, true>), grid, dim3(256), 0,
+                           ctx->stream, pa);
+    else
+        hipLaunchKernelGGL((smk::k_sgm_paths<VL, DPLV * 16 / VL, LANESH, DPLH, CENSUS, LT>), grid, dim3(256), 0,
+                           ctx->stream, pa);
     HIP_TRY(ctx, hipGetLastError());
     return SM_OK;
 }
@@ -358,9 +452,9 @@ int launch_wta_t(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs)
 {
     using LT = typename std::conditional<CENSUS, uint8_t, uint16_t>::type;
     constexpr int D = 16 * DPLV;
-    StageTimer t(ctx, stream_b(ctx), SM_STAGE_WTA, g.G);
+    StageTimer t(ctx, stream_b(ctx), ctx->fb_guard ? SM_STAGE_FALLBACK : SM_STAGE_WTA, g.G);
     if constexpr (D % 64 == 0) {
-        if (row_mode(ctx, n)) {
+        if (row_mode(ctx, n) && !ctx->fb_guard) {
             smk::RowArgs ra{};
             ra.cl = (const uint64_t*)bs.census[0].p;
             ra.cr = (const uint64_t*)bs.census[1].p;
@@ -407,7 +501,17 @@ int launch_wta_t(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs)
     wa.uniq = n.uniq;
     wa.disp12 = n.disp12;
     wa.disp = (int16_t*)bs.raw.p;
-    hipLaunchKernelGGL((smk::k_wta<DPLV, LT, 1024>), dim3(g.H, g.G), dim3(1024), (size_t)g.W * 8, stream_b(ctx), wa);
+    dim3 grid(g.H, g.G);
+    if (ctx->fb_guard) {
+        wa.guard = ctx->fb_guard;
+        wa.fallbacks = (uint32_t*)ctx->sweep_err.p + ERR_FALLBACKS;
+        wa.npairs = g.G;
+        grid = dim3(std::min(g.H * g.G, 256), 1);
+    }
+    if (ctx->fb_guard)
+        hipLaunchKernelGGL((smk::k_wta<DPLV, LT, 1024, true>), grid, dim3(1024), (size_t)g.W * 8, stream_b(ctx), wa);
+    else
+        hipLaunchKernelGGL((smk::k_wta<DPLV, LT, 1024>), grid, dim3(1024), (size_t)g.W * 8, stream_b(ctx), wa);
     HIP_TRY(ctx, hipGetLastError());
     return SM_OK;
 }
@@ -494,8 +598,29 @@ struct SweepJob {
     size_t part_pair;
     uint32_t* key2;
     uint32_t* pre;  // sub-pixel inputs (SweepArgs::nb)
+    uint32_t* err;  // word a strip sets when it gives up waiting for a neighbour
     int G;
 };
+
+// CUs the stream may run on: its CU mask (sm_set_cu_mask), the whole device when unmasked
+int stream_cus(hipStream_t st, int ncu)
+{
+    uint32_t mask[32] = {0};
+    const uint32_t words = (uint32_t)std::min(32, (ncu + 31) / 32);
+    if (hipExtStreamGetCUMask(st, words, mask) != hipSuccess) return ncu;
+    int c = 0;
+    for (uint32_t i = 0; i < words; i++) c += __builtin_popcount(mask[i]);
+    return c > 0 ? std::min(c, ncu) : ncu;
+}
+
+int ensure_sweep_err(sm_ctx* ctx)
+{
+    if (ctx->sweep_err.p) return SM_OK;
+    int rc = ensure(ctx, ctx->sweep_err, 256);
+    if (rc != SM_OK) return rc;
+    HIP_TRY(ctx, hipMemsetAsync(ctx->sweep_err.p, 0, 256, ctx->stream));
+    return SM_OK;
+}
 
 // one sweep pass (MODE 0/1/2, sm_sweep.hpp) over the job's G pairs, in launches
 // whose workgroups are all co-resident (strips of a pair wait on each other)
@@ -507,10 +632,11 @@ int sweep_pass(sm_ctx* ctx, const Norm& n, const Geo& g, const SweepJob& j, int 
         return fail(ctx, SM_E_UNSUPPORTED, "sweep: numDisparities %d not built", n.D);
     int ncu = 0;
     HIP_TRY(ctx, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    ncu = stream_cus(ctx->stream, std::max(ncu, 1));  // a CU-masked stream only reaches its CUs
     // the API's answer can be one block per CU high at >= 82 SGPRs (MI355X guide);
     // for 512-thread blocks SGPRs allow >= 3 per CU, so a margin is kept only above 2
     const int per_cu = si.blocks_per_cu >= 3 ? si.blocks_per_cu - 1 : std::max(si.blocks_per_cu, 1);
-    const int cap = per_cu * std::max(ncu, 1);
+    const int cap = per_cu * ncu;
     const int nwg = (n.width1 + si.cw - 1) / si.cw;
     const int nblk = (g.H + si.hb - 1) / si.hb;
     if (nwg > cap) return fail(ctx, SM_E_UNSUPPORTED, "sweep: %d strips exceed %d resident workgroups", nwg, cap);
@@ -525,10 +651,7 @@ int sweep_pass(sm_ctx* ctx, const Norm& n, const Geo& g, const SweepJob& j, int 
         HIP_TRY(ctx, hipMemsetAsync(ctx->hop.p, 0, ctx->hop.n, ctx->stream));
         ctx->hop_epoch = 0;
     }
-    if (!ctx->sweep_err.p) {
-        if ((rc = ensure(ctx, ctx->sweep_err, 256)) != SM_OK) return rc;
-        HIP_TRY(ctx, hipMemsetAsync(ctx->sweep_err.p, 0, 256, ctx->stream));
-    }
+    if ((rc = ensure_sweep_err(ctx)) != SM_OK) return rc;
     for (int p0 = 0; p0 < j.G; p0 += per_launch) {
         const int np = std::min(per_launch, j.G - p0);
         if (++ctx->hop_epoch > 0xFFFFu) {  // tags repeat: clear the granules once per 65535 launches
@@ -547,7 +670,7 @@ int sweep_pass(sm_ctx* ctx, const Norm& n, const Geo& g, const SweepJob& j, int 
         a.hop_pair = hop_pair;
         a.rec = j.key2 ? j.key2 + (size_t)p0 * g.H * g.W : nullptr;
         a.nb = j.pre ? j.pre + (size_t)p0 * g.H * g.W : nullptr;
-        a.err = (uint32_t*)ctx->sweep_err.p;
+        a.err = j.err;
         a.H = g.H;
         a.W = g.W;
         a.W1 = n.width1;
@@ -577,7 +700,7 @@ struct StreamSwap {
 // E/W volumes -> [down sweep partial] -> WTA sweep -> LR check into bs.raw.  With
 // wta_stream != ctx->stream (5 paths, two-stream overlap) the WTA sweep and the
 // LR pass run there, beside the next launch group's cost + E/W on ctx->stream.
-int run_sweep(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs, hipStream_t wta_stream)
+int run_sweep(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs, hipStream_t wta_stream, uint32_t* err)
 {
     const int G = g.G;
     int rc;
@@ -593,22 +716,18 @@ int run_sweep(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs, hipStream_t 
     if ((rc = ensure(ctx, bs.pre, (size_t)G * g.H * g.W * 4)) != SM_OK) return rc;
     j.key2 = (uint32_t*)bs.key2.p;
     j.pre = (uint32_t*)bs.pre.p;
+    j.err = err;
     {
         StageTimer t(ctx, ctx->stream, SM_STAGE_PATHS, G);
         if (n.ndirs == 8) {
             // 8 paths: the E/W kernel (latency-bound serial rows) runs on the side
             // stream beside the down sweep (latency-bound serial columns); the
-            // WTA sweep needs both
+            // WTA sweep needs both.  The sweep is enqueued first, so that its strips
+            // (which wait on each other) are dispatched before the E/W workgroups
+            // fill the CUs; E/W waits for the cost volume only.
             if ((rc = ensure_event(ctx, ctx->ev_fork)) != SM_OK) return rc;
             if ((rc = ensure_event(ctx, ctx->ev_join)) != SM_OK) return rc;
             HIP_TRY(ctx, hipEventRecord(ctx->ev_fork, ctx->stream));
-            HIP_TRY(ctx, hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
-            const hipStream_t main = ctx->stream;
-            ctx->stream = ctx->side;
-            rc = dispatch(ctx, n, g, bs, DISPATCH_HORIZONTAL);
-            ctx->stream = main;
-            if (rc != SM_OK) return rc;
-            HIP_TRY(ctx, hipEventRecord(ctx->ev_join, ctx->side));
             if ((rc = ensure(ctx, bs.part, (size_t)G * g.vol * 2)) != SM_OK) return rc;
             j.part = (uint16_t*)bs.part.p;
             j.part_pair = g.vol * 2;
@@ -616,6 +735,13 @@ int run_sweep(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs, hipStream_t 
                 StageTimer ts(ctx, ctx->stream, SM_STAGE_SWEEP, G);
                 if ((rc = sweep_pass(ctx, n, g, j, 0)) != SM_OK) return rc;
             }
+            HIP_TRY(ctx, hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
+            const hipStream_t main = ctx->stream;
+            ctx->stream = ctx->side;
+            rc = dispatch(ctx, n, g, bs, DISPATCH_HORIZONTAL);
+            ctx->stream = main;
+            if (rc != SM_OK) return rc;
+            HIP_TRY(ctx, hipEventRecord(ctx->ev_join, ctx->side));
             HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
         } else if ((rc = dispatch(ctx, n, g, bs, DISPATCH_HORIZONTAL)) != SM_OK) {
             return rc;
@@ -645,6 +771,8 @@ int run_hybrid(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs)
     j.cost = (const uint8_t*)bs.cost.p;
     j.cost_pair = g.vol * elem_bytes(n);
     j.G = G;
+    if ((rc = ensure_sweep_err(ctx)) != SM_OK) return rc;
+    j.err = (uint32_t*)ctx->sweep_err.p + ERR_STICKY;  // no fallback here: a give-up is an error
     if ((rc = ensure(ctx, bs.part, (size_t)G * g.vol * 2)) != SM_OK) return rc;
     j.part = (uint16_t*)bs.part.p;
     j.part_pair = g.vol * 2;
@@ -668,14 +796,16 @@ int run_hybrid(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs)
     return SM_OK;
 }
 
-// device-side error word of the sweep engine (boundary poll timeout); clears it
+// sticky device-side error of the unguarded (hybrid) sweep use; clears it.  The
+// default sweep engine recovers on the device instead (run_group's fallback).
 int check_sweep_errors(sm_ctx* ctx)
 {
     if (!ctx->sweep_err.p) return SM_OK;
     uint32_t e = 0;
-    HIP_TRY(ctx, hipMemcpy(&e, ctx->sweep_err.p, 4, hipMemcpyDeviceToHost));
+    uint32_t* w = (uint32_t*)ctx->sweep_err.p + ERR_STICKY;
+    HIP_TRY(ctx, hipMemcpy(&e, w, 4, hipMemcpyDeviceToHost));
     if (e) {
-        HIP_TRY(ctx, hipMemset(ctx->sweep_err.p, 0, 4));
+        HIP_TRY(ctx, hipMemset(w, 0, 4));
         return fail(ctx, SM_E_HIP, "sweep: strip-boundary hand-off timed out (workgroups not co-resident?)");
     }
     return SM_OK;
@@ -918,7 +1048,26 @@ int run_group(sm_ctx* ctx, const Src& src, const Geo& g, const Norm& n, int16_t*
         // 5 paths: the WTA sweep of this group overlaps the next group's cost + E/W
         // (the 8-path sweeps keep the second stream for their E/W fork)
         const hipStream_t ws = n.ndirs == 5 ? stream_b(ctx) : ctx->stream;
-        if ((rc = run_sweep(ctx, n, g, bs, ws)) != SM_OK) return rc;
+        if ((rc = ensure_sweep_err(ctx)) != SM_OK) return rc;
+        uint32_t* gflag = (uint32_t*)ctx->sweep_err.p + ERR_GROUP0 + s;
+        HIP_TRY(ctx, hipMemsetAsync(gflag, 0, 4, ctx->stream));
+        if ((rc = run_sweep(ctx, n, g, bs, ws, gflag)) != SM_OK) return rc;
+        // Strips of a sweep wait on their neighbours, so all of a launch's strips must be
+        // resident together; the grid is sized for that (sweep_pass), but work on other
+        // streams or processes can take the slots.  A strip that gives up raises the
+        // group flag, and this guarded per-direction launch pair (a small grid that exits
+        // at once while the flag is clear) then recomputes the whole group into bs.raw.
+        if (!(ctx->dbg_flags & DBG_NO_FALLBACK)) {
+            if (ctx->dbg_flags & DBG_FORCE_FALLBACK) HIP_TRY(ctx, hipMemsetAsync(gflag, 1, 1, ws));
+            StreamSwap sw(ctx, ws);
+            ctx->wta_override = ws;
+            ctx->fb_guard = gflag;
+            rc = dispatch(ctx, n, g, bs, DISPATCH_PATHS);
+            if (rc == SM_OK) rc = dispatch(ctx, n, g, bs, DISPATCH_WTA);
+            ctx->fb_guard = nullptr;
+            ctx->wta_override = nullptr;
+            if (rc != SM_OK) return rc;
+        }
     } else if (g.hybrid) {
         if ((rc = run_hybrid(ctx, n, g, bs)) != SM_OK) return rc;
     } else if ((rc = dispatch(ctx, n, g, bs, DISPATCH_PATHS)) != SM_OK) {
@@ -969,8 +1118,9 @@ int run_pairs(sm_ctx* ctx, const Src& src, int npairs, int H, int W, int stride,
     g.slot_bytes = (g.vol * elem_bytes(n) + 255) & ~size_t(255);
     g.hybrid = use_hybrid(ctx, n, H);
     g.sweep = !g.hybrid && use_sweep(ctx, n, H);
-    // sweep engine keeps only the E and W volumes, the hybrid E, W (+ NE, N, NW at 8 paths)
-    g.L_pair = g.slot_bytes * (g.sweep ? 2 : g.hybrid ? hybrid_slots(n) : n.ndirs);
+    // sweep engine: E and W volumes in slots 0/1 plus room for every direction's volume
+    // (written only by the guarded fallback); hybrid: E, W (+ NE, N, NW at 8 paths)
+    g.L_pair = g.slot_bytes * (g.hybrid ? hybrid_slots(n) : n.ndirs);
     g.census_pair = (size_t)H * W;
     g.cost_pair = n.cost == SM_COST_CENSUS ? 0 : g.vol;
     ctx->last_ndirs = g.sweep ? 2 : g.hybrid ? hybrid_slots(n) : n.ndirs;
@@ -1322,6 +1472,7 @@ void sm_destroy(sm_ctx* ctx)
         (void)hipEventDestroy(t.b);
     }
     for (auto e : ctx->free_events) (void)hipEventDestroy(e);
+    if (ctx->pin) (void)hipHostFree(ctx->pin);
     if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
     if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
     if (ctx->side) (void)hipStreamDestroy(ctx->side);
@@ -1402,15 +1553,17 @@ int sm_compute(sm_ctx* ctx, const uint8_t* L, const uint8_t* R, int H, int W, in
     for (int i = 0; i < 2; i++)
         if ((rc = ensure(ctx, ctx->img[i], img)) != SM_OK) return rc;
     if ((rc = ensure(ctx, ctx->out, img * 2)) != SM_OK) return rc;
-    HIP_TRY(ctx, hipMemcpy2DAsync(ctx->img[0].p, W, L, stride, W, H, hipMemcpyHostToDevice, ctx->stream));
-    HIP_TRY(ctx, hipMemcpy2DAsync(ctx->img[1].p, W, R, stride, W, H, hipMemcpyHostToDevice, ctx->stream));
+    HostStage hs(ctx);
+    if ((rc = hs.reserve(stage_bytes(img, 2) + stage_bytes(img * 2))) != SM_OK) return rc;
+    if ((rc = hs.in(ctx->img[0].p, L, H, W, stride)) != SM_OK) return rc;
+    if ((rc = hs.in(ctx->img[1].p, R, H, W, stride)) != SM_OK) return rc;
     Src src;
     src.L = (const uint8_t*)ctx->img[0].p;
     src.R = (const uint8_t*)ctx->img[1].p;
     rc = run_pairs(ctx, src, 1, H, W, W, n, (int16_t*)ctx->out.p);
     if (rc != SM_OK) return rc;
-    HIP_TRY(ctx, hipMemcpyAsync(disp_out, ctx->out.p, img * 2, hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if ((rc = hs.out(disp_out, ctx->out.p, img * 2)) != SM_OK) return rc;
+    if ((rc = hs.finish()) != SM_OK) return rc;
     return check_sweep_errors(ctx);
 }
 
@@ -1448,11 +1601,17 @@ int sm_aggregate_cost_f32(sm_ctx* ctx, const float* cost, int D, int H, int W, c
     int rc;
     if ((rc = ensure(ctx, ctx->volbuf, img * D * 4)) != SM_OK) return rc;
     if ((rc = ensure(ctx, ctx->out, img * 2)) != SM_OK) return rc;
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->volbuf.p, cost, img * D * 4, hipMemcpyHostToDevice, ctx->stream));
+    {
+        StageTimer t_(ctx, ctx->stream, SM_STAGE_H2D, 1);
+        HIP_TRY(ctx, hipMemcpyAsync(ctx->volbuf.p, cost, img * D * 4, hipMemcpyHostToDevice, ctx->stream));
+    }
     rc = sm_aggregate_cost_f32_device(ctx, (const float*)ctx->volbuf.p, 1, img * D, D, H, W, p, offset, scale,
                                       (int16_t*)ctx->out.p);
     if (rc != SM_OK) return rc;
-    HIP_TRY(ctx, hipMemcpyAsync(disp_out, ctx->out.p, img * 2, hipMemcpyDeviceToHost, ctx->stream));
+    {
+        StageTimer t_(ctx, ctx->stream, SM_STAGE_D2H, 1);
+        HIP_TRY(ctx, hipMemcpyAsync(disp_out, ctx->out.p, img * 2, hipMemcpyDeviceToHost, ctx->stream));
+    }
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     return check_sweep_errors(ctx);
 }
@@ -1510,14 +1669,16 @@ int sm_wls_filter(sm_ctx* ctx, const int16_t* displ, const int16_t* dispr, const
     if ((rc = ensure(ctx, ctx->wls_disp[1], img * 2)) != SM_OK) return rc;
     if ((rc = ensure(ctx, ctx->img[0], img)) != SM_OK) return rc;
     if ((rc = ensure(ctx, ctx->wls_out, img * 2)) != SM_OK) return rc;
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->wls_disp[0].p, displ, img * 2, hipMemcpyHostToDevice, ctx->stream));
-    if (dispr) HIP_TRY(ctx, hipMemcpyAsync(ctx->wls_disp[1].p, dispr, img * 2, hipMemcpyHostToDevice, ctx->stream));
-    HIP_TRY(ctx, hipMemcpy2DAsync(ctx->img[0].p, W, guide, guide_stride, W, H, hipMemcpyHostToDevice, ctx->stream));
+    HostStage hs(ctx);
+    if ((rc = hs.reserve(stage_bytes(img * 2, 3) + stage_bytes(img))) != SM_OK) return rc;
+    if ((rc = hs.in(ctx->wls_disp[0].p, displ, 1, img * 2, img * 2)) != SM_OK) return rc;
+    if (dispr && (rc = hs.in(ctx->wls_disp[1].p, dispr, 1, img * 2, img * 2)) != SM_OK) return rc;
+    if ((rc = hs.in(ctx->img[0].p, guide, H, W, guide_stride)) != SM_OK) return rc;
     rc = run_wls(ctx, (const int16_t*)ctx->wls_disp[0].p, dispr ? (const int16_t*)ctx->wls_disp[1].p : nullptr, img,
                  (const uint8_t*)ctx->img[0].p, img, W, 1, H, W, n, (int16_t*)ctx->wls_out.p);
     if (rc != SM_OK) return rc;
-    HIP_TRY(ctx, hipMemcpyAsync(out, ctx->wls_out.p, img * 2, hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if ((rc = hs.out(out, ctx->wls_out.p, img * 2)) != SM_OK) return rc;
+    if ((rc = hs.finish()) != SM_OK) return rc;
     return check_sweep_errors(ctx);
 }
 
@@ -1559,15 +1720,17 @@ int sm_compute_disparity(sm_ctx* ctx, const uint8_t* L, const uint8_t* R, int H,
     if ((rc = ensure(ctx, ctx->wls_disp[0], img * 2)) != SM_OK) return rc;
     if ((rc = ensure(ctx, ctx->wls_disp[1], img * 2)) != SM_OK) return rc;
     if ((rc = ensure(ctx, ctx->wls_out, img * 2)) != SM_OK) return rc;
-    HIP_TRY(ctx, hipMemcpy2DAsync(ctx->img[0].p, W, L, stride, W, H, hipMemcpyHostToDevice, ctx->stream));
-    HIP_TRY(ctx, hipMemcpy2DAsync(ctx->img[1].p, W, R, stride, W, H, hipMemcpyHostToDevice, ctx->stream));
+    HostStage hs(ctx);
+    if ((rc = hs.reserve(stage_bytes(img, 2) + stage_bytes(img * 2, 2))) != SM_OK) return rc;
+    if ((rc = hs.in(ctx->img[0].p, L, H, W, stride)) != SM_OK) return rc;
+    if ((rc = hs.in(ctx->img[1].p, R, H, W, stride)) != SM_OK) return rc;
     rc = sm_compute_disparity_batch_device(ctx, (const uint8_t*)ctx->img[0].p, (const uint8_t*)ctx->img[1].p, 1, img,
                                            H, W, W, left, wls, (int16_t*)ctx->wls_disp[0].p,
                                            (int16_t*)ctx->wls_disp[1].p, (int16_t*)ctx->wls_out.p);
     if (rc != SM_OK) return rc;
-    HIP_TRY(ctx, hipMemcpyAsync(displ, ctx->wls_disp[0].p, img * 2, hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(ctx, hipMemcpyAsync(filtered, ctx->wls_out.p, img * 2, hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if ((rc = hs.out(displ, ctx->wls_disp[0].p, img * 2)) != SM_OK) return rc;
+    if ((rc = hs.out(filtered, ctx->wls_out.p, img * 2)) != SM_OK) return rc;
+    if ((rc = hs.finish()) != SM_OK) return rc;
     return check_sweep_errors(ctx);
 }
 
@@ -1590,11 +1753,17 @@ int sm_filter_speckles(sm_ctx* ctx, int16_t* img, int H, int W, int new_val, int
     const size_t bytes = (size_t)H * W * 2;
     int rc;
     if ((rc = ensure(ctx, ctx->out, bytes)) != SM_OK) return rc;
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->out.p, img, bytes, hipMemcpyHostToDevice, ctx->stream));
+    {
+        StageTimer t_(ctx, ctx->stream, SM_STAGE_H2D, 1);
+        HIP_TRY(ctx, hipMemcpyAsync(ctx->out.p, img, bytes, hipMemcpyHostToDevice, ctx->stream));
+    }
     if ((rc = sm_filter_speckles_device(ctx, (int16_t*)ctx->out.p, 1, H, W, new_val, max_speckle_size, max_diff)) !=
         SM_OK)
         return rc;
-    HIP_TRY(ctx, hipMemcpyAsync(img, ctx->out.p, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    {
+        StageTimer t_(ctx, ctx->stream, SM_STAGE_D2H, 1);
+        HIP_TRY(ctx, hipMemcpyAsync(img, ctx->out.p, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    }
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     return check_sweep_errors(ctx);
 }
@@ -1651,11 +1820,17 @@ int sm_reproject_image_to_3d(sm_ctx* ctx, const void* disp, int disp_type, int H
     int rc;
     if ((rc = ensure(ctx, ctx->rp_in, ib)) != SM_OK) return rc;
     if ((rc = ensure(ctx, ctx->rp_out, npx * 12)) != SM_OK) return rc;
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->rp_in.p, disp, ib, hipMemcpyHostToDevice, ctx->stream));
+    {
+        StageTimer t_(ctx, ctx->stream, SM_STAGE_H2D, 1);
+        HIP_TRY(ctx, hipMemcpyAsync(ctx->rp_in.p, disp, ib, hipMemcpyHostToDevice, ctx->stream));
+    }
     if ((rc = sm_reproject_image_to_3d_device(ctx, ctx->rp_in.p, disp_type, 1, H, W, Q, handle_missing,
                                               (float*)ctx->rp_out.p)) != SM_OK)
         return rc;
-    HIP_TRY(ctx, hipMemcpyAsync(xyz, ctx->rp_out.p, npx * 12, hipMemcpyDeviceToHost, ctx->stream));
+    {
+        StageTimer t_(ctx, ctx->stream, SM_STAGE_D2H, 1);
+        HIP_TRY(ctx, hipMemcpyAsync(xyz, ctx->rp_out.p, npx * 12, hipMemcpyDeviceToHost, ctx->stream));
+    }
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     return check_sweep_errors(ctx);
 }
@@ -1717,14 +1892,15 @@ int sm_bm_compute(sm_ctx* ctx, const uint8_t* L, const uint8_t* R, int H, int W,
     for (int i = 0; i < 2; i++)
         if ((rc = ensure(ctx, ctx->img[i], img)) != SM_OK) return rc;
     if ((rc = ensure(ctx, ctx->out, img * 2)) != SM_OK) return rc;
-    HIP_TRY(ctx, hipMemcpy2DAsync(ctx->img[0].p, W, L, stride, W, H, hipMemcpyHostToDevice, ctx->stream));
-    HIP_TRY(ctx, hipMemcpy2DAsync(ctx->img[1].p, W, R, stride, W, H, hipMemcpyHostToDevice, ctx->stream));
+    HostStage hs(ctx);
+    if ((rc = hs.reserve(stage_bytes(img, 2) + stage_bytes(img * 2))) != SM_OK) return rc;
+    if ((rc = hs.in(ctx->img[0].p, L, H, W, stride)) != SM_OK) return rc;
+    if ((rc = hs.in(ctx->img[1].p, R, H, W, stride)) != SM_OK) return rc;
     rc = run_bm(ctx, (const uint8_t*)ctx->img[0].p, (const uint8_t*)ctx->img[1].p, img, 1, H, W, W, n,
                 (int16_t*)ctx->out.p);
     if (rc != SM_OK) return rc;
-    HIP_TRY(ctx, hipMemcpyAsync(disp_out, ctx->out.p, img * 2, hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    return check_sweep_errors(ctx);
+    if ((rc = hs.out(disp_out, ctx->out.p, img * 2)) != SM_OK) return rc;
+    return hs.finish();
 }
 
 // Multi-device batch from one process: ctxs[k] (one per device,
@@ -1756,21 +1932,22 @@ int sm_compute_batch(sm_ctx** ctxs, int ngpu, const uint8_t* const* left, const 
             for (int i = 0; i < 2; i++)
                 if ((rc = ensure(ctx, ctx->img[i], img * n)) != SM_OK) return rc;
             if ((rc = ensure(ctx, ctx->out, img * 2 * n)) != SM_OK) return rc;
+            HostStage hs(ctx);
+            if ((rc = hs.reserve(stage_bytes(img, 2 * n) + stage_bytes(img * 2 * n))) != SM_OK) return rc;
             for (int i = 0; i < n; i++) {
                 if (!left[a + i] || !right[a + i]) return fail(ctx, SM_E_ARG, "pair %d has a NULL image", a + i);
-                HIP_TRY(ctx, hipMemcpyAsync((uint8_t*)ctx->img[0].p + img * i, left[a + i], img, hipMemcpyHostToDevice,
-                                            ctx->stream));
-                HIP_TRY(ctx, hipMemcpyAsync((uint8_t*)ctx->img[1].p + img * i, right[a + i], img,
-                                            hipMemcpyHostToDevice, ctx->stream));
+                if ((rc = hs.in((uint8_t*)ctx->img[0].p + img * i, left[a + i], 1, img, img)) != SM_OK) return rc;
+                if ((rc = hs.in((uint8_t*)ctx->img[1].p + img * i, right[a + i], 1, img, img)) != SM_OK) return rc;
             }
             Src src;
             src.L = (const uint8_t*)ctx->img[0].p;
             src.R = (const uint8_t*)ctx->img[1].p;
             src.pair_stride = img;
             if ((rc = run_pairs(ctx, src, n, H, W, W, nm, (int16_t*)ctx->out.p)) != SM_OK) return rc;
-            HIP_TRY(ctx, hipMemcpyAsync(out + img * a, ctx->out.p, img * 2 * n, hipMemcpyDeviceToHost, ctx->stream));
-            HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-            return SM_OK;
+            if ((rc = hs.out(out + img * a, ctx->out.p, img * 2 * n)) != SM_OK) return rc;
+            if ((rc = hs.finish()) != SM_OK) return rc;
+            HIP_TRY(ctx, hipStreamSynchronize(ctx->side));
+            return check_sweep_errors(ctx);
         };
         rcs[k] = run();
     };
@@ -1792,6 +1969,50 @@ int sm_synchronize(sm_ctx* ctx)
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->side));
     return check_sweep_errors(ctx);
+}
+
+int sm_get_counters(sm_ctx* ctx, long long* sweep_fallbacks)
+{
+    if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
+    uint32_t n = 0;
+    if (ctx->sweep_err.p) {
+        HIP_TRY(ctx, hipSetDevice(ctx->device));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->side));
+        HIP_TRY(ctx, hipMemcpy(&n, (uint32_t*)ctx->sweep_err.p + ERR_FALLBACKS, 4, hipMemcpyDeviceToHost));
+    }
+    if (sweep_fallbacks) *sweep_fallbacks = n;
+    return SM_OK;
+}
+
+int sm_set_cu_mask(sm_ctx* ctx, const uint32_t* mask, int nwords)
+{
+    if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
+    if (nwords < 0 || (nwords > 0 && !mask)) return fail(ctx, SM_E_ARG, "bad CU mask");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    HIP_TRY(ctx, hipDeviceSynchronize());
+    hipStream_t a = nullptr, b = nullptr;
+    if (nwords > 0) {
+        HIP_TRY(ctx, hipExtStreamCreateWithCUMask(&a, (uint32_t)nwords, mask));
+        hipError_t e = hipExtStreamCreateWithCUMask(&b, (uint32_t)nwords, mask);
+        if (e != hipSuccess) {
+            (void)hipStreamDestroy(a);
+            return fail(ctx, SM_E_HIP, "hipExtStreamCreateWithCUMask: %s", hipGetErrorString(e));
+        }
+    } else {
+        HIP_TRY(ctx, hipStreamCreateWithFlags(&a, hipStreamNonBlocking));
+        hipError_t e = hipStreamCreateWithFlags(&b, hipStreamNonBlocking);
+        if (e != hipSuccess) {
+            (void)hipStreamDestroy(a);
+            return fail(ctx, SM_E_HIP, "hipStreamCreateWithFlags: %s", hipGetErrorString(e));
+        }
+    }
+    (void)hipStreamDestroy(ctx->own_stream);
+    (void)hipStreamDestroy(ctx->side);
+    ctx->own_stream = a;
+    ctx->side = b;
+    ctx->stream = a;
+    return SM_OK;
 }
 
 int sm_set_timing(sm_ctx* ctx, int enable)

@@ -41,7 +41,18 @@ struct PathsArgs {
     int dbg;      // timing ablations only: 1 skip horizontal, 2 skip vertical, 4 drop stores
     int nv;       // vertical-family directions in this launch
     int v_dx[6], v_dy[6], v_slot[6], v_blk_start[7], v_line_lo[6], v_nlines[6];
+    // fused-sweep fallback (sm_api.hip run_group): when set, the launch is a small
+    // grid that does nothing unless *guard != 0 (a sweep strip gave up waiting for
+    // its neighbours), and then walks all nblocks x npairs blocks grid-stride
+    const uint32_t* guard;
+    int nblocks, npairs;
 };
+
+// fallback launches read the sweep's group flag (written by another kernel)
+__device__ __forceinline__ bool guard_clear(const uint32_t* g)
+{
+    return __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
+}
 
 template <int LANES, int DPL>
 __device__ __forceinline__ uint32_t sgm_step(const uint32_t (&Lp)[DPL], uint32_t minLp, const uint32_t (&C)[DPL],
@@ -419,19 +430,27 @@ constexpr int lds_per_wave()
     return VWin<D, LPW>::WORDS > 128 ? VWin<D, LPW>::WORDS : 128;
 }
 
-// VL: lanes per vertical-family line (16 or 8); DPLV = D / VL
-template <int VL, int DPLV, int LANESH, int DPLH, bool CENSUS, typename LT>
+// VL: lanes per vertical-family line (16 or 8); DPLV = D / VL.  FB: the sweep
+// engine's guarded fallback instance (see PathsArgs::guard); a separate
+// instance so the normal one carries none of its code (registers).
+template <int VL, int DPLV, int LANESH, int DPLH, bool CENSUS, typename LT, bool FB = false>
 __global__ void __launch_bounds__(256) k_sgm_paths(PathsArgs a)
 {
     constexpr int PW = lds_per_wave<VL * DPLV, 64 / VL>();
     __shared__ __attribute__((aligned(16))) uint64_t lds[4 * PW];
     uint64_t* mine = lds + (threadIdx.x >> 6) * PW;
-    const int pair = blockIdx.y;
-    const int b = blockIdx.x;
-    if (b < 2 * a.hblocks) {
-        if (!(a.dbg & 1)) horz_family<LANESH, DPLH, CENSUS, LT>(a, pair, b, mine);
+    auto block = [&](int pair, int b) {
+        if (b < 2 * a.hblocks) {
+            if (!(a.dbg & 1)) horz_family<LANESH, DPLH, CENSUS, LT>(a, pair, b, mine);
+        } else {
+            if (!(a.dbg & 2)) vert_family<VL, DPLV, CENSUS, LT>(a, pair, b - 2 * a.hblocks, mine);
+        }
+    };
+    if constexpr (FB) {  // wave-private LDS only: no barrier between blocks
+        if (guard_clear(a.guard)) return;
+        for (int v = blockIdx.x; v < a.nblocks * a.npairs; v += gridDim.x) block(v / a.nblocks, v % a.nblocks);
     } else {
-        if (!(a.dbg & 2)) vert_family<VL, DPLV, CENSUS, LT>(a, pair, b - 2 * a.hblocks, mine);
+        block(blockIdx.y, blockIdx.x);
     }
 }
 
@@ -445,18 +464,21 @@ struct WtaArgs {
     int16_t* disp;  // [pair][H][W] pre-median
     const uint16_t* part;  // hybrid engine: u16 S + SE + SW sums [pair][H][width1][D], or null
     size_t part_pair;      // elements
+    // sweep fallback (see PathsArgs::guard): grid-stride over H x npairs rows; the
+    // launch's first workgroup counts the fallback in *fallbacks
+    const uint32_t* guard;
+    uint32_t* fallbacks;
+    int npairs;
 };
 
 template <int DPL, typename LT, int NT>
-__global__ void __launch_bounds__(NT) k_wta(WtaArgs a)
+__device__ __forceinline__ void wta_row(const WtaArgs& a, const int y, const int pair, uint32_t* smem)
 {
-    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const int W = a.W, D = a.D, minD = a.minD, minX1 = a.minX1;
     const int maxX1 = minX1 + a.width1;
     const int INVALID = (minD - 1) * 16;
     uint32_t* key2 = smem;
     int* drow = reinterpret_cast<int*>(smem + W);
-    const int y = blockIdx.x, pair = blockIdx.y;
     for (int i = threadIdx.x; i < W; i += NT) {
         key2[i] = 0xFFFFFFFFu;
         drow[i] = INVALID;
@@ -576,6 +598,22 @@ __global__ void __launch_bounds__(NT) k_wta(WtaArgs a)
             if (rej1 && rej2) d1 = INVALID;
         }
         out[X] = (int16_t)d1;
+    }
+}
+
+template <int DPL, typename LT, int NT, bool FB = false>
+__global__ void __launch_bounds__(NT) k_wta(WtaArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    if constexpr (FB) {  // sweep fallback: grid-stride over the rows of every pair
+        if (guard_clear(a.guard)) return;
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(a.fallbacks, 1u);
+        for (int v = blockIdx.x; v < a.H * a.npairs; v += gridDim.x) {
+            wta_row<DPL, LT, NT>(a, v % a.H, v / a.H, smem);
+            __syncthreads();  // the next row reuses the shared row buffers
+        }
+    } else {
+        wta_row<DPL, LT, NT>(a, blockIdx.x, blockIdx.y, smem);
     }
 }
 

@@ -1,0 +1,64 @@
+"""bench.py contract on CPU: the --gpus N launcher (torch.distributed.run as a
+child, gloo stand-in step), the world-size guard, and the SURVEY §8(d) byte
+attribution the roofline line uses."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+
+
+def _run(args, env=None, timeout=240):
+    e = dict(os.environ)
+    e.pop("WORLD_SIZE", None)
+    e.update(env or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, cwd=ROOT, env=e,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+def _json_line(stdout):
+    lines = [ln for ln in stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, stdout
+    return json.loads(lines[0])
+
+
+def test_launcher_spawns_two_ranks():
+    r = _run(["--gpus", "2", "--selftest-cpu", "--steps", "2", "--warmup", "1", "--config", "tsukuba",
+              "--pairs-per-gpu", "3"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_line(r.stdout)
+    assert d["n_gpus"] == 2
+    assert d["config"]["global_batch"] == 6
+    assert d["config"]["parallelism"] == "pairs/dp2"
+    assert d["distributed"]["world_size"] == 2
+    assert d["distributed"]["backend"] == "gloo"
+    assert d["distributed"]["gathered_in_pair_order"] is True
+
+
+def test_gpus_must_match_world_size():
+    r = _run(["--gpus", "2", "--selftest-cpu"], env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0
+    assert "WORLD_SIZE" in r.stderr
+
+
+@pytest.mark.parametrize("mode,P", [("census8", 8), ("sgbm5", 5), ("sgbm8", 8), ("volume8", 8)])
+@pytest.mark.parametrize("sweep", [False, True])
+def test_stage_attribution_sums_to_model(mode, P, sweep):
+    H, W, D = 375, 1242, 128
+    stages = ("cost", "paths", "wta", "horizontal", "sweep", "sweep_wta", "median")
+    tot = sum(bench.model_stage_bytes(s, mode, H, W, D, P, sweep) for s in stages)
+    assert tot == bench.model_pair_bytes(mode, H, W, D, P)
+
+
+def test_headline_model_numbers():
+    # KITTI census 8 paths = 775.0 MB of volume traffic + I/O per pair
+    H, W, D = 375, 1242, 128
+    assert bench.model_pair_bytes("census8", H, W, D, 8) == 59_616_000 * 13 + 6 * H * W
+    # per-direction aggregation owns P reads + the u16 S write: 10 B per cell (4.77 GB / 8 pairs)
+    assert bench.model_stage_bytes("paths", "census8", H, W, D, 8, False) * 8 == 4_769_280_000

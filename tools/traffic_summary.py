@@ -7,7 +7,11 @@ import collections
 import csv
 import glob
 import json
+import os
 import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+import bench  # noqa: E402  (source_hash: the stamp bench.py checks before using these numbers)
 
 out, config, mode = sys.argv[1], sys.argv[2], sys.argv[3]
 vals = collections.defaultdict(lambda: collections.defaultdict(list))
@@ -35,5 +39,7 @@ for k, d in vals.items():
         summary.setdefault("stages", {})[stage] = {"kernel": k, "hbm_bytes_per_launch": (rd or 0) + (wr or 0),
                                                    "read_bytes": rd, "write_bytes": wr}
 summary["pairs_per_launch"] = 8  # bench.py default --pairs-per-gpu (one launch group)
+summary["engine"] = "sweep" if any("k_sweep" in n for n in vals) else "perdir"
+summary["src_sha16"] = bench.source_hash()
 json.dump(summary, open(out + "/summary.json", "w"), indent=1)
 print(json.dumps(summary, indent=1))
