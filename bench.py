@@ -370,11 +370,11 @@ def main():
                 "gather_bytes_to_root": gpairs * H * W * 2,
                 "compute_ms_per_step": (elapsed * 1e3 - gather_ms) / K,
             }
+        hs_pair = None
         if world == 1 and args.host_surface_calls > 0 and args.config == "kitti":
-            line["host_surface"] = host_surface(args, local_rank)
+            line["host_surface"], hs_pair = host_surface(args, local_rank)
         if world == 1 and args.cpu_baseline_pairs > 0:
-            line["cpu_baseline"] = cpu_baseline(args, H, W, D, p, lefts, rights, out0, volume, full,
-                                                line.get("host_surface"))
+            line["cpu_baseline"] = cpu_baseline(args, H, W, D, p, lefts, rights, out0, volume, full, hs_pair)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -486,8 +486,7 @@ def host_surface(args, device):
                          "h2d_ms_per_call": st1["h2d"][0] / n, "d2h_ms_per_call": st1["d2h"][0] / n,
                          "device_ms_per_call": (st1["total"][0] + st1["wls"][0]) / n,
                          "same_as_python_surface": bool(np.array_equal(d1, displ) and np.array_equal(f1, filt))},
-        "_pair": (gl, gr, s, displ, filt),
-    }
+    }, (gl, gr, s, displ, filt)
 
 
 def cpu_baseline(args, H, W, D, p, lefts, rights, out0, volume, full=False, hs=None):
@@ -496,8 +495,9 @@ def cpu_baseline(args, H, W, D, p, lefts, rights, out0, volume, full=False, hs=N
     ``--cpu-baseline-pairs`` pairs concurrently (ctypes releases the GIL; the
     port is single-threaded per pair, the pairs are independent), plus the
     one-thread rate.  Also re-checks pair 0 bit for bit; the numpy oracle on
-    Tsukuba (BASELINE.md CPU plan step 2); and the host-surface pair through
-    the C port + numpy WLS."""
+    Tsukuba (BASELINE.md CPU plan step 2); and the host-surface pair
+    ``hs`` = (left, right, settings, displ, filtered) through the C port +
+    numpy WLS."""
     import threading
 
     from oracle import ref_c, sgm_np, wls_np
@@ -578,7 +578,7 @@ def cpu_baseline(args, H, W, D, p, lefts, rights, out0, volume, full=False, hs=N
                             "sample": "oracle/sgm_np.py, 384x288 D=16 OpenCV-SGBM 5-path (settings.ini), "
                                       "median of 5 after 1 warm-up"}
     if hs is not None:  # host surface: the same pair through the C port (both matchers) + numpy WLS
-        gl, gr, s, displ, filt = hs.pop("_pair")
+        gl, gr, s, displ, filt = hs
         Dh = s["num_disparities"]
         hp = synthetic.parity_params(Dh, s["window_size"])
         lp = dict(hp, uniquenessRatio=0, disp12MaxDiff=1000000)

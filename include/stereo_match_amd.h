@@ -285,8 +285,12 @@ long long sm_debug_fetch(sm_ctx* ctx, int what, void* host, size_t bytes);
  * horizontal family; bit 12 (valid results) uses the per-direction engine
  * (one path volume per direction + WTA kernel) instead of the fused sweeps,
  * so that sm_debug_fetch(1) has every direction; bit 13 (valid results) one
- * pair per fused-sweep launch; bit 14 (valid results) the fused sweeps for 8
- * paths too; bit 15 (valid results, 8 paths) the hybrid engine: the down
+ * pair per fused-sweep launch; bit 14 (valid results) forces the fused sweeps
+ * wherever their preconditions hold (by default census 8 paths and launch
+ * groups of fewer than 3 pairs run on the per-direction engine); bit 23 (valid
+ * results) flags every fused-sweep group as given up, so the guarded
+ * per-direction fallback recomputes it; bit 31 drops the guarded fallback
+ * launches (timing only); bit 15 (valid results, 8 paths) the hybrid engine: the down
  * sweep on a second stream beside a per-direction launch of the other five
  * directions; bits 16-19: launch-group size cap (0 = none); bits 24-27:
  * fused-sweep timing ablations (results become wrong).

@@ -92,6 +92,11 @@ struct sm_ctx {
     DevBuf hop, sweep_err;  // sweep engine: strip-boundary granules, device error word
     void* pin = nullptr;    // page-locked host staging of the host-pointer entry points (HostStage)
     size_t pin_n = 0;
+    // compute_disparity: the right matcher runs on a twin context (own streams and
+    // buffers) beside the left one; created on first use, destroyed with this one
+    sm_ctx* twin = nullptr;
+    hipEvent_t ev_lr_fork = nullptr, ev_lr_join = nullptr;
+    std::vector<uint32_t> cu_mask;  // sm_set_cu_mask words (applied to the twin too)
     uint32_t hop_epoch = 0;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;  // sweep engine: E/W kernel on the side stream
     const uint32_t* fb_guard = nullptr;  // set while enqueuing a group's guarded per-direction fallback
@@ -327,6 +332,7 @@ const int kVdy[6] = {1, 1, 1, -1, -1, -1};
 
 constexpr size_t kSetBudget = size_t(12) << 30;  // bytes of path volumes per buffer set
 constexpr int kMaxGroup = 16;
+constexpr int kSweepMinPairs = 3;  // smallest launch group the fused sweeps run by default
 
 struct Src {  // where a launch group's pairs come from (device pointers)
     const uint8_t* L = nullptr;  // census / SGBM: images, pair i at L + i*pair_stride
@@ -432,7 +438,7 @@ int launch_paths_t(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs, int dir
         pa.guard = ctx->fb_guard;
         pa.nblocks = (int)grid.x;
         pa.npairs = g.G;
-        grid = dim3(std::min<unsigned>(grid.x * g.G, 512u), 1);
+        grid = dim3(std::min<unsigned>(grid.x * g.G, 128u), 1);
     }
     StageTimer t(ctx, ctx->stream,
                  ctx->fb_guard ? SM_STAGE_FALLBACK : dirset == DIRS_EW ? SM_STAGE_HORIZONTAL : SM_STAGE_PATHS, g.G);
@@ -506,7 +512,7 @@ int launch_wta_t(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs)
         wa.guard = ctx->fb_guard;
         wa.fallbacks = (uint32_t*)ctx->sweep_err.p + ERR_FALLBACKS;
         wa.npairs = g.G;
-        grid = dim3(std::min(g.H * g.G, 256), 1);
+        grid = dim3(std::min(g.H * g.G, 64), 1);
     }
     if (ctx->fb_guard)
         hipLaunchKernelGGL((smk::k_wta<DPLV, LT, 1024, true>), grid, dim3(1024), (size_t)g.W * 8, stream_b(ctx), wa);
@@ -573,6 +579,8 @@ bool use_hybrid(const sm_ctx* ctx, const Norm& n, int H)
     return use_sweep(&tmp, n, H);
 }
 
+// preconditions of the fused sweeps (run_pairs also requires kSweepMinPairs pairs per
+// launch group unless flag 16384 forces them)
 bool use_sweep(const sm_ctx* ctx, const Norm& n, int H)
 {
     if (ctx->dbg_flags & (DBG_LEGACY | DBG_ROW)) return false;
@@ -800,6 +808,10 @@ int run_hybrid(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs)
 // default sweep engine recovers on the device instead (run_group's fallback).
 int check_sweep_errors(sm_ctx* ctx)
 {
+    if (ctx->twin) {
+        int rc = check_sweep_errors(ctx->twin);
+        if (rc != SM_OK) return fail(ctx, rc, "%s", ctx->twin->err.c_str());
+    }
     if (!ctx->sweep_err.p) return SM_OK;
     uint32_t e = 0;
     uint32_t* w = (uint32_t*)ctx->sweep_err.p + ERR_STICKY;
@@ -1123,8 +1135,15 @@ int run_pairs(sm_ctx* ctx, const Src& src, int npairs, int H, int W, int stride,
     g.L_pair = g.slot_bytes * (g.hybrid ? hybrid_slots(n) : n.ndirs);
     g.census_pair = (size_t)H * W;
     g.cost_pair = n.cost == SM_COST_CENSUS ? 0 : g.vol;
+    int G = group_size(ctx, n, H, npairs, g.sweep, g.hybrid);
+    // the sweeps' parallelism is (strips x pairs): below kSweepMinPairs pairs per launch
+    // group the per-direction engine is faster (KITTI D=128, sgbm5: 521 vs 901 us for one
+    // pair, 459 vs 527 for two, 426 vs 416 for three); flag 16384 forces them
+    if (g.sweep && std::min(G, npairs) < kSweepMinPairs && !(ctx->dbg_flags & DBG_SWEEP8)) {
+        g.sweep = false;
+        G = group_size(ctx, n, H, npairs, false, false);
+    }
     ctx->last_ndirs = g.sweep ? 2 : g.hybrid ? hybrid_slots(n) : n.ndirs;
-    const int G = group_size(ctx, n, H, npairs, g.sweep, g.hybrid);
     int rc = SM_OK;
     {
         StageTimer total(ctx, ctx->stream, SM_STAGE_TOTAL, npairs);
@@ -1473,6 +1492,9 @@ void sm_destroy(sm_ctx* ctx)
     }
     for (auto e : ctx->free_events) (void)hipEventDestroy(e);
     if (ctx->pin) (void)hipHostFree(ctx->pin);
+    if (ctx->ev_lr_fork) (void)hipEventDestroy(ctx->ev_lr_fork);
+    if (ctx->ev_lr_join) (void)hipEventDestroy(ctx->ev_lr_join);
+    sm_destroy(ctx->twin);
     if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
     if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
     if (ctx->side) (void)hipStreamDestroy(ctx->side);
@@ -1699,9 +1721,28 @@ int sm_compute_disparity_batch_device(sm_ctx* ctx, const uint8_t* dL, const uint
     lm.uniqueness_ratio = 0;             // createDisparityWLSFilter (:172) mutates the left one
     lm.disp12_max_diff = 1000000;
     lm.speckle_window_size = 0;
-    int rc = sm_compute_batch_device(ctx, dL, dR, npairs, pair_stride, H, W, stride, &lm, d_displ);
-    if (rc != SM_OK) return rc;
-    rc = sm_compute_batch_device(ctx, dR, dL, npairs, pair_stride, H, W, stride, &rm, d_dispr);
+    // the two matchers are independent: the right one runs on the twin context's
+    // stream beside the left one (a single pair fills a fraction of the chip)
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    int rc;
+    if (!ctx->twin) {
+        if ((rc = sm_create(ctx->device, &ctx->twin)) != SM_OK) return fail(ctx, rc, "%s", g_thread_error.c_str());
+        ctx->twin->timing = ctx->timing;
+        ctx->twin->dbg_flags = ctx->dbg_flags;
+        if (!ctx->cu_mask.empty() &&
+            (rc = sm_set_cu_mask(ctx->twin, ctx->cu_mask.data(), (int)ctx->cu_mask.size())) != SM_OK)
+            return fail(ctx, rc, "%s", ctx->twin->err.c_str());
+    }
+    if ((rc = ensure_event(ctx, ctx->ev_lr_fork)) != SM_OK) return rc;
+    if ((rc = ensure_event(ctx, ctx->ev_lr_join)) != SM_OK) return rc;
+    sm_ctx* tw = ctx->twin;
+    HIP_TRY(ctx, hipEventRecord(ctx->ev_lr_fork, ctx->stream));
+    HIP_TRY(ctx, hipStreamWaitEvent(tw->stream, ctx->ev_lr_fork, 0));
+    rc = sm_compute_batch_device(tw, dR, dL, npairs, pair_stride, H, W, stride, &rm, d_dispr);
+    if (rc != SM_OK) return fail(ctx, rc, "right matcher: %s", tw->err.c_str());
+    HIP_TRY(ctx, hipEventRecord(ctx->ev_lr_join, tw->stream));
+    rc = sm_compute_batch_device(ctx, dL, dR, npairs, pair_stride, H, W, stride, &lm, d_displ);
+    HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_lr_join, 0));  // joined on every path
     if (rc != SM_OK) return rc;
     return sm_wls_filter_batch_device(ctx, d_displ, d_dispr, dL, npairs, pair_stride, stride, H, W, wls, d_filtered);
 }
@@ -1966,6 +2007,10 @@ int sm_compute_batch(sm_ctx** ctxs, int ngpu, const uint8_t* const* left, const 
 int sm_synchronize(sm_ctx* ctx)
 {
     if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
+    if (ctx->twin) {
+        int rc = sm_synchronize(ctx->twin);
+        if (rc != SM_OK) return fail(ctx, rc, "%s", ctx->twin->err.c_str());
+    }
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->side));
     return check_sweep_errors(ctx);
@@ -1981,7 +2026,9 @@ int sm_get_counters(sm_ctx* ctx, long long* sweep_fallbacks)
         HIP_TRY(ctx, hipStreamSynchronize(ctx->side));
         HIP_TRY(ctx, hipMemcpy(&n, (uint32_t*)ctx->sweep_err.p + ERR_FALLBACKS, 4, hipMemcpyDeviceToHost));
     }
-    if (sweep_fallbacks) *sweep_fallbacks = n;
+    long long t = 0;
+    if (ctx->twin) sm_get_counters(ctx->twin, &t);
+    if (sweep_fallbacks) *sweep_fallbacks = n + t;
     return SM_OK;
 }
 
@@ -2012,12 +2059,18 @@ int sm_set_cu_mask(sm_ctx* ctx, const uint32_t* mask, int nwords)
     ctx->own_stream = a;
     ctx->side = b;
     ctx->stream = a;
+    ctx->cu_mask.assign(mask, mask + nwords);
+    if (ctx->twin) {
+        int rc = sm_set_cu_mask(ctx->twin, mask, nwords);
+        if (rc != SM_OK) return fail(ctx, rc, "%s", ctx->twin->err.c_str());
+    }
     return SM_OK;
 }
 
 int sm_set_timing(sm_ctx* ctx, int enable)
 {
     if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
+    if (ctx->twin) sm_set_timing(ctx->twin, enable);
     ctx->timing = enable != 0;
     return SM_OK;
 }
@@ -2025,6 +2078,7 @@ int sm_set_timing(sm_ctx* ctx, int enable)
 int sm_set_debug_flags(sm_ctx* ctx, int flags)
 {
     if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
+    if (ctx->twin) sm_set_debug_flags(ctx->twin, flags);
     ctx->dbg_flags = flags;
     return SM_OK;
 }
@@ -2032,6 +2086,7 @@ int sm_set_debug_flags(sm_ctx* ctx, int flags)
 int sm_reset_timing(sm_ctx* ctx)
 {
     if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
+    if (ctx->twin) sm_reset_timing(ctx->twin);
     harvest_timing(ctx);
     for (int i = 0; i < SM_NUM_STAGES; i++) {
         ctx->stage_ms[i] = 0;
@@ -2046,9 +2101,19 @@ int sm_get_timing(sm_ctx* ctx, int stage, double* total_ms, long long* launches,
     if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
     if (stage < 0 || stage >= SM_NUM_STAGES) return fail(ctx, SM_E_ARG, "stage %d out of range", stage);
     harvest_timing(ctx);
-    if (total_ms) *total_ms = ctx->stage_ms[stage];
-    if (launches) *launches = ctx->stage_launches[stage];
-    if (pairs) *pairs = ctx->stage_pairs[stage];
+    double ms = ctx->stage_ms[stage];
+    long long nl = ctx->stage_launches[stage], np = ctx->stage_pairs[stage];
+    if (ctx->twin) {  // the right matcher of compute_disparity (sm_compute_disparity_batch_device)
+        double tms = 0;
+        long long tl = 0, tp = 0;
+        sm_get_timing(ctx->twin, stage, &tms, &tl, &tp);
+        ms += tms;
+        nl += tl;
+        np += tp;
+    }
+    if (total_ms) *total_ms = ms;
+    if (launches) *launches = nl;
+    if (pairs) *pairs = np;
     return SM_OK;
 }
 

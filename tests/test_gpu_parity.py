@@ -91,11 +91,10 @@ for _i in range(36):
 @pytest.mark.parametrize("flags", [0, 4096, 16384, 32768], ids=["default", "perdir", "sweep8", "hybrid"])
 @pytest.mark.parametrize("c", CASES, ids=lambda c: "H{H}W{W}D{D}m{minD}c{cost}p{mode}".format(**c))
 def test_random_shapes_vs_c_oracle(eng, c, flags):
-    """Default engines, the per-direction engine (4096), the fused sweeps for
-    census 8 paths too (16384; the other configurations run on the sweeps by
-    default) and the hybrid engine (32768, 5 and 8 paths)."""
-    if flags == 16384 and (c["mode"] != 8 or not c["cost"]):
-        pytest.skip("5 paths already run on the sweeps by default")
+    """Default engines (one pair per call: per-direction), the per-direction
+    engine (4096), the fused sweeps forced for every configuration (16384; by
+    default they need >= 3 pairs per launch group) and the hybrid engine
+    (32768, 5 and 8 paths)."""
     eng.set_debug_flags(flags)
     try:
         _random_case(eng, c)
@@ -137,7 +136,8 @@ def test_sgbm_cost_block_sizes(eng, bs, D, minD):
                                                   ("kitti", 0, 5, 4096), ("mccnn", 1, 8, 16384),
                                                   ("kitti", 1, 8, 32768), ("kitti", 0, 8, 32768),
                                                   ("mccnn", 1, 8, 32768), ("kitti", 0, 5, 32768),
-                                                  ("kitti", 0, 5, 1 << 22), ("kitti", 0, 8, 4096)])
+                                                  ("kitti", 0, 5, 1 << 22), ("kitti", 0, 8, 4096),
+                                                  ("kitti", 0, 5, 16384), ("kitti", 1, 5, 16384)])
 def test_full_size_bit_exact(eng, name, cost, mode, flags):
     H, W, D = synthetic.CONFIGS[name]
     left, right, gt = synthetic.random_dot_pair(H, W, D, seed=42)
@@ -280,11 +280,16 @@ def test_timing_counters(eng):
     eng.set_timing(False)
     assert t["paths"][1] == 3 and t["total"][1] == 3
     assert 0 < t["paths"][0] <= t["total"][0]
-    # sweep engine (5 paths): E/W kernel and the WTA sweep are timed on their own too
+    # sweep engine (5 paths; forced: one pair per call runs per-direction by default):
+    # E/W kernel and the WTA sweep are timed on their own too
     eng.set_timing(True)
     eng.reset_timing()
-    for _ in range(2):
-        run(eng, left, right, synthetic.parity_params(64))
+    eng.set_debug_flags(16384)
+    try:
+        for _ in range(2):
+            run(eng, left, right, synthetic.parity_params(64))
+    finally:
+        eng.set_debug_flags(0)
     t = eng.timing()
     eng.set_timing(False)
     assert t["paths"][1] == 2 and t["horizontal"][1] == 2 and t["sweep_wta"][1] == 2 and t["wta"][1] == 2

@@ -14,7 +14,7 @@ from stereo_match_amd import _lib, synthetic
 pytestmark = pytest.mark.gpu
 
 FORCE_FALLBACK = 1 << 23  # sm_api.hip DBG_FORCE_FALLBACK
-SWEEP8 = 16384            # fused sweeps for census 8 paths too
+SWEEP8 = 16384            # force the fused sweeps (any group size, census 8 paths too)
 PERDIR = 4096
 
 
@@ -33,7 +33,7 @@ def _run(eng, left, right, p, flags=0):
         eng.set_debug_flags(0)
 
 
-@pytest.mark.parametrize("cost,mode,extra", [(1, 8, SWEEP8), (0, 5, 0), (0, 8, 0), (1, 5, 0)],
+@pytest.mark.parametrize("cost,mode,extra", [(1, 8, SWEEP8), (0, 5, SWEEP8), (0, 8, SWEEP8), (1, 5, SWEEP8)],
                          ids=["census8", "sgbm5", "sgbm8", "census5"])
 def test_forced_sweep_fallback_is_exact(eng, cost, mode, extra):
     """Every sweep group flagged as given-up: the guarded per-direction launches
@@ -61,7 +61,7 @@ def test_forced_fallback_batch_device(eng):
     out = torch.full((n, H, W), 777, dtype=torch.int16, device="cuda")
     p = synthetic.parity_params(D)
     eng.set_stream(torch.cuda.current_stream().cuda_stream)
-    eng.set_debug_flags(FORCE_FALLBACK | (2 << 16))  # launch groups of 2 pairs: 3 groups, all recomputed
+    eng.set_debug_flags(FORCE_FALLBACK | SWEEP8 | (2 << 16))  # groups of 2 pairs: 3 groups, all recomputed
     before = eng.counters()["sweep_fallbacks"]
     try:
         eng.compute_batch_device(L.data_ptr(), R.data_ptr(), n, H * W, H, W, W, synthetic.to_sm_params(p),
@@ -76,7 +76,7 @@ def test_forced_fallback_batch_device(eng):
     assert eng.counters()["sweep_fallbacks"] == before + 3
 
 
-@pytest.mark.parametrize("mode,cost,extra", [(5, 0, 0), (8, 1, SWEEP8)], ids=["sgbm5", "census8"])
+@pytest.mark.parametrize("mode,cost,extra", [(5, 0, SWEEP8), (8, 1, SWEEP8)], ids=["sgbm5", "census8"])
 def test_sweep_on_half_the_cus(mode, cost, extra):
     """A context restricted to half the CUs (hipExtStreamCreateWithCUMask):
     the sweeps size their co-resident launches from the CUs the stream
@@ -103,7 +103,7 @@ def test_full_size_sweeps_do_not_fall_back(eng):
     H, W, D = synthetic.CONFIGS["kitti"]
     left, right, _ = synthetic.random_dot_pair(H, W, D, seed=6)
     before = eng.counters()["sweep_fallbacks"]
-    for p, flags in ((synthetic.parity_params(D), 0), (synthetic.headline_params(D), SWEEP8)):
+    for p, flags in ((synthetic.parity_params(D), SWEEP8), (synthetic.headline_params(D), SWEEP8)):
         assert np.array_equal(_run(eng, left, right, p, flags), ref_c.compute(left, right, p))
     assert eng.counters()["sweep_fallbacks"] == before
 

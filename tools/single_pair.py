@@ -1,0 +1,57 @@
+"""Single-pair latency of the reference surface (one pair per call, as
+stereo_vision.py:178-182 runs it): stage breakdown of sm_compute_disparity at
+settings.ini values (D=160) for each engine flag set.
+    python tools/single_pair.py [--flags 0,4096] [--calls 20]"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--flags", default="0,4096")
+    ap.add_argument("--calls", type=int, default=20)
+    ap.add_argument("--D", type=int, default=160)
+    args = ap.parse_args()
+    import stereo_match_amd as sm
+    from stereo_match_amd import _lib, synthetic, wls
+    from stereo_match_amd.stereo_vision import matcher_from_settings
+
+    s = dict(sm.DEFAULT_SETTINGS, window_size=5, num_disparities=args.D)
+    H, W = synthetic.CONFIGS["kitti"][:2]
+    gl, gr, _ = synthetic.random_dot_pair(H, W, args.D, seed=77)
+    lm = matcher_from_settings(s)
+    prm = lm.params()
+    wf = wls.createDisparityWLSFilter(lm)
+    wf.setLambda(s["lmbda"])
+    wf.setSigmaColor(s["sigma"])
+    wp = wf.params(H, W)
+    e = _lib.Engine(0)
+    ref = None
+    for f in [int(x) for x in args.flags.split(",")]:
+        e.set_debug_flags(f)
+        d, fl = e.compute_disparity(gl, gr, prm, wp)
+        if ref is None:
+            ref = (d, fl)
+        same = bool(np.array_equal(d, ref[0]) and np.array_equal(fl, ref[1]))
+        e.set_timing(True)
+        e.reset_timing()
+        ts = []
+        for _ in range(args.calls):
+            t0 = time.perf_counter()
+            e.compute_disparity(gl, gr, prm, wp)
+            ts.append(time.perf_counter() - t0)
+        st = e.timing()
+        e.set_timing(False)
+        print(json.dumps({"flags": f, "same_as_first": same, "ms_per_call": round(float(np.median(ts)) * 1e3, 3),
+                          "stage_us_per_call": {k: round(v[0] * 1e3 / args.calls, 1) for k, v in st.items() if v[0] > 0}}))
+
+
+if __name__ == "__main__":
+    main()
