@@ -340,6 +340,29 @@ def _cdiv(n, m):
     return np.where(n >= 0, n // m, -((-n) // m))
 
 
+SIMD_LANES = 8  # CV_SIMD128 int16 lanes (OpenCV 3.x x86 builds: SSE2)
+
+
+def wta_best(S: np.ndarray, mode: int) -> np.ndarray:
+    """bestDisp among the minima of S over d (App. A.6).
+
+    MODE_HH (8 paths) takes the first minimum (scalar loop).  MODE_SGBM
+    (5 paths) fuses its WTA into the SIMD loop of the backward pass
+    (``if( useSIMD )`` branch of computeDisparitySGBM, always taken on x86):
+    lane i of an 8 x int16 register keeps the first minimum among
+    d = i, i+8, i+16, ... (strict ``_minS > L0``), and the winner is the
+    lowest lane holding the overall minimum (``LSBTab`` of the equality
+    mask).  So ties break by (d mod 8) first, then by d.
+    """
+    if mode != 5:
+        return S.argmin(-1)
+    D = S.shape[-1]
+    d = np.arange(D)
+    rank = (d % SIMD_LANES) * D + d
+    at_min = S == S.min(-1, keepdims=True)
+    return d[np.where(at_min, rank, np.iinfo(np.int64).max).argmin(-1)]
+
+
 def wta(S: np.ndarray, H, W, prm):
     """Returns disp (int16 [H, W], pre-median) following App. A.6."""
     minD, D = prm["minD"], prm["D"]
@@ -350,7 +373,7 @@ def wta(S: np.ndarray, H, W, prm):
     if width1 <= 0:
         return disp.astype(np.int16)
     u = prm["uniq"]
-    best = S.argmin(-1)                                  # first minimum
+    best = wta_best(S, prm["mode"])
     minS = S.min(-1)
     dd = np.arange(D)
     bad = ((S * (100 - u) < (minS * 100)[..., None])

@@ -384,6 +384,10 @@ static int compute_core(const uint8_t* img1, const uint8_t* img2, int H, int W, 
                         CostType* Sp = S + (size_t)x * D;
                         int minS = MAX_COST, bestDisp = -1, d;
                         if (npasses == 1) {
+                            /* CV_SIMD128 branch (x86): lane i keeps the first minimum among
+                             * d = i, i+8, ...; the lowest lane holding the overall minimum wins */
+                            int laneMin[8], laneBest[8];
+                            for (int i = 0; i < 8; i++) { laneMin[i] = MAX_COST; laneBest[i] = -1; }
                             int minL0 = MAX_COST;
                             int delta0 = MINLR(minLr[0], x + 1)[0] + P2;
                             CostType* Lr_p0 = LR(Lr[0], x + 1, 0);
@@ -396,9 +400,12 @@ static int compute_core(const uint8_t* img1, const uint8_t* img2, int H, int W, 
                                 minL0 = imin(minL0, L0);
                                 int sv = Sp[d] + L0;
                                 int Sval = Sp[d] = (CostType)(sv > MAX_COST ? MAX_COST : (sv < -32768 ? -32768 : sv));
-                                if (Sval < minS) { minS = Sval; bestDisp = d; }
+                                if (laneMin[d & 7] > Sval) { laneMin[d & 7] = Sval; laneBest[d & 7] = d; }
                             }
                             MINLR(minLr[0], x)[0] = (CostType)minL0;
+                            for (int i = 0; i < 8; i++) minS = imin(minS, laneMin[i]);
+                            for (int i = 0; i < 8; i++)
+                                if (laneMin[i] == minS) { bestDisp = laneBest[i]; break; }
                         } else {
                             for (d = 0; d < D; d++) {
                                 int Sval = Sp[d];

@@ -507,6 +507,7 @@ int launch_wta_t(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs)
     wa.uniq = n.uniq;
     wa.disp12 = n.disp12;
     wa.disp = (int16_t*)bs.raw.p;
+    wa.lane8 = n.ndirs == 5;
     dim3 grid(g.H, g.G);
     if (ctx->fb_guard) {
         wa.guard = ctx->fb_guard;

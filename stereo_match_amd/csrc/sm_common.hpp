@@ -7,6 +7,20 @@
 
 namespace smk {
 
+// WTA tie-break.  MODE_SGBM (5 paths) takes its winner inside OpenCV's CV_SIMD128
+// loop (x86 builds): each int16 lane (d mod 8) keeps its first minimum and the lowest
+// lane holding the overall minimum wins, so equal minima rank by (d mod 8, d)
+// (oracle/sgm_np.py:wta_best).  MODE_HH (8 paths) keeps the first minimum.  The rank
+// sits in the low 16 bits of the (S << 16 | rank) min-keys; D <= 256.
+__device__ __forceinline__ uint32_t wta_rank(int d, bool lane8)
+{
+    return lane8 ? ((((uint32_t)d & 7u) << 5) | ((uint32_t)d >> 3)) : (uint32_t)d;
+}
+__device__ __forceinline__ int wta_unrank(uint32_t r, bool lane8)
+{
+    return lane8 ? (int)(((r & 31u) << 3) | (r >> 5)) : (int)r;
+}
+
 constexpr int kMaxDirs = 8;
 constexpr uint32_t kBig = 0x7FFF;  // OpenCV MAX_COST used at d = -1 / d = D
 

@@ -464,6 +464,7 @@ struct WtaArgs {
     int16_t* disp;  // [pair][H][W] pre-median
     const uint16_t* part;  // hybrid engine: u16 S + SE + SW sums [pair][H][width1][D], or null
     size_t part_pair;      // elements
+    int lane8;             // 5 paths: OpenCV's SIMD tie-break among equal minima (wta_rank)
     // sweep fallback (see PathsArgs::guard): grid-stride over H x npairs rows; the
     // launch's first workgroup counts the fallback in *fallbacks
     const uint32_t* guard;
@@ -547,10 +548,10 @@ __device__ __forceinline__ void wta_row(const WtaArgs& a, const int y, const int
 #pragma unroll
         for (int i = 0; i < DPL; i++) {
             S[i] = min(S[i], 32767u);
-            key = min(key, (S[i] << 16) | (uint32_t)(g * DPL + i));
+            key = min(key, (S[i] << 16) | wta_rank(g * DPL + i, a.lane8));
         }
         key = row16_min(key);
-        const int minS = (int)(key >> 16), best = (int)(key & 0xFFFF);
+        const int minS = (int)(key >> 16), best = wta_unrank(key & 0xFFFF, a.lane8);
         uint32_t bad = 0, nb = 0;
 #pragma unroll
         for (int i = 0; i < DPL; i++) {

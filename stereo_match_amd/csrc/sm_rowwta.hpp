@@ -87,10 +87,10 @@ __device__ __forceinline__ void row_sweep(const RowArgs& a, int pair, int y, uin
 #pragma unroll
                 for (int k = 0; k < NOTHER; k++) acc += oth[k].template get<LT>(i);
                 S[i] = min(acc, 32767u);
-                kmin = min(kmin, (S[i] << 16) | (uint32_t)(lane * DPL + i));
+                kmin = min(kmin, (S[i] << 16) | wta_rank(lane * DPL + i, NDIR == 5));
             }
             kmin = Line<64>::min(kmin);
-            const int minS = (int)(kmin >> 16), best = (int)(kmin & 0xFFFF);
+            const int minS = (int)(kmin >> 16), best = wta_unrank(kmin & 0xFFFF, NDIR == 5);
             bool badl = false;
 #pragma unroll
             for (int i = 0; i < DPL; i++) {

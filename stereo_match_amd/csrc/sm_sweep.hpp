@@ -545,13 +545,13 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL>::THREADS)) k_sweep(SweepArg
                             Sp[i] = t;
                             S[2 * i] = t & 0xFFFFu;
                             S[2 * i + 1] = t >> 16;
-                            key = min(key, min((t << 16) | (uint32_t)(g * DPL + 2 * i),
-                                               (t & 0xFFFF0000u) | (uint32_t)(g * DPL + 2 * i + 1)));
+                            key = min(key, min((t << 16) | wta_rank(g * DPL + 2 * i, MODE == 1),
+                                               (t & 0xFFFF0000u) | wta_rank(g * DPL + 2 * i + 1, MODE == 1)));
                         }
                         lds_put_pk<NP>(&srow[(wave - 1) % (NCW - 2)][kl][g * DPL], Sp);
                         key = group_min<VL>(key);
                         const uint32_t minS = key >> 16;
-                        const int best = (int)(key & 0xFFFF);
+                        const int best = wta_unrank(key & 0xFFFF, MODE == 1);  // MODE 1 = 5 paths
                         const int bm = max(best - 1, 0), bq = min(best + 1, D - 1);
                         const uint32_t Sm = srow[(wave - 1) % (NCW - 2)][kl][bm];
                         const uint32_t Sq = srow[(wave - 1) % (NCW - 2)][kl][bq];
@@ -698,12 +698,12 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL>::THREADS)) k_sweep(SweepArg
                         if constexpr (MODE == 2) t += Pin[i];
                         if constexpr (sizeof(CT) == 2) t = min(t, 32767u);  // census sums stay below 2^11
                         S[i] = t;
-                        key = min(key, (t << 16) | (uint32_t)(g * DPL + i));
+                        key = min(key, (t << 16) | wta_rank(g * DPL + i, MODE == 1));
                     }
                     lds_put<DPL>(&srow[(wave - 1) % (NCW - 2)][kl][g * DPL], S);
                     key = group_min<VL>(key);
                     const uint32_t minS = key >> 16;
-                    const int best = (int)(key & 0xFFFF);
+                    const int best = wta_unrank(key & 0xFFFF, MODE == 1);  // MODE 1 = 5 paths
                     // far entries (|d - best| > 1) below the uniqueness threshold
                     uint32_t far = 0;
                     const int gb = g * DPL - best + 1;  // d - best + 1 of element 0

@@ -60,6 +60,39 @@ def test_k3_subpixel_c_truncation():
     assert _wta_one_pixel([900] * 15 + [3], 0) == 15 * DS
 
 
+def _wta_mode(S_row, mode):
+    D = len(S_row)
+    S = np.asarray(S_row, np.int64).reshape(1, 1, D)
+    prm = sgm_np.normalize_params(dict(numDisparities=D, uniquenessRatio=0, disp12MaxDiff=1000000, mode=mode))
+    return int(sgm_np.wta(S, 1, D + 1, prm)[0, D])
+
+
+def test_k7_simd_lane_tie_break():
+    """K7: MODE_SGBM's WTA runs in OpenCV's CV_SIMD128 loop (x86): with equal
+    minima at d=2 and d=9, lane 1 (d=9) beats lane 2 (d=2); MODE_HH's scalar
+    loop keeps the first minimum.  d=9 interpolates S[8..10] = 50,20,80:
+    den = 90, num = (50-80)*16+90 = -390, -390/180 = -2 (C) -> 9*16-2."""
+    S = [90] * 16
+    S[2] = S[9] = 20
+    S[1], S[3], S[8], S[10] = 40, 60, 50, 80
+    assert _wta_mode(S, 5) == 9 * DS - 2
+    # 8 paths: first minimum d=2, S[1..3] = 40,20,60: den 60, num (40-60)*16+60 = -260 -> -2
+    assert _wta_mode(S, 8) == 2 * DS - 2
+    # same lane: the smaller d wins in both modes
+    T = [90] * 16
+    T[3] = T[11] = 20
+    assert _wta_mode(T, 5) == _wta_mode(T, 8) == 3 * DS  # den 140, num 140 -> 140/280 = 0
+    # the rule in the vectorised helper: rank by (d mod 8, d)
+    rng = np.random.default_rng(3)
+    for _ in range(200):
+        row = rng.integers(0, 4, 32)
+        m = row.min()
+        cand = [d for d in range(32) if row[d] == m]
+        want = min(cand, key=lambda d: (d % 8, d))
+        assert int(sgm_np.wta_best(row[None], 5)[0]) == want
+        assert int(sgm_np.wta_best(row[None], 8)[0]) == cand[0]
+
+
 def test_k3b_all_saturated_is_invalid():
     """OpenCV's bestDisp stays -1 when every S == 32767 -> pixel invalid."""
     assert _wta_one_pixel([32767] * 16, 0) == -16
