@@ -38,6 +38,14 @@ def load():
         lib.sgm_ref_compute.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                         ctypes.c_int, ctypes.POINTER(SgmRefParams), ctypes.c_void_p,
                                         ctypes.c_int]
+        lib.sgm_ref_compute_cn.restype = ctypes.c_int
+        lib.sgm_ref_compute_cn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_int, ctypes.c_int, ctypes.POINTER(SgmRefParams),
+                                           ctypes.c_void_p, ctypes.c_int]
+        lib.sgm_ref_cost_volume_cn.restype = ctypes.c_int
+        lib.sgm_ref_cost_volume_cn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                               ctypes.c_int, ctypes.c_int, ctypes.POINTER(SgmRefParams),
+                                               ctypes.c_void_p, ctypes.c_void_p]
         lib.sgm_ref_compute_volume.restype = ctypes.c_int
         lib.sgm_ref_compute_volume.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                                ctypes.POINTER(SgmRefParams), ctypes.c_float, ctypes.c_float,
@@ -59,17 +67,39 @@ def make_params(p: dict) -> SgmRefParams:
 
 
 def compute(left: np.ndarray, right: np.ndarray, params: dict, median: bool = True) -> np.ndarray:
+    """uint8 [H, W] gray or [H, W, 3] BGR pairs (OpenCV's x86 SIMD arithmetic, sgm_ref.c header)."""
     lib = load()
     left = np.ascontiguousarray(left, np.uint8)
     right = np.ascontiguousarray(right, np.uint8)
-    H, W = left.shape
+    if left.shape != right.shape or left.ndim not in (2, 3) or (left.ndim == 3 and left.shape[2] != 3):
+        raise ValueError("left/right must be same-size uint8 [H, W] or [H, W, 3]")
+    H, W = left.shape[:2]
+    cn = 1 if left.ndim == 2 else 3
     out = np.empty((H, W), np.int16)
     prm = make_params(params)
-    rc = lib.sgm_ref_compute(left.ctypes.data, right.ctypes.data, H, W, W, ctypes.byref(prm),
-                             out.ctypes.data, int(bool(median)))
+    rc = lib.sgm_ref_compute_cn(left.ctypes.data, right.ctypes.data, H, W, W * cn, cn, ctypes.byref(prm),
+                                out.ctypes.data, int(bool(median)))
     if rc != 0:
         raise ValueError(f"sgm_ref_compute failed ({rc})")
     return out
+
+
+def cost_volume(left: np.ndarray, right: np.ndarray, params: dict) -> np.ndarray:
+    """OpenCV's int16 cost rows C[H][width1][D] (P2 seed included; SGBM cost only)."""
+    lib = load()
+    left = np.ascontiguousarray(left, np.uint8)
+    right = np.ascontiguousarray(right, np.uint8)
+    H, W = left.shape[:2]
+    cn = 1 if left.ndim == 2 else 3
+    minD, D = int(params.get("minDisparity", 0)), int(params.get("numDisparities", 16))
+    width1 = W + min(minD, 0) - max(minD + D, 0)
+    C = np.zeros((H, max(width1, 0), D), np.int16)
+    out = np.empty((H, W), np.int16)
+    rc = lib.sgm_ref_cost_volume_cn(left.ctypes.data, right.ctypes.data, H, W, W * cn, cn,
+                                    ctypes.byref(make_params(params)), C.ctypes.data, out.ctypes.data)
+    if rc != 0:
+        raise ValueError(f"sgm_ref_cost_volume_cn failed ({rc})")
+    return C
 
 
 def compute_volume(vol: np.ndarray, params: dict, offset: float = 0.0, scale: float = 1.0,

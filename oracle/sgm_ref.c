@@ -21,6 +21,17 @@
  *
  * The census cost (north-star mode, no reference counterpart) feeds the same
  * row engine: C(x,y,d) = popcount(census_l ^ census_r) (+P2 seed).
+ *
+ * Arithmetic follows OpenCV's x86 build, where hasSIMD128() is true and the
+ * CV_SIMD128 branches run (SSE2; OpenCV 3.x universal intrinsics, whose int16
+ * + and - saturate): the incremental box-sum update of C for y > 0, every
+ * L_r step and the S sums saturate to int16 (sat16), the delta = minLr + P2
+ * broadcast is a (short) cast (wrap16), and MODE_SGBM's winner is chosen
+ * per 8 x int16 lane (see the WTA below).  Row y == 0 of C and the x == 0
+ * horizontal sums run the scalar loops (int16 casts: wrap16).  Inside the
+ * int16-exact range the GPU's fast kernels cover (no sum can reach 2^15),
+ * saturating and plain arithmetic agree; outside it (large blockSize,
+ * preFilterCap, P2, colour input) these rules decide.
  */
 #include <stdint.h>
 #include <stdlib.h>
@@ -41,6 +52,8 @@ typedef struct {
 } sgm_ref_params;
 
 static inline int imin(int a, int b) { return a < b ? a : b; }
+static inline int sat16(int v) { return v > 32767 ? 32767 : (v < -32768 ? -32768 : v); }
+static inline int wrap16(int v) { return (int)(int16_t)(uint16_t)(unsigned)v; }
 static inline int imax(int a, int b) { return a > b ? a : b; }
 static inline int iabs(int a) { return a < 0 ? -a : a; }
 
@@ -64,9 +77,11 @@ void sgm_ref_census9x7(const uint8_t* img, int H, int W, int stride, uint64_t* o
 }
 
 /* ------------------------------------------------------ calcPixelCostBT */
-/* cost[x1*D + d] for x1 in [0,width1): BT(left x1+minX1, right x1+minX1-minD-d),
- * prefiltered channel (shift 0) + raw channel (shift 2). */
-static void calc_pixel_cost_bt(const uint8_t* img1, const uint8_t* img2, int stride,
+/* cost[x1*D + d] for x1 in [0,width1): BT(left x1+minX1, right x1+minX1-minD-d)
+ * summed over 2*cn channels: the clipped x-derivative of each colour channel
+ * (shift 0), then each raw channel (shift 2).  Rows hold cn interleaved bytes
+ * per pixel (cn = 1 gray, 3 BGR), stride in bytes. */
+static void calc_pixel_cost_bt(const uint8_t* img1, const uint8_t* img2, int stride, int cn,
                                int H, int W, int y, int minD, int maxD,
                                CostType* cost, uint8_t* tmp, const uint8_t* tab)
 {
@@ -77,25 +92,26 @@ static void calc_pixel_cost_bt(const uint8_t* img1, const uint8_t* img2, int str
     int n = y > 0 ? -stride : 0, s = y < H - 1 ? stride : 0;
     /* prow1[c][x] (left), prow2[c][W-1-x] (right, reversed like OpenCV) */
     uint8_t* prow1 = tmp;
-    uint8_t* prow2 = tmp + 2 * W;
-    uint8_t* buf0 = tmp + 4 * W; /* v0 */
-    uint8_t* buf1 = tmp + 5 * W; /* v1 */
-    for (int c = 0; c < 2; c++) {
+    uint8_t* prow2 = tmp + 2 * cn * W;
+    uint8_t* buf0 = tmp + 4 * cn * W; /* v0 */
+    uint8_t* buf1 = buf0 + W;         /* v1 */
+    for (int c = 0; c < 2 * cn; c++) {
         prow1[W * c] = prow1[W * c + W - 1] = prow2[W * c] = prow2[W * c + W - 1] = tab[0];
     }
-    for (int x = 1; x < W - 1; x++) {
-        prow1[x] = tab[(row1[x + 1] - row1[x - 1]) * 2 + row1[x + n + 1] - row1[x + n - 1] +
-                       row1[x + s + 1] - row1[x + s - 1]];
-        prow2[W - 1 - x] = tab[(row2[x + 1] - row2[x - 1]) * 2 + row2[x + n + 1] - row2[x + n - 1] +
-                               row2[x + s + 1] - row2[x + s - 1]];
-        prow1[x + W] = row1[x];
-        prow2[W - 1 - x + W] = row2[x];
-    }
+    for (int x = 1; x < W - 1; x++)
+        for (int ch = 0; ch < cn; ch++) {
+            int a = (x + 1) * cn + ch, b = (x - 1) * cn + ch;
+            prow1[x + W * ch] = tab[(row1[a] - row1[b]) * 2 + row1[a + n] - row1[b + n] + row1[a + s] - row1[b + s]];
+            prow2[W - 1 - x + W * ch] =
+                tab[(row2[a] - row2[b]) * 2 + row2[a + n] - row2[b + n] + row2[a + s] - row2[b + s]];
+            prow1[x + W * (cn + ch)] = row1[x * cn + ch];
+            prow2[W - 1 - x + W * (cn + ch)] = row2[x * cn + ch];
+        }
     memset(cost, 0, sizeof(CostType) * (size_t)width1 * D);
-    for (int c = 0; c < 2; c++) {
+    for (int c = 0; c < 2 * cn; c++) {
         const uint8_t* p1 = prow1 + W * c;
         const uint8_t* p2 = prow2 + W * c;
-        int diff_scale = c == 0 ? 0 : 2;
+        int diff_scale = c < cn ? 0 : 2;
         for (int x = 0; x < W; x++) {
             int v = p2[x];
             int vl = x > 0 ? (v + p2[x - 1]) / 2 : v;
@@ -201,11 +217,22 @@ static inline int quant_cost(float c, float offset, float scale)
     return (int)v;
 }
 
-static int compute_core(const uint8_t* img1, const uint8_t* img2, int H, int W, int stride, const float* vol,
-                        float vol_offset, float vol_scale, const sgm_ref_params* prm, int16_t* disp1,
-                        int apply_median)
+/* one L_r step of the SIMD loop: L = min(Lp[d], Lp[d-1]+P1, Lp[d+1]+P1, delta);
+ * L = (L - delta) + C, every + and - saturating to int16 (Lp[-1] = Lp[D] = MAX_COST) */
+static inline int l_step(const CostType* Lp, int d, int P1, int delta, int Cpd)
 {
-    if ((!vol && (!img1 || !img2 || stride < W)) || !disp1 || !prm || H <= 0 || W <= 0) return -1;
+    int v = imin((int)Lp[d], imin(sat16(Lp[d - 1] + P1), sat16(Lp[d + 1] + P1)));
+    v = imin(v, delta);
+    return sat16(sat16(v - delta) + Cpd);
+}
+
+static int compute_core(const uint8_t* img1, const uint8_t* img2, int H, int W, int stride, int cn,
+                        const float* vol, float vol_offset, float vol_scale, const sgm_ref_params* prm,
+                        int16_t* disp1, int apply_median, int16_t* dumpC)
+{
+    if ((!vol && (!img1 || !img2 || (cn != 1 && cn != 3) || stride < W * cn)) || !disp1 || !prm || H <= 0 ||
+        W <= 0)
+        return -1;
     int minD = prm->min_disparity, D = prm->num_disparities, maxD = minD + D;
     if (D <= 0 || D % 16) return -1;
     int bs = prm->block_size > 0 ? prm->block_size : 5;
@@ -247,9 +274,10 @@ static int compute_core(const uint8_t* img1, const uint8_t* img2, int H, int W, 
         }
         CostType* disp2cost = (CostType*)malloc(sizeof(CostType) * (size_t)W);
         int16_t* disp2 = (int16_t*)malloc(sizeof(int16_t) * (size_t)W);
-        uint8_t* tmp = (uint8_t*)malloc((size_t)W * 8);
+        uint8_t* tmp = (uint8_t*)malloc((size_t)W * (4 * cn + 2));
         uint64_t *cl = NULL, *cr = NULL;
         if (census) {
+            if (cn != 1) return -1;
             cl = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)H * W);
             cr = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)H * W);
             sgm_ref_census9x7(img1, H, W, stride, cl);
@@ -295,7 +323,7 @@ static int compute_core(const uint8_t* img1, const uint8_t* img2, int H, int W, 
                         for (int k = dy1; k <= dy2; k++) {
                             CostType* hsumAdd = hsumBuf + (size_t)(imin(k, H - 1) % hsumBufNRows) * costBufSize;
                             if (k < H) {
-                                calc_pixel_cost_bt(img1, img2, stride, H, W, k, minD, maxD, pixDiff, tmp,
+                                calc_pixel_cost_bt(img1, img2, stride, cn, H, W, k, minD, maxD, pixDiff, tmp,
                                                    clipTab + TAB_OFS);
                                 for (int d = 0; d < D; d++) {
                                     int acc = pixDiff[d] * (SW2 + 1);
@@ -306,14 +334,17 @@ static int compute_core(const uint8_t* img1, const uint8_t* img2, int H, int W, 
                                     const CostType* hsumSub =
                                         hsumBuf + (size_t)(imax(y - SH2 - 1, 0) % hsumBufNRows) * costBufSize;
                                     const CostType* Cprev = !fullDP || y == 0 ? C : C - costBufSize;
+                                    /* SIMD: v_load(Cprev) + v_load(hsumAdd) - v_load(hsumSub) */
                                     for (int d = 0; d < D; d++)
-                                        C[d] = (CostType)(Cprev[d] + hsumAdd[d] - hsumSub[d]);
+                                        C[d] = (CostType)sat16(sat16(Cprev[d] + hsumAdd[d]) - hsumSub[d]);
                                     for (size_t x = D; x < costBufSize; x += D) {
                                         const CostType* pixAdd = pixDiff + imin((int)x + SW2 * D, (width1 - 1) * D);
                                         const CostType* pixSub = pixDiff + imax((int)x - (SW2 + 1) * D, 0);
                                         for (int d = 0; d < D; d++) {
-                                            int hv = hsumAdd[x + d] = (CostType)(hsumAdd[x - D + d] + pixAdd[d] - pixSub[d]);
-                                            C[x + d] = (CostType)(Cprev[x + d] + hv - hsumSub[x + d]);
+                                            /* hv = hv - psub + padd; Cx = Cx - hsumSub + hv (all saturating) */
+                                            int hv = hsumAdd[x + d] =
+                                                (CostType)sat16(sat16(hsumAdd[x - D + d] - pixSub[d]) + pixAdd[d]);
+                                            C[x + d] = (CostType)sat16(sat16(Cprev[x + d] - hsumSub[x + d]) + hv);
                                         }
                                     }
                                 } else {
@@ -333,6 +364,8 @@ static int compute_core(const uint8_t* img1, const uint8_t* img2, int H, int W, 
                         }
                     }
                     memset(S, 0, sizeof(CostType) * costBufSize);
+                    if (dumpC) /* OpenCV's C row as stored (P2 seed included) */
+                        memcpy(dumpC + (size_t)y * costBufSize, C, sizeof(CostType) * costBufSize);
                 }
 
                 /* clear the left and right borders of the current Lr row */
@@ -341,12 +374,13 @@ static int compute_core(const uint8_t* img1, const uint8_t* img2, int H, int W, 
                 memset(MINLR(minLr[0], -1), 0, sizeof(CostType) * NR2);
                 memset(MINLR(minLr[0], width1), 0, sizeof(CostType) * NR2);
 
-                /* r0 = (-dx,0), r1 = (-1,-dy), r2 = (0,-dy), r3 = (1,-dy) */
+                /* r0 = (-dx,0), r1 = (-1,-dy), r2 = (0,-dy), r3 = (1,-dy); the
+                 * SIMD broadcast of delta = minLr + P2 is a (short) cast */
                 for (int x = x1; x != x2; x += dx) {
-                    int delta0 = MINLR(minLr[0], x - dx)[0] + P2;
-                    int delta1 = MINLR(minLr[1], x - 1)[1] + P2;
-                    int delta2 = MINLR(minLr[1], x)[2] + P2;
-                    int delta3 = MINLR(minLr[1], x + 1)[3] + P2;
+                    int delta0 = wrap16(MINLR(minLr[0], x - dx)[0] + P2);
+                    int delta1 = wrap16(MINLR(minLr[1], x - 1)[1] + P2);
+                    int delta2 = wrap16(MINLR(minLr[1], x)[2] + P2);
+                    int delta3 = wrap16(MINLR(minLr[1], x + 1)[3] + P2);
                     CostType* Lr_p0 = LR(Lr[0], x - dx, 0);
                     CostType* Lr_p1 = LR(Lr[1], x - 1, 1);
                     CostType* Lr_p2 = LR(Lr[1], x, 2);
@@ -358,16 +392,16 @@ static int compute_core(const uint8_t* img1, const uint8_t* img2, int H, int W, 
                     int minL0 = MAX_COST, minL1 = MAX_COST, minL2 = MAX_COST, minL3 = MAX_COST;
                     for (int d = 0; d < D; d++) {
                         int Cpd = Cp[d], L0, L1, L2, L3;
-                        L0 = Cpd + imin((int)Lr_p0[d], imin(Lr_p0[d - 1] + P1, imin(Lr_p0[d + 1] + P1, delta0))) - delta0;
-                        L1 = Cpd + imin((int)Lr_p1[d], imin(Lr_p1[d - 1] + P1, imin(Lr_p1[d + 1] + P1, delta1))) - delta1;
-                        L2 = Cpd + imin((int)Lr_p2[d], imin(Lr_p2[d - 1] + P1, imin(Lr_p2[d + 1] + P1, delta2))) - delta2;
-                        L3 = Cpd + imin((int)Lr_p3[d], imin(Lr_p3[d - 1] + P1, imin(Lr_p3[d + 1] + P1, delta3))) - delta3;
+                        L0 = l_step(Lr_p0, d, P1, delta0, Cpd);
+                        L1 = l_step(Lr_p1, d, P1, delta1, Cpd);
+                        L2 = l_step(Lr_p2, d, P1, delta2, Cpd);
+                        L3 = l_step(Lr_p3, d, P1, delta3, Cpd);
                         LR(Lr[0], x, 0)[d] = (CostType)L0; minL0 = imin(minL0, L0);
                         LR(Lr[0], x, 1)[d] = (CostType)L1; minL1 = imin(minL1, L1);
                         LR(Lr[0], x, 2)[d] = (CostType)L2; minL2 = imin(minL2, L2);
                         LR(Lr[0], x, 3)[d] = (CostType)L3; minL3 = imin(minL3, L3);
-                        int sv = Sp[d] + L0 + L1 + L2 + L3;
-                        Sp[d] = (CostType)(sv > MAX_COST ? MAX_COST : (sv < -32768 ? -32768 : sv));
+                        /* L0 = L0 + L1; L2 = L2 + L3; Sval = Sval + L0; Sval = Sval + L2 */
+                        Sp[d] = (CostType)sat16(sat16(Sp[d] + sat16(L0 + L1)) + sat16(L2 + L3));
                     }
                     CostType* mL = MINLR(minLr[0], x);
                     mL[0] = (CostType)minL0; mL[1] = (CostType)minL1;
@@ -389,17 +423,16 @@ static int compute_core(const uint8_t* img1, const uint8_t* img2, int H, int W, 
                             int laneMin[8], laneBest[8];
                             for (int i = 0; i < 8; i++) { laneMin[i] = MAX_COST; laneBest[i] = -1; }
                             int minL0 = MAX_COST;
-                            int delta0 = MINLR(minLr[0], x + 1)[0] + P2;
+                            int delta0 = wrap16(MINLR(minLr[0], x + 1)[0] + P2);
                             CostType* Lr_p0 = LR(Lr[0], x + 1, 0);
                             Lr_p0[-1] = Lr_p0[D] = MAX_COST;
                             CostType* Lr_p = LR(Lr[0], x, 0);
                             const CostType* Cp = C + (size_t)x * D;
                             for (d = 0; d < D; d++) {
-                                int L0 = Cp[d] + imin((int)Lr_p0[d], imin(Lr_p0[d - 1] + P1, imin(Lr_p0[d + 1] + P1, delta0))) - delta0;
+                                int L0 = l_step(Lr_p0, d, P1, delta0, Cp[d]);
                                 Lr_p[d] = (CostType)L0;
                                 minL0 = imin(minL0, L0);
-                                int sv = Sp[d] + L0;
-                                int Sval = Sp[d] = (CostType)(sv > MAX_COST ? MAX_COST : (sv < -32768 ? -32768 : sv));
+                                int Sval = Sp[d] = (CostType)sat16(L0 + Sp[d]);
                                 if (laneMin[d & 7] > Sval) { laneMin[d & 7] = Sval; laneBest[d & 7] = d; }
                             }
                             MINLR(minLr[0], x)[0] = (CostType)minL0;
@@ -465,7 +498,21 @@ done:
 int sgm_ref_compute(const uint8_t* img1, const uint8_t* img2, int H, int W, int stride,
                     const sgm_ref_params* prm, int16_t* disp1, int apply_median)
 {
-    return compute_core(img1, img2, H, W, stride, NULL, 0.f, 1.f, prm, disp1, apply_median);
+    return compute_core(img1, img2, H, W, stride, 1, NULL, 0.f, 1.f, prm, disp1, apply_median, NULL);
+}
+
+/* cn-channel input (1 gray, 3 BGR interleaved), stride in bytes */
+int sgm_ref_compute_cn(const uint8_t* img1, const uint8_t* img2, int H, int W, int stride, int cn,
+                       const sgm_ref_params* prm, int16_t* disp1, int apply_median)
+{
+    return compute_core(img1, img2, H, W, stride, cn, NULL, 0.f, 1.f, prm, disp1, apply_median, NULL);
+}
+
+/* the cost volume C[H][width1][D] as OpenCV holds it for each row (int16, P2 seed included) */
+int sgm_ref_cost_volume_cn(const uint8_t* img1, const uint8_t* img2, int H, int W, int stride, int cn,
+                           const sgm_ref_params* prm, int16_t* C, int16_t* disp1)
+{
+    return compute_core(img1, img2, H, W, stride, cn, NULL, 0.f, 1.f, prm, disp1, 0, C);
 }
 
 /* SGM over an external d-major float32 cost volume vol[D][H][W] (mc-cnn). */
@@ -473,5 +520,5 @@ int sgm_ref_compute_volume(const float* vol, int H, int W, const sgm_ref_params*
                            int16_t* disp1, int apply_median)
 {
     if (!vol) return -1;
-    return compute_core(NULL, NULL, H, W, W, vol, offset, scale, prm, disp1, apply_median);
+    return compute_core(NULL, NULL, H, W, W, 1, vol, offset, scale, prm, disp1, apply_median, NULL);
 }

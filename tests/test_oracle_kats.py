@@ -288,3 +288,31 @@ def test_bm_validate_and_arguments():
     for bad in (dict(blockSize=4), dict(blockSize=6), dict(numDisparities=24), dict(preFilterCap=64)):
         with pytest.raises(ValueError):
             bm_np.stereo_bm(left, right, dict(dict(numDisparities=32, blockSize=7), **bad))
+
+
+def test_k8_int16_wrap_and_saturation_of_the_box_sums():
+    """K8 (x86 OpenCV arithmetic, oracle/sgm_ref.c header): constant 0 vs
+    255 pair, disparity_test.py's blockSize 23 / preFilterCap 1 / P2 887.
+    Interior pixel cost = (255 >> 2) = 63 (the clipped derivatives are flat),
+    horizontal sum 23 * 63 = 1449.  Row 0 of C is built by the scalar loop
+    with int16 casts: 887 + 12 * 1449 + 11 * 1449 wraps to -31322.  Rows >= 1
+    use the saturating SIMD update (C - hsumSub) + hsumAdd: -31322 - 1449
+    saturates at -32768, + 1449 = -31319, and stays there."""
+    p = dict(minDisparity=0, numDisparities=16, blockSize=23, P1=222, P2=887, disp12MaxDiff=20,
+             uniquenessRatio=0, preFilterCap=1, mode=5, cost=0)
+    l = np.zeros((40, 80), np.uint8)
+    r = np.full((40, 80), 255, np.uint8)
+    C = ref_c.cost_volume(l, r, p)
+    assert (C[0, 12:51] == -31322).all()  # windows clear of the border columns
+    assert (C[1:, 12:51] == -31319).all()
+
+
+def test_k9_colour_replicated_channels():
+    """K9: a BGR pair whose three channels equal the gray pair costs three
+    times the gray cost per pixel (each channel adds its own derivative and
+    raw BT terms), inside the int16-exact range."""
+    l, r, _ = synthetic.random_dot_pair(30, 90, 16, seed=4)
+    p = dict(synthetic.parity_params(16), blockSize=3, P1=10, P2=96)
+    C1 = ref_c.cost_volume(l, r, p).astype(np.int64)
+    C3 = ref_c.cost_volume(np.repeat(l[..., None], 3, -1), np.repeat(r[..., None], 3, -1), p).astype(np.int64)
+    assert np.array_equal(C3 - 96, 3 * (C1 - 96))
