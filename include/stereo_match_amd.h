@@ -88,6 +88,20 @@ int sm_compute_batch_device(sm_ctx* ctx, const uint8_t* d_left, const uint8_t* d
                             size_t pair_stride_bytes, int H, int W, int stride, const sm_params* p,
                             int16_t* d_disp_out);
 
+/* The same two entry points for cn-channel images (OpenCV's StereoSGBM takes
+ * gray or BGR; the reference's try_try.py:56-57,81 passes cv2.imread BGR
+ * images): channels = 1 or 3 interleaved bytes per pixel, stride in bytes
+ * (>= W*channels), pair_stride in bytes.  BGR input and configurations whose
+ * sums can reach 2^15 (blockSize > 11, large preFilterCap / P2: e.g.
+ * disparity_test.py:165-177) run OpenCV's x86 int16 arithmetic exactly
+ * (sm_wide.hpp); the rest take the fast kernels.  blockSize <= 55,
+ * preFilterCap <= 126. */
+int sm_compute_cn(sm_ctx* ctx, const uint8_t* left, const uint8_t* right, int H, int W, int stride, int channels,
+                  const sm_params* p, int16_t* disp_out);
+int sm_compute_batch_device_cn(sm_ctx* ctx, const uint8_t* d_left, const uint8_t* d_right, int npairs,
+                               size_t pair_stride, int H, int W, int stride, int channels, const sm_params* p,
+                               int16_t* d_out);
+
 /* SGM over an external matching-cost volume (mc-cnn; the reference memmaps
  * one as float32 (1, D, H, W) at mapTo3D_mc_cnn.py:71 and feeds its
  * disparities to the WLS filter, :81-100).  cost: float32 [D][H][W], d-major,

@@ -72,6 +72,11 @@ _SIGS = {
                                      _c.POINTER(SmParams), _c.c_void_p]),
     "sm_compute_batch_device": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_int, _c.c_size_t,
                                            _c.c_int, _c.c_int, _c.c_int, _c.POINTER(SmParams), _c.c_void_p]),
+    "sm_compute_cn": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_int, _c.c_int, _c.c_int, _c.c_int,
+                                 _c.POINTER(SmParams), _c.c_void_p]),
+    "sm_compute_batch_device_cn": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_int, _c.c_size_t,
+                                              _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.POINTER(SmParams),
+                                              _c.c_void_p]),
     "sm_aggregate_cost_f32": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_int, _c.c_int, _c.c_int,
                                          _c.POINTER(SmParams), _c.c_float, _c.c_float, _c.c_void_p]),
     "sm_aggregate_cost_f32_device": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_int, _c.c_size_t, _c.c_int,
@@ -231,12 +236,14 @@ class Engine:
 
     # -- host arrays -------------------------------------------------------
     def compute(self, left: np.ndarray, right: np.ndarray, params: SmParams) -> np.ndarray:
+        """uint8 [H, W] gray or [H, W, 3] BGR pairs -> int16 [H, W] disparity x16."""
         left = np.ascontiguousarray(left)
         right = np.ascontiguousarray(right)
-        H, W = left.shape
+        H, W = left.shape[:2]
+        cn = 1 if left.ndim == 2 else left.shape[2]
         out = np.empty((H, W), np.int16)
-        self._check(self._lib.sm_compute(self.ctx, left.ctypes.data, right.ctypes.data, H, W, W,
-                                         ctypes.byref(params), out.ctypes.data))
+        self._check(self._lib.sm_compute_cn(self.ctx, left.ctypes.data, right.ctypes.data, H, W, W * cn, cn,
+                                            ctypes.byref(params), out.ctypes.data))
         return out
 
     # -- device pointers (e.g. torch tensors' data_ptr()) -------------------
@@ -246,10 +253,10 @@ class Engine:
                                                 H, W, stride, ctypes.byref(params), ctypes.c_void_p(d_out)))
 
     def compute_batch_device(self, d_left: int, d_right: int, npairs: int, pair_stride: int, H: int, W: int,
-                             stride: int, params: SmParams, d_out: int):
-        self._check(self._lib.sm_compute_batch_device(
+                             stride: int, params: SmParams, d_out: int, channels: int = 1):
+        self._check(self._lib.sm_compute_batch_device_cn(
             self.ctx, ctypes.c_void_p(d_left), ctypes.c_void_p(d_right), npairs, pair_stride, H, W, stride,
-            ctypes.byref(params), ctypes.c_void_p(d_out)))
+            channels, ctypes.byref(params), ctypes.c_void_p(d_out)))
 
     # -- external cost volume (mc-cnn) ----------------------------------------
     def aggregate_cost_f32(self, vol: np.ndarray, params: SmParams, offset: float = 0.0,

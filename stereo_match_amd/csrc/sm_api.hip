@@ -34,6 +34,7 @@
 #include "sm_speckle.hpp"
 #include "sm_reproject.hpp"
 #include "sm_bm.hpp"
+#include "sm_wide.hpp"
 #include "sm_sweep_host.hpp"
 
 #define SM_VERSION "stereo_match_amd 0.2.0 (gfx950)"
@@ -50,6 +51,8 @@ struct DevBuf {
 struct Norm {
     int minD, D, maxD, bs, P1, P2, ftzero, uniq, disp12, speckle_ws, speckle_range, cost, mode;
     int minX1, maxX1, width1, ndirs, dpl;
+    int cn;    // input channels (1 gray, 3 BGR)
+    bool wide;  // SGBM cost outside the int16-exact range (or BGR): sm_wide.hpp path
 };
 
 struct TimedEvent {
@@ -155,7 +158,7 @@ int ensure(sm_ctx* ctx, DevBuf& b, size_t bytes)
     return SM_OK;
 }
 
-int normalize(sm_ctx* ctx, const sm_params* p, int H, int W, Norm& n)
+int normalize(sm_ctx* ctx, const sm_params* p, int H, int W, Norm& n, int cn = 1)
 {
     if (!p) return fail(ctx, SM_E_ARG, "params is NULL");
     if (H <= 0 || W <= 0) return fail(ctx, SM_E_ARG, "empty image (%dx%d)", W, H);
@@ -180,20 +183,27 @@ int normalize(sm_ctx* ctx, const sm_params* p, int H, int W, Norm& n)
         return fail(ctx, SM_E_ARG, "cost_kind %d unknown", n.cost);
     if (n.mode != SM_MODE_SGBM && n.mode != SM_MODE_HH)
         return fail(ctx, SM_E_UNSUPPORTED, "mode %d not supported (5 = MODE_SGBM, 8 = MODE_HH)", n.mode);
+    if (cn != 1 && cn != 3) return fail(ctx, SM_E_ARG, "images must have 1 or 3 channels (got %d)", cn);
+    if (cn != 1 && n.cost != SM_COST_SGBM) return fail(ctx, SM_E_UNSUPPORTED, "colour input needs the SGBM cost");
+    n.cn = cn;
+    n.wide = false;
     if (n.cost == SM_COST_SGBM) {
-        if (n.bs > 2 * 5 + 1) return fail(ctx, SM_E_UNSUPPORTED, "blockSize %d > 11 not built", n.bs);
+        // the fast kernels need every sum below 2^15 (no int16 saturation or wrap);
+        // outside that, and for BGR input, the sm_wide.hpp path restates OpenCV's
+        // x86 int16 arithmetic.  Window side 2*(bs/2)+1, as OpenCV's SW2 = bs/2.
+        const int side = 2 * (n.bs / 2) + 1;
         const int maxpix = 2 * n.ftzero + (255 >> 2);
-        if ((long long)n.bs * n.bs * maxpix + n.P2 > 16383)
-            return fail(ctx, SM_E_UNSUPPORTED,
-                        "blockSize=%d/preFilterCap/P2=%d outside the int16-exact range (bs^2*(2*ftzero+63)+P2 <= 16383)",
-                        n.bs, n.P2);
+        n.wide = cn != 1 || n.bs / 2 > 5 || (long long)side * side * maxpix + n.P2 > 16383;
+        if (n.ftzero > 127) return fail(ctx, SM_E_UNSUPPORTED, "preFilterCap %d > 126 not built", p->pre_filter_cap);
+        if (n.bs / 2 > 27) return fail(ctx, SM_E_UNSUPPORTED, "blockSize %d > 55 not built", n.bs);
+        if (n.P1 > 32767 || n.P2 > 32767) return fail(ctx, SM_E_UNSUPPORTED, "P1/P2 above 32767 not built");
     } else if (n.cost == SM_COST_CENSUS) {
         if (62 + n.P2 > 255) return fail(ctx, SM_E_UNSUPPORTED, "census mode needs P2 <= 193 (8-bit path values)");
     } else {
         if (smk::VOL_CMAX + n.P2 > 16383)
             return fail(ctx, SM_E_UNSUPPORTED, "cost-volume mode needs P2 <= %d", 16383 - smk::VOL_CMAX);
     }
-    if (n.P1 > 16383 || n.P2 > 16383) return fail(ctx, SM_E_UNSUPPORTED, "P1/P2 too large");
+    if (!n.wide && (n.P1 > 16383 || n.P2 > 16383)) return fail(ctx, SM_E_UNSUPPORTED, "P1/P2 too large");
     n.minX1 = std::max(n.maxD, 0);
     n.maxX1 = W + std::min(n.minD, 0);
     n.width1 = n.maxX1 - n.minX1;
@@ -925,6 +935,141 @@ int run_speckles(sm_ctx* ctx, hipStream_t st, int16_t* img, int G, int H, int W,
     return SM_OK;
 }
 
+// median + speckle filter of a launch group's pre-median maps (bs.raw -> d_out) on
+// stream sb, and the bookkeeping sm_debug_fetch reads
+int finish_group(sm_ctx* ctx, const Geo& g, const Norm& n, BufSet& bs, int s, int16_t* d_out, hipStream_t sb)
+{
+    const int H = g.H, W = g.W, G = g.G;
+    int rc;
+    {
+        StageTimer t(ctx, sb, SM_STAGE_MEDIAN, G);
+        hipLaunchKernelGGL(smk::k_median3, dim3((W + 255) / 256, H, G), dim3(256), 0, sb,
+                           (const int16_t*)bs.raw.p, d_out, H, W, (size_t)H * W);
+        HIP_TRY(ctx, hipGetLastError());
+    }
+    if (n.speckle_ws > 0) {  // filterSpeckles(disp, INVALID, speckleWindowSize, 16*speckleRange)
+        if ((rc = run_speckles(ctx, sb, d_out, G, H, W, (n.minD - 1) * 16, n.speckle_ws, 16 * n.speckle_range)) !=
+            SM_OK)
+            return rc;
+    }
+    if (sb != ctx->stream) {
+        HIP_TRY(ctx, hipEventRecord(bs.wta_done, sb));
+        bs.pending = true;
+    }
+    ctx->last_width1 = n.width1;
+    ctx->last_index = G - 1;
+    ctx->last_L_pair = g.L_pair;
+    ctx->last_set = s;
+    return SM_OK;
+}
+
+// OpenCV-SGBM outside the int16-exact range or on BGR input (sm_wide.hpp): planes
+// per channel -> horizontal box sums -> OpenCV's row-by-row int16 C -> int16 path
+// lines -> saturating S + WTA + LR check, all on the caller's stream, into bs.raw
+template <int DPL>
+int wide_paths_wta(sm_ctx* ctx, const Geo& g, const Norm& n, BufSet& bs)
+{
+    smk::WidePathArgs pa{};
+    pa.C = (const int16_t*)bs.cost.p;
+    pa.vol = g.vol;
+    pa.L = (uint8_t*)bs.L.p;
+    pa.slot_bytes = g.slot_bytes;
+    pa.L_pair_bytes = g.L_pair;
+    pa.H = g.H;
+    pa.width1 = n.width1;
+    pa.D = n.D;
+    pa.P1 = n.P1;
+    pa.P2 = n.P2;
+    pa.ndirs = n.ndirs;
+    const int dys[8] = {0, 0, 1, 1, 1, -1, -1, -1}, dxs[8] = {1, -1, 1, 0, -1, 1, 0, -1};
+    int blocks = 0;
+    for (int k = 0; k < n.ndirs; k++) {
+        pa.blk_start[k] = blocks;
+        const int nl = dys[k] == 0 ? g.H : dxs[k] == 0 ? n.width1 : n.width1 + g.H - 1;
+        blocks += (nl + 15) / 16;
+    }
+    for (int k = n.ndirs; k <= 8; k++) pa.blk_start[k] = blocks;
+    {
+        StageTimer t(ctx, ctx->stream, SM_STAGE_PATHS, g.G);
+        hipLaunchKernelGGL((smk::k_wide_paths<DPL>), dim3(blocks, g.G), dim3(256), 0, ctx->stream, pa);
+        HIP_TRY(ctx, hipGetLastError());
+    }
+    smk::WideWtaArgs wa{};
+    wa.L = (const uint8_t*)bs.L.p;
+    wa.slot_bytes = g.slot_bytes;
+    wa.L_pair_bytes = g.L_pair;
+    wa.H = g.H;
+    wa.W = g.W;
+    wa.width1 = n.width1;
+    wa.D = n.D;
+    wa.minD = n.minD;
+    wa.minX1 = n.minX1;
+    wa.uniq = n.uniq;
+    wa.disp12 = n.disp12;
+    wa.ndirs = n.ndirs;
+    wa.disp = (int16_t*)bs.raw.p;
+    StageTimer t(ctx, ctx->stream, SM_STAGE_WTA, g.G);
+    hipLaunchKernelGGL((smk::k_wide_wta<DPL, 1024>), dim3(g.H, g.G), dim3(1024), (size_t)g.W * 8, ctx->stream, wa);
+    HIP_TRY(ctx, hipGetLastError());
+    return SM_OK;
+}
+
+int run_wide(sm_ctx* ctx, const Src& src, const Geo& g, const Norm& n, BufSet& bs)
+{
+    const int H = g.H, W = g.W, G = g.G;
+    int rc;
+    {
+        StageTimer t(ctx, ctx->stream, SM_STAGE_COST, G);
+        if ((rc = ensure(ctx, ctx->planes, (size_t)G * 2 * n.cn * H * W * 8)) != SM_OK) return rc;
+        if ((rc = ensure(ctx, bs.cost, (size_t)G * g.vol * 2)) != SM_OK) return rc;
+        if ((rc = ensure(ctx, bs.part, (size_t)G * g.vol * 2)) != SM_OK) return rc;  // horizontal sums
+        smk::PrefilterArgs pf{};
+        pf.img[0] = src.L;
+        pf.img[1] = src.R;
+        pf.in_pair = src.pair_stride;
+        pf.planes = (uint8_t*)ctx->planes.p;
+        pf.H = H;
+        pf.W = W;
+        pf.stride = g.stride;
+        pf.ftzero = n.ftzero;
+        pf.cn = n.cn;
+        hipLaunchKernelGGL(smk::k_sgbm_prefilter, dim3((W + 255) / 256, H, 2 * G * n.cn), dim3(256), 0, ctx->stream,
+                           pf);
+        HIP_TRY(ctx, hipGetLastError());
+        smk::WideArgs wa{};
+        wa.planes = (const uint2*)ctx->planes.p;
+        wa.hsum = (int16_t*)bs.part.p;
+        wa.C = (int16_t*)bs.cost.p;
+        wa.vol = g.vol;
+        wa.H = H;
+        wa.W = W;
+        wa.width1 = n.width1;
+        wa.D = n.D;
+        wa.minD = n.minD;
+        wa.minX1 = n.minX1;
+        wa.cn = n.cn;
+        wa.SW2 = n.bs / 2;
+        wa.SH2 = n.bs / 2;
+        wa.P2 = n.P2;
+        wa.hh = n.mode == SM_MODE_HH;
+        constexpr int TX = 64;
+        hipLaunchKernelGGL((smk::k_wide_hsum<TX>), dim3((n.width1 + TX - 1) / TX, H, G), dim3(256),
+                           (size_t)(TX + 2 * wa.SW2) * n.D * 2, ctx->stream, wa);
+        HIP_TRY(ctx, hipGetLastError());
+        hipLaunchKernelGGL(smk::k_wide_vscan, dim3((unsigned)((g.vol / H + 255) / 256), G), dim3(256), 0,
+                           ctx->stream, wa);
+        HIP_TRY(ctx, hipGetLastError());
+    }
+    switch (n.dpl) {
+#define CASE(k) \
+    case k: return wide_paths_wta<k>(ctx, g, n, bs);
+        CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
+        CASE(9) CASE(10) CASE(11) CASE(12) CASE(13) CASE(14) CASE(15) CASE(16)
+#undef CASE
+    default: return fail(ctx, SM_E_UNSUPPORTED, "numDisparities %d not built", n.D);
+    }
+}
+
 // G pairs (device pointers; pair i at dL + i*pair_stride).
 int run_group(sm_ctx* ctx, const Src& src, const Geo& g, const Norm& n, int16_t* d_out)
 {
@@ -952,6 +1097,10 @@ int run_group(sm_ctx* ctx, const Src& src, const Geo& g, const Norm& n, int16_t*
     }
     if ((rc = ensure(ctx, bs.L, g.L_pair * G)) != SM_OK) return rc;
     if ((rc = ensure(ctx, bs.raw, (size_t)G * H * W * 2)) != SM_OK) return rc;
+    if (n.wide) {
+        if ((rc = run_wide(ctx, src, g, n, bs)) != SM_OK) return rc;
+        return finish_group(ctx, g, n, bs, s, d_out, ctx->stream);
+    }
     {
         StageTimer t(ctx, ctx->stream, SM_STAGE_COST, G);
         if (n.cost == SM_COST_CENSUS) {
@@ -1020,6 +1169,7 @@ int run_group(sm_ctx* ctx, const Src& src, const Geo& g, const Norm& n, int16_t*
             pf.W = W;
             pf.stride = g.stride;
             pf.ftzero = n.ftzero;
+            pf.cn = 1;
             hipLaunchKernelGGL(smk::k_sgbm_prefilter, dim3((W + 255) / 256, H, 2 * G), dim3(256), 0, ctx->stream, pf);
             HIP_TRY(ctx, hipGetLastError());
             smk::SgbmCostArgs sc{};
@@ -1092,26 +1242,7 @@ int run_group(sm_ctx* ctx, const Src& src, const Geo& g, const Norm& n, int16_t*
         HIP_TRY(ctx, hipStreamWaitEvent(sb, bs.paths_done, 0));
     }
     if (!g.sweep && (rc = dispatch(ctx, n, g, bs, DISPATCH_WTA)) != SM_OK) return rc;
-    {
-        StageTimer t(ctx, sb, SM_STAGE_MEDIAN, G);
-        hipLaunchKernelGGL(smk::k_median3, dim3((W + 255) / 256, H, G), dim3(256), 0, sb,
-                           (const int16_t*)bs.raw.p, d_out, H, W, (size_t)H * W);
-        HIP_TRY(ctx, hipGetLastError());
-    }
-    if (n.speckle_ws > 0) {  // filterSpeckles(disp, INVALID, speckleWindowSize, 16*speckleRange)
-        if ((rc = run_speckles(ctx, sb, d_out, G, H, W, (n.minD - 1) * 16, n.speckle_ws, 16 * n.speckle_range)) !=
-            SM_OK)
-            return rc;
-    }
-    if (sb != ctx->stream) {
-        HIP_TRY(ctx, hipEventRecord(bs.wta_done, sb));
-        bs.pending = true;
-    }
-    ctx->last_width1 = n.width1;
-    ctx->last_index = G - 1;
-    ctx->last_L_pair = g.L_pair;
-    ctx->last_set = s;
-    return SM_OK;
+    return finish_group(ctx, g, n, bs, s, d_out, sb);
 }
 
 int run_pairs(sm_ctx* ctx, const Src& src, int npairs, int H, int W, int stride, const Norm& n, int16_t* d_out)
@@ -1129,8 +1260,8 @@ int run_pairs(sm_ctx* ctx, const Src& src, int npairs, int H, int W, int stride,
     g.stride = stride;
     g.vol = (size_t)H * std::max(n.width1, 0) * n.D;
     g.slot_bytes = (g.vol * elem_bytes(n) + 255) & ~size_t(255);
-    g.hybrid = use_hybrid(ctx, n, H);
-    g.sweep = !g.hybrid && use_sweep(ctx, n, H);
+    g.hybrid = !n.wide && use_hybrid(ctx, n, H);
+    g.sweep = !n.wide && !g.hybrid && use_sweep(ctx, n, H);
     // sweep engine: E and W volumes in slots 0/1 plus room for every direction's volume
     // (written only by the guarded fallback); hybrid: E, W (+ NE, N, NW at 8 paths)
     g.L_pair = g.slot_bytes * (g.hybrid ? hybrid_slots(n) : n.ndirs);
@@ -1544,16 +1675,16 @@ int sm_compute_device(sm_ctx* ctx, const uint8_t* dL, const uint8_t* dR, int H, 
     return run_pairs(ctx, src, 1, H, W, stride, n, d_out);
 }
 
-int sm_compute_batch_device(sm_ctx* ctx, const uint8_t* dL, const uint8_t* dR, int npairs, size_t pair_stride,
-                            int H, int W, int stride, const sm_params* p, int16_t* d_out)
+int sm_compute_batch_device_cn(sm_ctx* ctx, const uint8_t* dL, const uint8_t* dR, int npairs, size_t pair_stride,
+                               int H, int W, int stride, int channels, const sm_params* p, int16_t* d_out)
 {
     if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
     if (npairs < 0) return fail(ctx, SM_E_ARG, "npairs < 0");
     if (!dL || !dR || !d_out) return fail(ctx, SM_E_ARG, "NULL image/output pointer");
-    if (stride < W) return fail(ctx, SM_E_ARG, "stride %d < width %d", stride, W);
     Norm n;
-    int rc = normalize(ctx, p, H, W, n);
+    int rc = normalize(ctx, p, H, W, n, channels);
     if (rc != SM_OK) return rc;
+    if (stride < W * channels) return fail(ctx, SM_E_ARG, "stride %d < width %d x %d channels", stride, W, channels);
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     Src src;
     src.L = dL;
@@ -1562,32 +1693,45 @@ int sm_compute_batch_device(sm_ctx* ctx, const uint8_t* dL, const uint8_t* dR, i
     return run_pairs(ctx, src, npairs, H, W, stride, n, d_out);
 }
 
-int sm_compute(sm_ctx* ctx, const uint8_t* L, const uint8_t* R, int H, int W, int stride, const sm_params* p,
-               int16_t* disp_out)
+int sm_compute_batch_device(sm_ctx* ctx, const uint8_t* dL, const uint8_t* dR, int npairs, size_t pair_stride,
+                            int H, int W, int stride, const sm_params* p, int16_t* d_out)
+{
+    return sm_compute_batch_device_cn(ctx, dL, dR, npairs, pair_stride, H, W, stride, 1, p, d_out);
+}
+
+int sm_compute_cn(sm_ctx* ctx, const uint8_t* L, const uint8_t* R, int H, int W, int stride, int channels,
+                  const sm_params* p, int16_t* disp_out)
 {
     if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
     if (!L || !R || !disp_out) return fail(ctx, SM_E_ARG, "NULL image/output pointer");
-    if (stride < W) return fail(ctx, SM_E_ARG, "stride %d < width %d", stride, W);
     Norm n;
-    int rc = normalize(ctx, p, H, W, n);
+    int rc = normalize(ctx, p, H, W, n, channels);
     if (rc != SM_OK) return rc;
+    const size_t row = (size_t)W * channels;
+    if ((size_t)stride < row) return fail(ctx, SM_E_ARG, "stride %d < width %d x %d channels", stride, W, channels);
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    const size_t img = (size_t)H * W;
+    const size_t img = (size_t)H * row;
     for (int i = 0; i < 2; i++)
         if ((rc = ensure(ctx, ctx->img[i], img)) != SM_OK) return rc;
-    if ((rc = ensure(ctx, ctx->out, img * 2)) != SM_OK) return rc;
+    if ((rc = ensure(ctx, ctx->out, (size_t)H * W * 2)) != SM_OK) return rc;
     HostStage hs(ctx);
-    if ((rc = hs.reserve(stage_bytes(img, 2) + stage_bytes(img * 2))) != SM_OK) return rc;
-    if ((rc = hs.in(ctx->img[0].p, L, H, W, stride)) != SM_OK) return rc;
-    if ((rc = hs.in(ctx->img[1].p, R, H, W, stride)) != SM_OK) return rc;
+    if ((rc = hs.reserve(stage_bytes(img, 2) + stage_bytes((size_t)H * W * 2))) != SM_OK) return rc;
+    if ((rc = hs.in(ctx->img[0].p, L, H, row, stride)) != SM_OK) return rc;
+    if ((rc = hs.in(ctx->img[1].p, R, H, row, stride)) != SM_OK) return rc;
     Src src;
     src.L = (const uint8_t*)ctx->img[0].p;
     src.R = (const uint8_t*)ctx->img[1].p;
-    rc = run_pairs(ctx, src, 1, H, W, W, n, (int16_t*)ctx->out.p);
+    rc = run_pairs(ctx, src, 1, H, W, (int)row, n, (int16_t*)ctx->out.p);
     if (rc != SM_OK) return rc;
-    if ((rc = hs.out(disp_out, ctx->out.p, img * 2)) != SM_OK) return rc;
+    if ((rc = hs.out(disp_out, ctx->out.p, (size_t)H * W * 2)) != SM_OK) return rc;
     if ((rc = hs.finish()) != SM_OK) return rc;
     return check_sweep_errors(ctx);
+}
+
+int sm_compute(sm_ctx* ctx, const uint8_t* L, const uint8_t* R, int H, int W, int stride, const sm_params* p,
+               int16_t* disp_out)
+{
+    return sm_compute_cn(ctx, L, R, H, W, stride, 1, p, disp_out);
 }
 
 int sm_aggregate_cost_f32_device(sm_ctx* ctx, const float* d_cost, int npairs, size_t pair_stride_elems, int D,

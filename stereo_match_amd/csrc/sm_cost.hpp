@@ -171,26 +171,30 @@ __global__ void __launch_bounds__(256) k_census_cost(CensusCostArgs a)
 struct PrefilterArgs {
     const uint8_t* img[2];
     size_t in_pair;  // bytes between pairs' images
-    uint8_t* planes;  // packed uint2 per pixel, [pair][view][H][W]
+    uint8_t* planes;  // packed uint2 per pixel, [pair][view][channel][H][W]
     int H, W, stride, ftzero;
+    int cn;  // channels per pixel (1 gray, 3 BGR interleaved; 0 = 1); stride in bytes
 };
 
 // Packed per-pixel planes for the BT cost: one uint2 per pixel per view,
 // bytes [g, g_min, g_max, raw, raw_min, raw_max, 0, 0] (g = clipped Sobel-x,
 // min/max over the half-pixel neighbours as calcPixelCostBT); blockIdx.z =
-// 2*pair + view.
+// (2*pair + view)*cn + channel (colour: one plane per channel, as OpenCV's
+// calcPixelCostBT keeps a derivative and a raw row per channel).
 __global__ void __launch_bounds__(256) k_sgbm_prefilter(PrefilterArgs a)
 {
     // one workgroup per (256 columns, row, view): the three image rows (+2 halo
     // columns each side) and the clipped Sobel of columns x0-1 .. x0+256 in LDS
     __shared__ uint8_t rows[3][260];
     __shared__ int gs[258];
-    const int x0 = blockIdx.x * 256, y = blockIdx.y, im = blockIdx.z & 1, pair = blockIdx.z >> 1;
+    const int cn = a.cn > 0 ? a.cn : 1;
+    const int ch = blockIdx.z % cn, view = blockIdx.z / cn;
+    const int x0 = blockIdx.x * 256, y = blockIdx.y, im = view & 1, pair = view >> 1;
     const int W = a.W, H = a.H, ft = a.ftzero, tid = threadIdx.x;
-    const uint8_t* img = a.img[im] + (size_t)pair * a.in_pair;
+    const uint8_t* img = a.img[im] + (size_t)pair * a.in_pair + ch;
     for (int i = tid; i < 3 * 260; i += 256) {
         const int r = i / 260, c = i - r * 260;
-        rows[r][c] = img[(size_t)min(max(y - 1 + r, 0), H - 1) * a.stride + min(max(x0 - 2 + c, 0), W - 1)];
+        rows[r][c] = img[(size_t)min(max(y - 1 + r, 0), H - 1) * a.stride + (size_t)min(max(x0 - 2 + c, 0), W - 1) * cn];
     }
     __syncthreads();
     for (int i = tid; i < 258; i += 256) {  // column xx = x0 - 1 + i sits at rows[.][i + 1]
@@ -226,7 +230,7 @@ __global__ void __launch_bounds__(256) k_sgbm_prefilter(PrefilterArgs a)
     uint2 w;
     w.x = b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
     w.y = b[4] | (b[5] << 8);
-    reinterpret_cast<uint2*>(a.planes)[((size_t)(pair * 2 + im) * H + y) * W + x] = w;
+    reinterpret_cast<uint2*>(a.planes)[((size_t)blockIdx.z * H + y) * W + x] = w;
 }
 
 // C_true[y][x1][d] for the rows OpenCV's incremental box filter actually

@@ -104,7 +104,7 @@ class StereoSGBM:
             return _compute_torch(left, right, prm)
         left = np.asarray(left)
         right = np.asarray(right)
-        _check_pair(left, right)
+        _check_pair(left, right, colour=True)
         out = _lib.engine(self.device).compute(left, right, prm)
         if disparity is not None:
             np.copyto(disparity, out)
@@ -145,15 +145,18 @@ class StereoSGBM:
         return _lib.engine(self.device).aggregate_cost_f32(v, prm, offset, scale)
 
 
-def _check_pair(left, right):
+def _check_pair(left, right, colour=False):
+    """OpenCV's asserts: same size and type, CV_8U; StereoSGBM takes 1 or 3
+    channels (try_try.py:56-57,81 passes cv2.imread BGR images), StereoBM gray."""
     if left.shape != right.shape or left.dtype != right.dtype:
         raise ValueError("left and right images must have the same size and type")
     if left.dtype != np.uint8:
         raise ValueError("images must be CV_8U (uint8)")
-    if left.ndim == 3:
-        raise SmError(_lib.SM_E_UNSUPPORTED, "multi-channel input is not implemented on the GPU path; "
-                      "convert with cvtColor(BGR2GRAY) as disparity_calculation.py:286 does")
-    if left.ndim != 2 or left.size == 0:
+    if left.ndim == 3 and colour and left.shape[2] == 1:
+        return
+    if left.ndim == 3 and not (colour and left.shape[2] == 3):
+        raise ValueError("images must be gray (H, W)" + (" or BGR (H, W, 3)" if colour else ""))
+    if left.ndim not in (2, 3) or left.size == 0:
         raise ValueError("images must be non-empty 2-D arrays")
 
 
