@@ -52,8 +52,16 @@ def weight_table(sigma: float) -> np.ndarray:
 
 
 def _reflect101(i, n):
-    i = np.where(i < 0, -i, i)
-    return np.where(i >= n, 2 * n - 2 - i, i) if n > 1 else np.zeros_like(i)
+    """cv::borderInterpolate(BORDER_REFLECT_101): reflect until inside (windows
+    wider than the image reflect more than once)."""
+    if n == 1:
+        return np.zeros_like(i)
+    i = np.asarray(i).copy()
+    while True:
+        bad = (i < 0) | (i >= n)
+        if not bad.any():
+            return i
+        i = np.where(i < 0, -i, np.where(i >= n, 2 * n - 2 - i, i))
 
 
 def _box_means(disp: np.ndarray, r: int, y0, y1, x0, x1):

@@ -70,6 +70,10 @@ struct BufSet {
 
 // debug flags (sm_set_debug_flags); 1 skip horizontal, 2 skip vertical and 4 drop stores are read in-kernel
 constexpr int DBG_VL16 = 8, DBG_STORE_W = 16, DBG_ROW = 32, DBG_OVERLAP = 64, DBG_H64 = 512, DBG_NO_C8 = 1024;
+// 256: the sweep engine's E/W volumes from the other E/W kernel (u8 costs: the
+// per-direction engine's row lines instead of the packed k_ew; u16: k_ew instead of the
+// row lines); 128 and 1 << 27: the fused sweeps on k_sweep2 (see sweep_variant)
+constexpr int DBG_OLD_EW = 256, DBG_SWEEP_V2 = 128, DBG_SWEEP2_NW = 1 << 27;
 // 4096: per-direction engine (one path volume per direction + k_wta) instead of the fused sweeps
 constexpr int DBG_LEGACY = 4096, DBG_SWEEP1 = 8192, DBG_SWEEP8 = 16384, DBG_HYBRID = 32768;
 constexpr int DBG_COST_TILE = 1 << 22;
@@ -641,13 +645,22 @@ int ensure_sweep_err(sm_ctx* ctx)
     return SM_OK;
 }
 
+// which fused-sweep kernel: k_sweep (0) by default; ablation flags select k_sweep2 (column-
+// per-lane layout, sm_sweep2.hpp; u8 costs at D = 128, k_sweep elsewhere): 128 -> 6 compute
+// waves of 8 columns, 1 << 27 -> 3 waves of 16 columns (slower at 8 pairs)
+int sweep_variant(const sm_ctx* ctx)
+{
+    if (ctx->dbg_flags & DBG_SWEEP_V2) return 6;
+    return (ctx->dbg_flags & DBG_SWEEP2_NW) ? 3 : 0;
+}
+
 // one sweep pass (MODE 0/1/2, sm_sweep.hpp) over the job's G pairs, in launches
 // whose workgroups are all co-resident (strips of a pair wait on each other)
 int sweep_pass(sm_ctx* ctx, const Norm& n, const Geo& g, const SweepJob& j, int mode)
 {
     const int ct = (int)elem_bytes(n);
     smk::SweepInfo si{};
-    if (smk::sweep_info(n.D, ct, mode, ctx->device, &si) != hipSuccess)
+    if (smk::sweep_info(n.D, ct, mode, sweep_variant(ctx), ctx->device, &si) != hipSuccess)
         return fail(ctx, SM_E_UNSUPPORTED, "sweep: numDisparities %d not built", n.D);
     int ncu = 0;
     HIP_TRY(ctx, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
@@ -702,8 +715,8 @@ int sweep_pass(sm_ctx* ctx, const Norm& n, const Geo& g, const SweepJob& j, int 
         a.inv_ku = n.uniq < 100 ? 1.0f / (float)(100 - n.uniq) : 0.f;
         a.nwg = nwg;
         a.epoch = ctx->hop_epoch;
-        a.dbg = (ctx->dbg_flags >> 24) & 15;  // timing ablations (results wrong): 1 no polls
-        HIP_TRY(ctx, smk::sweep_launch(n.D, ct, mode, a, np, ctx->stream));
+        a.dbg = (ctx->dbg_flags >> 24) & 7;  // timing ablations (results wrong): 1 no polls
+        HIP_TRY(ctx, smk::sweep_launch(n.D, ct, mode, sweep_variant(ctx), a, np, ctx->stream));
     }
     return SM_OK;
 }
@@ -715,6 +728,32 @@ struct StreamSwap {
     StreamSwap(sm_ctx* c_, hipStream_t s) : c(c_), old(c_->stream) { c->stream = s; }
     ~StreamSwap() { c->stream = old; }
 };
+
+// E and W path volumes of the sweep engine (slots 0, 1 of bs.L): the packed
+// horizontal-line kernel (sm_ew.hpp), or the per-direction engine's row lines
+// (ablation flag 256)
+int launch_ew(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs)
+{
+    const size_t et = elem_bytes(n);
+    // measured (8 KITTI pairs): u8 costs 114 vs 122 us per pair beside the down sweep;
+    // u16 costs (alone) 103 vs 92, the row lines stay
+    if ((et == 1) == ((ctx->dbg_flags & DBG_OLD_EW) != 0)) return dispatch(ctx, n, g, bs, DISPATCH_HORIZONTAL);
+    smk::EwArgs a{};
+    a.cost = (const uint8_t*)bs.cost.p;
+    a.cost_pair = g.vol * et;
+    a.out = (uint8_t*)bs.L.p;
+    a.out_pair = g.L_pair;
+    a.out_slot = g.slot_bytes;
+    a.H = g.H;
+    a.W1 = n.width1;
+    a.P1 = n.P1;
+    a.P2 = n.P2;
+    StageTimer t(ctx, ctx->stream, SM_STAGE_HORIZONTAL, g.G);
+    const hipError_t e = smk::ew_launch(n.D, (int)et, 0, a, g.G, ctx->stream);
+    if (e == hipErrorInvalidValue) return fail(ctx, SM_E_UNSUPPORTED, "E/W lines: numDisparities %d not built", n.D);
+    HIP_TRY(ctx, e);
+    return SM_OK;
+}
 
 // E/W volumes -> [down sweep partial] -> WTA sweep -> LR check into bs.raw.  With
 // wta_stream != ctx->stream (5 paths, two-stream overlap) the WTA sweep and the
@@ -757,12 +796,12 @@ int run_sweep(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs, hipStream_t 
             HIP_TRY(ctx, hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
             const hipStream_t main = ctx->stream;
             ctx->stream = ctx->side;
-            rc = dispatch(ctx, n, g, bs, DISPATCH_HORIZONTAL);
+            rc = launch_ew(ctx, n, g, bs);
             ctx->stream = main;
             if (rc != SM_OK) return rc;
             HIP_TRY(ctx, hipEventRecord(ctx->ev_join, ctx->side));
             HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
-        } else if ((rc = dispatch(ctx, n, g, bs, DISPATCH_HORIZONTAL)) != SM_OK) {
+        } else if ((rc = launch_ew(ctx, n, g, bs)) != SM_OK) {
             return rc;
         }
     }

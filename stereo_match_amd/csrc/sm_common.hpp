@@ -132,6 +132,27 @@ struct Line<8> {
     static __device__ __forceinline__ uint32_t min(uint32_t v);
 };
 
+// 4-lane lines (four per DPP row): row shifts plus a fix-up at the quad edge
+template <>
+struct Line<4> {
+    template <typename T>
+    static __device__ __forceinline__ T prev(T edge, T v)
+    {
+        T r;
+        if constexpr (sizeof(T) == 8) r = dpp64<DPP_ROW_SHR1>(edge, v);
+        else r = dpp<DPP_ROW_SHR1>(edge, v);
+        return (threadIdx.x & 3) == 0 ? edge : r;
+    }
+    template <typename T>
+    static __device__ __forceinline__ T next(T edge, T v)
+    {
+        T r;
+        if constexpr (sizeof(T) == 8) r = dpp64<DPP_ROW_SHL1>(edge, v);
+        else r = dpp<DPP_ROW_SHL1>(edge, v);
+        return (threadIdx.x & 3) == 3 ? edge : r;
+    }
+};
+
 __device__ __forceinline__ uint32_t row16_or(uint32_t v)
 {
     v |= perm_dpp<DPP_QP_XOR1>(v);

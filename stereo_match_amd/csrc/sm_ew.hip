@@ -1,0 +1,43 @@
+// sm_ew.hip — translation unit of the packed horizontal-line kernel (sm_ew.hpp).
+#include "sm_ew.hpp"
+
+namespace smk {
+
+namespace {
+
+constexpr int ew_pf(int words) { return words >= 16 ? 4 : words >= 8 ? 8 : 16; }  // ring: <= 64 VGPRs
+
+template <int VL, int NP, typename CT>
+hipError_t run_ew(EwArgs a, int npairs, hipStream_t stream)
+{
+    constexpr int WORDS = RawBytes<2 * NP * (int)sizeof(CT)>::WORDS;
+    constexpr int LPW = 64 / VL;
+    a.nrb = (a.H + 4 * LPW - 1) / (4 * LPW);
+    hipLaunchKernelGGL((k_ew<VL, NP, CT, CT, ew_pf(WORDS)>), dim3(2 * a.nrb, npairs), dim3(256), 0, stream, a);
+    return hipGetLastError();
+}
+
+template <typename CT>
+hipError_t ew_d(int D, int vl, const EwArgs& a, int npairs, hipStream_t stream)
+{
+    if (D == 128 && vl == 4) return run_ew<4, 16, CT>(a, npairs, stream);
+    if (D == 128 && vl == 16) return run_ew<16, 4, CT>(a, npairs, stream);
+    if (vl != 0 && vl != 8) return hipErrorInvalidValue;
+    switch (D) {  // 8-lane lines, D / 16 u16 pairs per lane
+#define EW8(d) \
+    case d: return run_ew<8, d / 16, CT>(a, npairs, stream);
+        EW8(16) EW8(32) EW8(48) EW8(64) EW8(80) EW8(96) EW8(112) EW8(128)
+        EW8(144) EW8(160) EW8(176) EW8(192) EW8(208) EW8(224) EW8(240) EW8(256)
+#undef EW8
+    default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace
+
+hipError_t ew_launch(int D, int ct_bytes, int vl, EwArgs a, int npairs, hipStream_t stream)
+{
+    return ct_bytes == 1 ? ew_d<uint8_t>(D, vl, a, npairs, stream) : ew_d<uint16_t>(D, vl, a, npairs, stream);
+}
+
+}  // namespace smk

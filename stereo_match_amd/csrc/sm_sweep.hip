@@ -2,6 +2,7 @@
 // instantiates k_sweep for every built (D, cost type, mode) and exposes a
 // plain host interface to sm_api.hip, so the two units compile in parallel.
 #include "sm_sweep.hpp"
+#include "sm_sweep2.hpp"
 #include "sm_sweep_host.hpp"
 
 namespace smk {
@@ -78,19 +79,72 @@ struct LaunchF {
     }
 };
 
+// column-per-lane sweeps (sm_sweep2.hpp, a measured ablation): built for u8 (census) costs
+// at D = 128; variant = compute waves per workgroup: 3 (16 columns per wave), 6 (8 columns)
+constexpr int sw2_pf(int mode) { return mode == 2 ? 2 : 4; }
+
+template <int NW, int CPW, int NP, int MODE>
+hipError_t sweep2_run(bool info, int device, SweepInfo* out, const SweepArgs* a, int npairs, hipStream_t stream)
+{
+    using SG = Sweep2Geo<NW, CPW, NP>;
+    auto kern = k_sweep2<NW, CPW, NP, uint8_t, MODE, sw2_pf(MODE)>;
+    if (info) {
+        static int per_cu = -1;
+        if (per_cu < 0) {
+            int nb = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, SG::THREADS, 0) != hipSuccess) nb = 1;
+            per_cu = nb;
+        }
+        out->cw = SG::CW;
+        out->hb = SG::HB;
+        out->ngr = SG::NGR;
+        out->threads = SG::THREADS;
+        out->blocks_per_cu = per_cu;
+        return hipSuccess;
+    }
+    hipLaunchKernelGGL(kern, dim3(a->nwg, npairs), dim3(SG::THREADS), 0, stream, *a);
+    return hipGetLastError();
+}
+
+template <int NW, int CPW>
+hipError_t sweep2_d(int D, bool info, int device, SweepInfo* out, const SweepArgs* a, int npairs, hipStream_t stream)
+{
+    constexpr int PARTS = 64 / CPW;
+    if (D != 128) return hipErrorInvalidValue;
+    return sweep2_run<NW, CPW, 128 / (2 * PARTS), SWEEP_MODE>(info, device, out, a, npairs, stream);
+}
+
+hipError_t sweep2(int D, int ct_bytes, int variant, bool info, int device, SweepInfo* out, const SweepArgs* a,
+                  int npairs, hipStream_t stream)
+{
+    if (ct_bytes != 1) return hipErrorInvalidValue;
+    switch (variant) {  // 3: 16 columns per wave; 6: 8 columns per wave
+    case 3: return sweep2_d<3, 16>(D, info, device, out, a, npairs, stream);
+    case 6: return sweep2_d<6, 8>(D, info, device, out, a, npairs, stream);
+    default: return hipErrorInvalidValue;
+    }
+}
+
 }  // namespace
 
 #define SW_CAT2(a, b) a##b
 #define SW_CAT(a, b) SW_CAT2(a, b)
 
-hipError_t SW_CAT(sweep_info_m, SWEEP_MODE)(int D, int ct_bytes, int device, SweepInfo* out)
+hipError_t SW_CAT(sweep_info_m, SWEEP_MODE)(int D, int ct_bytes, int variant, int device, SweepInfo* out)
 {
+    if (variant && sweep2(D, ct_bytes, variant, true, device, out, nullptr, 0, nullptr) == hipSuccess)
+        return hipSuccess;
     InfoF f{device, out};
     return with_sweep(D, ct_bytes, f);
 }
 
-hipError_t SW_CAT(sweep_launch_m, SWEEP_MODE)(int D, int ct_bytes, const SweepArgs& a, int npairs, hipStream_t stream)
+hipError_t SW_CAT(sweep_launch_m, SWEEP_MODE)(int D, int ct_bytes, int variant, const SweepArgs& a, int npairs,
+                                              hipStream_t stream)
 {
+    if (variant) {
+        const hipError_t e = sweep2(D, ct_bytes, variant, false, 0, nullptr, &a, npairs, stream);
+        if (e != hipErrorInvalidValue) return e;
+    }
     LaunchF f{&a, dim3(a.nwg, npairs), stream};
     return with_sweep(D, ct_bytes, f);
 }

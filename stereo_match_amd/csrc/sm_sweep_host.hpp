@@ -39,29 +39,46 @@ struct SweepInfo {
 template <typename CT, int MODE, class F>
 hipError_t with_d(int D, F& f);
 
-// per mode (one translation unit each); hipErrorInvalidValue when (D, ct_bytes) is not built
-hipError_t sweep_info_m0(int D, int ct_bytes, int device, SweepInfo* out);
-hipError_t sweep_info_m1(int D, int ct_bytes, int device, SweepInfo* out);
-hipError_t sweep_info_m2(int D, int ct_bytes, int device, SweepInfo* out);
+// per mode (one translation unit each); hipErrorInvalidValue when (D, ct_bytes) is not built.
+// variant 0: k_sweep (sm_sweep.hpp); 2 / 4: k_sweep2 (sm_sweep2.hpp) with that many compute
+// waves per workgroup where built (u8 costs, D = 64 / 128), k_sweep elsewhere.  sweep_info
+// and sweep_launch of one pass must get the same variant.
+hipError_t sweep_info_m0(int D, int ct_bytes, int variant, int device, SweepInfo* out);
+hipError_t sweep_info_m1(int D, int ct_bytes, int variant, int device, SweepInfo* out);
+hipError_t sweep_info_m2(int D, int ct_bytes, int variant, int device, SweepInfo* out);
 // grid (a.nwg, npairs), SweepInfo::threads threads
-hipError_t sweep_launch_m0(int D, int ct_bytes, const SweepArgs& a, int npairs, hipStream_t stream);
-hipError_t sweep_launch_m1(int D, int ct_bytes, const SweepArgs& a, int npairs, hipStream_t stream);
-hipError_t sweep_launch_m2(int D, int ct_bytes, const SweepArgs& a, int npairs, hipStream_t stream);
+hipError_t sweep_launch_m0(int D, int ct_bytes, int variant, const SweepArgs& a, int npairs, hipStream_t stream);
+hipError_t sweep_launch_m1(int D, int ct_bytes, int variant, const SweepArgs& a, int npairs, hipStream_t stream);
+hipError_t sweep_launch_m2(int D, int ct_bytes, int variant, const SweepArgs& a, int npairs, hipStream_t stream);
 
-inline hipError_t sweep_info(int D, int ct_bytes, int mode, int device, SweepInfo* out)
+inline hipError_t sweep_info(int D, int ct_bytes, int mode, int variant, int device, SweepInfo* out)
 {
-    return mode == 0 ? sweep_info_m0(D, ct_bytes, device, out)
-         : mode == 1 ? sweep_info_m1(D, ct_bytes, device, out)
-                     : sweep_info_m2(D, ct_bytes, device, out);
+    return mode == 0 ? sweep_info_m0(D, ct_bytes, variant, device, out)
+         : mode == 1 ? sweep_info_m1(D, ct_bytes, variant, device, out)
+                     : sweep_info_m2(D, ct_bytes, variant, device, out);
 }
-inline hipError_t sweep_launch(int D, int ct_bytes, int mode, const SweepArgs& a, int npairs, hipStream_t stream)
+inline hipError_t sweep_launch(int D, int ct_bytes, int mode, int variant, const SweepArgs& a, int npairs,
+                               hipStream_t stream)
 {
-    return mode == 0 ? sweep_launch_m0(D, ct_bytes, a, npairs, stream)
-         : mode == 1 ? sweep_launch_m1(D, ct_bytes, a, npairs, stream)
-                     : sweep_launch_m2(D, ct_bytes, a, npairs, stream);
+    return mode == 0 ? sweep_launch_m0(D, ct_bytes, variant, a, npairs, stream)
+         : mode == 1 ? sweep_launch_m1(D, ct_bytes, variant, a, npairs, stream)
+                     : sweep_launch_m2(D, ct_bytes, variant, a, npairs, stream);
 }
 // sub-pixel + disp2 + disp12MaxDiff check from the WTA sweep's records, one row per workgroup
 hipError_t lr_rows_launch(const uint32_t* rec, const uint32_t* nb, int16_t* out, int G, int H, int W, int D, int minD,
                           int minX1, int maxX1, int disp12, hipStream_t stream);
+
+// horizontal (E, W) path volumes, packed recurrence (sm_ew.hpp / sm_ew.hip)
+struct EwArgs {
+    const uint8_t* cost;  // [pair][H][W1][D] of CT
+    size_t cost_pair;     // bytes
+    uint8_t* out;         // E volume [pair][H][W1][D] of LT; W at out + out_slot
+    size_t out_pair, out_slot;
+    int H, W1, P1, P2;
+    int nrb;  // workgroups per direction (filled by ew_launch)
+};
+// lanes per line: vl = 4, 8 or 16 (0 = the default for D); hipErrorInvalidValue when
+// (D, ct_bytes, vl) is not built.  LT = CT (u8 census costs -> u8 volumes, u16 -> u16).
+hipError_t ew_launch(int D, int ct_bytes, int vl, EwArgs a, int npairs, hipStream_t stream);
 
 }  // namespace smk

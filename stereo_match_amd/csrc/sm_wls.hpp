@@ -52,11 +52,12 @@ struct WlsConfArgs {
     float tab[256];  // -exp(-k / sigma), k = |delta guide|
 };
 
+// cv::borderInterpolate(BORDER_REFLECT_101): reflect until inside (a window
+// wider than the image reflects more than once)
 __device__ inline int reflect101(int i, int n)
 {
     if (n == 1) return 0;
-    if (i < 0) i = -i;
-    if (i >= n) i = 2 * n - 2 - i;
+    while ((unsigned)i >= (unsigned)n) i = i < 0 ? -i : 2 * n - 2 - i;
     return i;
 }
 

@@ -137,7 +137,11 @@ def test_sgbm_cost_block_sizes(eng, bs, D, minD):
                                                   ("kitti", 1, 8, 32768), ("kitti", 0, 8, 32768),
                                                   ("mccnn", 1, 8, 32768), ("kitti", 0, 5, 32768),
                                                   ("kitti", 0, 5, 1 << 22), ("kitti", 0, 8, 4096),
-                                                  ("kitti", 0, 5, 16384), ("kitti", 1, 5, 16384)])
+                                                  ("kitti", 0, 5, 16384), ("kitti", 1, 5, 16384),
+                                                  # sweep-engine E/W kernel swapped (256), k_sweep2 (128, 1 << 27)
+                                                  ("kitti", 1, 8, 16384 | 256), ("kitti", 0, 5, 256),
+                                                  ("kitti", 1, 8, 16384 | 128), ("kitti", 1, 8, 16384 | (1 << 27)),
+                                                  ("kitti", 1, 5, 128)])
 def test_full_size_bit_exact(eng, name, cost, mode, flags):
     H, W, D = synthetic.CONFIGS[name]
     left, right, gt = synthetic.random_dot_pair(H, W, D, seed=42)

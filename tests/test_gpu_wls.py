@@ -146,6 +146,19 @@ def test_wls_bad_args(eng):
         eng.wls_filter(d, g, d, wls_params(dict(left_offset=-1), 10, 40))
 
 
+@pytest.mark.parametrize("H,W,r", [(2, 20, 6), (3, 24, 64), (1, 40, 5), (5, 2, 9)])
+def test_wls_radius_wider_than_map(eng, H, W, r):
+    # the confidence window reflects more than once (cv::borderInterpolate REFLECT_101)
+    rng = np.random.default_rng(H * 1000 + W + r)
+    displ = rng.integers(-16, 40 * 16, (H, W)).astype(np.int16)
+    dispr = (-rng.integers(0, 40 * 16, (H, W))).astype(np.int16)
+    guide = rng.integers(0, 256, (H, W)).astype(np.uint8)
+    p = dict(lmbda=8000.0, sigma=1.5, lrc_thresh=24, radius=r, use_confidence=True, left_offset=0,
+             right_offset=0, top_offset=0, bottom_offset=0, num_iter=2, min_disp=0)
+    out = eng.wls_filter(displ, guide, dispr, wls_params(p, H, W))
+    assert np.array_equal(out, wls_np.wls_filter(displ, guide, dispr, p))
+
+
 from hypothesis import HealthCheck, given, settings, strategies as st  # noqa: E402
 
 

@@ -88,3 +88,22 @@ def test_empty_roi_is_fill_only():
 def test_golden_wls_fixtures_reproduce(golden_wls_cases):
     for name, displ, dispr, guide, p, expected in golden_wls_cases:
         assert np.array_equal(wls_np.wls_filter(displ, guide, dispr, p), expected), name
+
+
+def _border_interpolate_101(p, n):
+    """cv::borderInterpolate(p, n, BORDER_REFLECT_101), scalar form."""
+    if n == 1:
+        return 0
+    while not 0 <= p < n:
+        p = -p if p < 0 else 2 * n - 2 - p
+    return p
+
+
+def test_reflect101_windows_wider_than_image():
+    # radius up to 64 over maps as short as 2 rows: reflections repeat (a single
+    # reflection would index outside the map)
+    for n in (1, 2, 3, 5, 17):
+        idx = np.arange(-70, n + 70)
+        got = wls_np._reflect101(idx, n)
+        assert got.min() >= 0 and got.max() < n
+        assert [int(v) for v in got] == [_border_interpolate_101(int(p), n) for p in idx]
