@@ -46,8 +46,8 @@ METRIC = "stereo pairs/sec + Mpix·disp/sec, KITTI 1242×375 D=128 SGM, 1/2/4/8 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=400)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default=None, choices=["kitti", "middlebury", "tsukuba", "mccnn"],
                     help="default: kitti (mccnn for --mode volume8)")
     ap.add_argument("--mode", default="census8", choices=["census8", "sgbm5", "sgbm8", "volume8", "disparity5", "bm"],
