@@ -656,20 +656,45 @@ int sweep_variant(const sm_ctx* ctx)
 
 // one sweep pass (MODE 0/1/2, sm_sweep.hpp) over the job's G pairs, in launches
 // whose workgroups are all co-resident (strips of a pair wait on each other)
-int sweep_pass(sm_ctx* ctx, const Norm& n, const Geo& g, const SweepJob& j, int mode)
+// strips per pair (nwg) and co-resident workgroups the context's stream can hold (cap) for one
+// sweep mode; false when (D, cost type) is not built
+bool sweep_capacity(sm_ctx* ctx, const Norm& n, int mode, smk::SweepInfo& si, int& nwg, int& cap)
 {
-    const int ct = (int)elem_bytes(n);
-    smk::SweepInfo si{};
-    if (smk::sweep_info(n.D, ct, mode, sweep_variant(ctx), ctx->device, &si) != hipSuccess)
-        return fail(ctx, SM_E_UNSUPPORTED, "sweep: numDisparities %d not built", n.D);
+    if (smk::sweep_info(n.D, (int)elem_bytes(n), mode, sweep_variant(ctx), ctx->device, &si) != hipSuccess)
+        return false;
     int ncu = 0;
-    HIP_TRY(ctx, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess) return false;
     ncu = stream_cus(ctx->stream, std::max(ncu, 1));  // a CU-masked stream only reaches its CUs
     // the API's answer can be one block per CU high at >= 82 SGPRs (MI355X guide);
     // for 512-thread blocks SGPRs allow >= 3 per CU, so a margin is kept only above 2
     const int per_cu = si.blocks_per_cu >= 3 ? si.blocks_per_cu - 1 : std::max(si.blocks_per_cu, 1);
-    const int cap = per_cu * ncu;
-    const int nwg = (n.width1 + si.cw - 1) / si.cw;
+    cap = per_cu * ncu;
+    nwg = (n.width1 + si.cw - 1) / si.cw;
+    return true;
+}
+
+// every sweep pass of the configuration can make all strips of a pair co-resident (wide
+// images on few CUs cannot: those run on the per-direction engine)
+bool sweeps_fit(sm_ctx* ctx, const Norm& n, bool hybrid)
+{
+    // passes: hybrid = the down sweep; 8 paths = down + up/WTA; 5 paths = down/WTA
+    const int m8[2] = {0, 2}, m5[1] = {1}, mh[1] = {0};
+    const int* modes = hybrid ? mh : n.ndirs == 8 ? m8 : m5;
+    const int count = !hybrid && n.ndirs == 8 ? 2 : 1;
+    for (int k = 0; k < count; k++) {
+        smk::SweepInfo si{};
+        int nwg = 0, cap = 0;
+        if (!sweep_capacity(ctx, n, modes[k], si, nwg, cap) || nwg > cap) return false;
+    }
+    return true;
+}
+
+int sweep_pass(sm_ctx* ctx, const Norm& n, const Geo& g, const SweepJob& j, int mode)
+{
+    smk::SweepInfo si{};
+    int nwg = 0, cap = 0;
+    if (!sweep_capacity(ctx, n, mode, si, nwg, cap))
+        return fail(ctx, SM_E_UNSUPPORTED, "sweep: numDisparities %d not built", n.D);
     const int nblk = (g.H + si.hb - 1) / si.hb;
     if (nwg > cap) return fail(ctx, SM_E_UNSUPPORTED, "sweep: %d strips exceed %d resident workgroups", nwg, cap);
     // ablation / test flag 8192: one pair per sweep launch (exercises the chunked launches)
@@ -716,7 +741,7 @@ int sweep_pass(sm_ctx* ctx, const Norm& n, const Geo& g, const SweepJob& j, int 
         a.nwg = nwg;
         a.epoch = ctx->hop_epoch;
         a.dbg = (ctx->dbg_flags >> 24) & 7;  // timing ablations (results wrong): 1 no polls
-        HIP_TRY(ctx, smk::sweep_launch(n.D, ct, mode, sweep_variant(ctx), a, np, ctx->stream));
+        HIP_TRY(ctx, smk::sweep_launch(n.D, (int)elem_bytes(n), mode, sweep_variant(ctx), a, np, ctx->stream));
     }
     return SM_OK;
 }
@@ -1299,8 +1324,8 @@ int run_pairs(sm_ctx* ctx, const Src& src, int npairs, int H, int W, int stride,
     g.stride = stride;
     g.vol = (size_t)H * std::max(n.width1, 0) * n.D;
     g.slot_bytes = (g.vol * elem_bytes(n) + 255) & ~size_t(255);
-    g.hybrid = !n.wide && use_hybrid(ctx, n, H);
-    g.sweep = !n.wide && !g.hybrid && use_sweep(ctx, n, H);
+    g.hybrid = !n.wide && use_hybrid(ctx, n, H) && sweeps_fit(ctx, n, true);
+    g.sweep = !n.wide && !g.hybrid && use_sweep(ctx, n, H) && sweeps_fit(ctx, n, false);
     // sweep engine: E and W volumes in slots 0/1 plus room for every direction's volume
     // (written only by the guarded fallback); hybrid: E, W (+ NE, N, NW at 8 paths)
     g.L_pair = g.slot_bytes * (g.hybrid ? hybrid_slots(n) : n.ndirs);

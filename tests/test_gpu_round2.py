@@ -99,6 +99,23 @@ def test_sweep_on_half_the_cus(mode, cost, extra):
         e.close()
 
 
+@pytest.mark.parametrize("mode,cost", [(5, 0), (8, 1)], ids=["sgbm5", "census8"])
+def test_sweeps_too_wide_for_the_cus_run_per_direction(mode, cost):
+    """On 4 CUs a KITTI pair's strips cannot all be co-resident: the library
+    runs the per-direction engine instead (same maps, no device fallback)."""
+    e = _lib.Engine(0)
+    try:
+        e.set_cu_mask([0, 1, 2, 3])
+        H, W, D = synthetic.CONFIGS["kitti"]
+        left, right, _ = synthetic.random_dot_pair(H, W, D, seed=6)
+        p = dict(synthetic.headline_params(D) if cost else synthetic.parity_params(D), mode=mode)
+        out = _run(e, left, right, p, SWEEP8)
+        assert np.array_equal(out, ref_c.compute(left, right, p))
+        assert e.counters()["sweep_fallbacks"] == 0
+    finally:
+        e.close()
+
+
 def test_full_size_sweeps_do_not_fall_back(eng):
     H, W, D = synthetic.CONFIGS["kitti"]
     left, right, _ = synthetic.random_dot_pair(H, W, D, seed=6)

@@ -1,7 +1,9 @@
 #!/bin/bash
-# PMC passes over the census8 fused sweeps (8 pairs): k_sweep2 (default) and k_sweep (flag 128).
+# PMC passes over the census8 fused sweeps (8 pairs): k_sweep (16384) and k_sweep2 (16384 | 128).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export KF="sweep"
-bash tools/pmc.sh sw2 16384 "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_SALU SQ_INSTS_LDS" "SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_SALU SQ_ACTIVE_INST_MISC GRBM_GUI_ACTIVE" || exit $?
-bash tools/pmc.sh sw1 $((16384|128)) "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_SALU SQ_INSTS_LDS" "SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_SALU SQ_ACTIVE_INST_MISC GRBM_GUI_ACTIVE"
+C1="SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_SALU SQ_INSTS_LDS"
+C2="SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_SALU SQ_ACTIVE_INST_MISC GRBM_GUI_ACTIVE"
+bash tools/pmc.sh sweep 16384 "$C1" "$C2" || exit $?
+bash tools/pmc.sh sweep2 $((16384|128)) "$C1" "$C2"

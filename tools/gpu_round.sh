@@ -3,6 +3,7 @@
 #   bash tools/gpu_round.sh <tag> A : smoke -> GPU tests -> rocprofv3 kernel stats + PMC
 #       traffic (separate FETCH/WRITE passes) for the headline (census8) and the parity
 #       mode (sgbm5) -> headline bench + sgbm5 bench with their traffic files
+#   bash tools/gpu_round.sh <tag> T : part A without smoke, tests and kernel stats
 #   bash tools/gpu_round.sh <tag> B : the other bench modes / engines / configs
 # Each GPU step is time-limited; a failure (other than pytest's rc 1) stops the script.
 set -u
@@ -12,12 +13,14 @@ OUT=gpurun_out/$TAG; mkdir -p "$OUT"
 export TMPDIR=/tmp
 step() { local name=$1 t=$2; shift 2; echo "== $name"; timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1; local rc=$?
          echo "== $name rc=$rc"; tail -n 2 "$OUT/$name.log" | cut -c1-400; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi; }
-if [ "$PART" = A ]; then
+if [ "$PART" = A ] || [ "$PART" = T ]; then
+  if [ "$PART" = A ]; then
   step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()"
   step pytest_gpu 600 python -u -m pytest tests -m gpu -q -x --timeout 240 --timeout-method thread -p no:cacheprovider
+  fi
   for m in census8 sgbm5; do
-    step prof_$m 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$m" -o run --output-format csv -- python3 bench.py --mode $m --steps 10 --warmup 2 --cpu-baseline-pairs 0 --host-surface-calls 0
-    find "$OUT/prof_$m" -name "*kernel_stats.csv" -exec cp {} "$OUT/${m}_kernel_stats.csv" \;
+    [ "$PART" = T ] || step prof_$m 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$m" -o run --output-format csv -- python3 bench.py --mode $m --steps 10 --warmup 2 --cpu-baseline-pairs 0 --host-surface-calls 0
+    [ "$PART" = T ] || find "$OUT/prof_$m" -name "*kernel_stats.csv" -exec cp {} "$OUT/${m}_kernel_stats.csv" \;
     step traffic_$m 300 bash tools/traffic.sh kitti $m
     cp gpurun_out/traffic/summary.json "$OUT/${m}_traffic.json"
     rm -rf gpurun_out/traffic "$OUT/prof_$m"
