@@ -59,14 +59,16 @@ __global__ void __launch_bounds__(256) k_ew(EwArgs a)
     const uint64_t cells = (uint64_t)H * W1 * D;
     const rsrc_t rc = make_rsrc(a.cost + pair * a.cost_pair, cells * sizeof(CT));
     const rsrc_t ro = make_rsrc(a.out + pair * a.out_pair + (size_t)dir * a.out_slot, cells * sizeof(LT));
-    const int estep = dir ? -D : D;  // element step along the row
-    int e = (y * W1 + (dir ? W1 - 1 : 0)) * D + g * DPL;
+    // element index of this lane's slice, stepped along the row modulo 2^32 (a per-pair
+    // volume stays below 2^32 bytes: the host's kMaxRecords guard)
+    const uint32_t estep = dir ? (uint32_t)(-D) : (uint32_t)D;
+    uint32_t e = ((uint32_t)y * (uint32_t)W1 + (uint32_t)(dir ? W1 - 1 : 0)) * (uint32_t)D + (uint32_t)(g * DPL);
     const uint32_t P1p = (uint32_t)a.P1 * 0x10001u, P2 = (uint32_t)a.P2;
 
     RawBytes<CB> ring[PF];
 #pragma unroll
     for (int k = 0; k < PF; k++) {
-        ring[k].load(rc, k < W1 ? (uint32_t)(e + k * estep) * (uint32_t)sizeof(CT) : kOOB);
+        ring[k].load(rc, k < W1 ? (e + (uint32_t)k * estep) * (uint32_t)sizeof(CT) : kOOB);
         asm volatile("" ::: "memory");  // issue order = slot order (sm_paths.hpp horizontal ring)
     }
     uint32_t Lp[NP];
@@ -86,10 +88,10 @@ __global__ void __launch_bounds__(256) k_ew(EwArgs a)
             unpack_ct_pk<CT, DPL>(ring[k], C);
 #pragma unroll
             for (int i = 0; i < NP; i++) asm volatile("" : "+v"(C[i])::"memory");
-            ring[k].load(rc, s + PF < W1 ? (uint32_t)(e + PF * estep) * (uint32_t)sizeof(CT) : kOOB);
+            ring[k].load(rc, s + PF < W1 ? (e + (uint32_t)PF * estep) * (uint32_t)sizeof(CT) : kOOB);
             uint32_t Ln[NP];
             const uint32_t mn = sweep_step_pk<VL, NP>(Lp, minLp, C, P1p, P2, Ln);
-            store_pk<LT, NP>(ro, (line_ok && s < W1) ? (uint32_t)e * (uint32_t)sizeof(LT) : kOOB, Ln);
+            store_pk<LT, NP>(ro, (line_ok && s < W1) ? e * (uint32_t)sizeof(LT) : kOOB, Ln);
             e += estep;
 #pragma unroll
             for (int i = 0; i < NP; i++) Lp[i] = Ln[i];

@@ -259,7 +259,7 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL>::THREADS)) k_sweep(SweepArg
         bool dead = (a.dbg & 1) != 0;
         for (int b = 0; b < nblk; b++) {
 #pragma unroll 1
-            for (int j = 0; j < HB; j++) lds_barrier();
+            for (int j = 0; j < HB; j++) if (!(a.dbg & 4)) lds_barrier();  // 4: timing only, no row barriers
             if (b + 1 < nblk) {
                 if ((has_left || has_right) && !(a.dbg & 2)) {  // wave-uniform
                     uint32_t v[GPL];
@@ -488,7 +488,7 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL>::THREADS)) k_sweep(SweepArg
                     __builtin_amdgcn_raw_buffer_store_b32(recw, rrec, wpx ? px * 4 : kOOB, 0, 0);
                     __builtin_amdgcn_raw_buffer_store_b32(nbw, rnb, wpx ? px * 4 : kOOB, 0, 0);
                 }
-                lds_barrier();
+                if (!(a.dbg & 4)) lds_barrier();
             }
             if (b + 1 < nblk) lds_barrier();
         }
@@ -625,7 +625,7 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL>::THREADS)) k_sweep(SweepArg
                 __builtin_amdgcn_raw_buffer_store_b32(recw, rrec, wpx ? px * 4 : kOOB, 0, 0);
                 __builtin_amdgcn_raw_buffer_store_b32(nbw, rnb, wpx ? px * 4 : kOOB, 0, 0);
             }
-            lds_barrier();
+            if (!(a.dbg & 4)) lds_barrier();
         }
         if (b + 1 < nblk) lds_barrier();  // the poller has written the halo snapshot
     }

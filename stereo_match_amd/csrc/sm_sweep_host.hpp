@@ -24,7 +24,7 @@ struct SweepArgs {
     float inv_ku;  // 1 / (100 - uniq) (uniqueness threshold estimate; exact fix-up on the device)
     int nwg;
     uint32_t epoch;  // 1..65535, distinct from the previous launches on the same hop buffer
-    int dbg;         // timing ablations only: 1 no waiting in the halo polls, 2 no polls
+    int dbg;         // timing ablations only: 1 no waiting in the halo polls, 2 no polls, 4 no row barriers
 };
 
 
