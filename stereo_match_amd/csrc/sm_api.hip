@@ -74,6 +74,9 @@ constexpr int DBG_VL16 = 8, DBG_STORE_W = 16, DBG_ROW = 32, DBG_OVERLAP = 64, DB
 // per-direction engine's row lines instead of the packed k_ew; u16: k_ew instead of the
 // row lines); 128 and 1 << 27: the fused sweeps on k_sweep2 (see sweep_variant)
 constexpr int DBG_OLD_EW = 256, DBG_SWEEP_V2 = 128, DBG_SWEEP2_NW = 1 << 27;
+// WLS smoother timing ablations (results wrong): 1 << 28 skips the FGS sweeps, 1 << 29 its
+// global loads/stores
+constexpr int DBG_FGS_NO_SWEEP = 1 << 28, DBG_FGS_NO_MEM = 1 << 29;
 // 4096: per-direction engine (one path volume per direction + k_wta) instead of the fused sweeps
 constexpr int DBG_LEGACY = 4096, DBG_SWEEP1 = 8192, DBG_SWEEP8 = 16384, DBG_HYBRID = 32768;
 constexpr int DBG_COST_TILE = 1 << 22;
@@ -924,8 +927,7 @@ int launch_cost2_s(sm_ctx* ctx, const Norm& n, const Geo& g, const smk::SgbmCost
     const int strips = (n.width1 + TX - 1) / TX;
     // enough workgroups to fill the chip; bands at least 8 rows (warm-up 2S rows each)
     const int want = std::max(1, 2048 / std::max(1, strips * g.G));
-    const int tune = (ctx->dbg_flags >> 28) & 7;  // tuning: band height 8 * (bits 28-30)
-    c2.band = tune ? 8 * tune : std::max({(sc.Yc + want - 1) / want, 8, 4 * S});
+    c2.band = std::max({(sc.Yc + want - 1) / want, 8, 4 * S});
     const int bands = (sc.Yc + c2.band - 1) / c2.band;
     if (one)
         hipLaunchKernelGGL((smk::k_sgbm_cost2<S, CPT, 1>), dim3(strips, bands, g.G), dim3(bd), lds, ctx->stream, c2);
@@ -1452,7 +1454,7 @@ int run_wls(sm_ctx* ctx, const int16_t* dl, const int16_t* dr, size_t disp_pair,
             fa.w = n.w;
             fa.h = n.h;
             fa.wp = wp;
-            fa.dbg = ctx->dbg_flags;
+            fa.dbg = ((ctx->dbg_flags & DBG_FGS_NO_SWEEP) ? 1 : 0) | ((ctx->dbg_flags & DBG_FGS_NO_MEM) ? 2 : 0);
             float lam = n.lam;
             for (int it = 0; it < n.num_iter; it++) {
                 fa.lam = lam;

@@ -157,7 +157,7 @@ struct FgsArgs {
     size_t roi_pair;
     int w, h, wp;
     float lam;
-    int dbg;  // timing ablations: 128 skip the sweeps, 256 skip global loads/stores
+    int dbg;  // timing ablations (sm_api.hip DBG_FGS_*): 1 skip the sweeps, 2 skip global loads/stores
 };
 
 // Thomas solve of (I + lam*L_w) u = f along lines, 64 lines per workgroup
@@ -263,7 +263,7 @@ __global__ void __launch_bounds__(64) k_fgs(FgsArgs a)
     // columns advance 64 rows
     const uint32_t voff0 = tile_voff<ROWS>(l0, 0, wp, lane);
     const uint32_t cstep = ROWS ? FT * 4 : (uint32_t)FT * wp * 4;
-    const bool mem = !(a.dbg & 256), sweep = !(a.dbg & 128);
+    const bool mem = !(a.dbg & 2), sweep = !(a.dbg & 1);
     const float lam = a.lam;
     const int nchunks = (n + FT - 1) / FT;
     float4 rc[16], r0[16], r1[16];

@@ -205,3 +205,32 @@ def test_rccl_gather_world1():
         assert torch.equal(out.cpu(), maps)
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("D", [64, 128])
+def test_valid_result_flags_leave_compute_disparity_unchanged(eng, D):
+    """Every debug flag documented as 'valid results' (include/stereo_match_amd.h)
+    must leave the whole compute_disparity (both matchers + WLS) bit-identical,
+    e.g. no flag may double as another kernel's timing ablation."""
+    import stereo_match_amd as sm
+    from stereo_match_amd import wls
+    from stereo_match_amd.stereo_vision import matcher_from_settings
+
+    s = dict(sm.DEFAULT_SETTINGS, window_size=5, num_disparities=D)
+    H, W = 120, 420
+    gl, gr, _ = synthetic.random_dot_pair(H, W, D, seed=D + 3)
+    lm = matcher_from_settings(s)
+    prm = lm.params()
+    wf = wls.createDisparityWLSFilter(lm)
+    wf.setLambda(s["lmbda"])
+    wf.setSigmaColor(s["sigma"])
+    wp = wf.params(H, W)
+    ref = eng.compute_disparity(gl, gr, prm, wp)
+    for f in (8, 64, 128, 256, 1 << 12, 1 << 13, 1 << 14, (1 << 14) | 128, (1 << 14) | 256, 1 << 15,
+              1 << 20, 1 << 22, 1 << 23, 1 << 27, 2 << 16):
+        eng.set_debug_flags(f)
+        try:
+            got = eng.compute_disparity(gl, gr, prm, wp)
+        finally:
+            eng.set_debug_flags(0)
+        assert np.array_equal(got[0], ref[0]) and np.array_equal(got[1], ref[1]), f

@@ -1,5 +1,5 @@
 """Timing ablations of the WLS kernels (results are wrong under flags != 0):
-128 skips the FGS sweeps, 256 skips the FGS global loads/stores."""
+1 << 28 skips the FGS sweeps, 1 << 29 skips the FGS global loads/stores."""
 import json
 import os
 import sys
@@ -27,7 +27,7 @@ def main():
     eng.compute_disparity_batch_device(dL.data_ptr(), dR.data_ptr(), P, H * W, H, W, W, prm, wp,
                                        *(o.data_ptr() for o in outs))
     torch.cuda.synchronize()
-    for flags in [0, 128, 256, 384, 0]:
+    for flags in [0, 1 << 28, 1 << 29, 3 << 28, 0]:
         eng.set_debug_flags(flags)
         eng.set_timing(True)
         eng.reset_timing()
