@@ -315,7 +315,9 @@ long long sm_debug_fetch(sm_ctx* ctx, int what, void* host, size_t bytes);
  * XCD-aware pair mapping, bit 21 interleaved vertical directions;
  * bits 24-26: fused-sweep timing ablations (results become wrong: 1 no poll
  * waits, 2 no polls, 4 no per-row barriers); bits 28-29: WLS smoother timing
- * ablations (results become wrong: 28 no sweeps, 29 no global loads/stores).
+ * ablations (results become wrong: 28 no sweeps, 29 no global loads/stores);
+ * bit 30 (valid results): no Infinity-Cache-sized launch groups for the
+ * per-direction engine with u8 costs.
  * 0 = normal operation. */
 int sm_set_debug_flags(sm_ctx* ctx, int flags);
 

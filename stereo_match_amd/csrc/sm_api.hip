@@ -77,6 +77,8 @@ constexpr int DBG_OLD_EW = 256, DBG_SWEEP_V2 = 128, DBG_SWEEP2_NW = 1 << 27;
 // WLS smoother timing ablations (results wrong): 1 << 28 skips the FGS sweeps, 1 << 29 its
 // global loads/stores
 constexpr int DBG_FGS_NO_SWEEP = 1 << 28, DBG_FGS_NO_MEM = 1 << 29;
+// 1 << 30 (valid results): no Infinity-Cache-sized launch groups (group_size)
+constexpr int DBG_NO_MALL_GROUPS = 1 << 30;
 // 4096: per-direction engine (one path volume per direction + k_wta) instead of the fused sweeps
 constexpr int DBG_LEGACY = 4096, DBG_SWEEP1 = 8192, DBG_SWEEP8 = 16384, DBG_HYBRID = 32768;
 constexpr int DBG_COST_TILE = 1 << 22;
@@ -350,6 +352,10 @@ const int kVdy[6] = {1, 1, 1, -1, -1, -1};
 constexpr size_t kSetBudget = size_t(12) << 30;  // bytes of path volumes per buffer set
 constexpr int kMaxGroup = 16;
 constexpr int kSweepMinPairs = 3;  // smallest launch group the fused sweeps run by default
+// u8 cost volumes of a per-direction launch group kept below this (MI355X Infinity Cache:
+// 256 MiB), at no fewer than kMallMinPairs pairs per group
+constexpr size_t kMallBudget = size_t(224) << 20;
+constexpr int kMallMinPairs = 3;
 
 struct Src {  // where a launch group's pairs come from (device pointers)
     const uint8_t* L = nullptr;  // census / SGBM: images, pair i at L + i*pair_stride
@@ -960,12 +966,25 @@ int group_size(const sm_ctx* ctx, const Norm& n, int H, int npairs, bool sweep, 
     const size_t per = sweep    ? cells * (2 * elem_bytes(n) + (n.ndirs == 8 ? 2 : 0))
                        : hybrid ? cells * (hybrid_slots(n) * elem_bytes(n) + 2)
                                 : cells * elem_bytes(n) * n.ndirs;
-    const size_t g = std::max<size_t>(1, kSetBudget / std::max<size_t>(per, 1));
+    size_t g = std::max<size_t>(1, kSetBudget / std::max<size_t>(per, 1));
     // at least two groups per call when possible, so WTA(g) overlaps paths(g+1)
     const size_t half = overlap(ctx) ? std::max(1, (npairs + 1) / 2) : kMaxGroup;
     const int cap = (ctx->dbg_flags >> 16) & 15;  // ablation: launch-group size cap (0 = none)
     if (cap) return (int)std::min<size_t>({g, (size_t)cap, half});
-    return (int)std::min<size_t>({g, (size_t)kMaxGroup, half});
+    g = std::min<size_t>({g, (size_t)kMaxGroup, half});
+    // per-direction engine, u8 costs: a group whose cost volumes fit the Infinity Cache keeps
+    // them there while the 8 directions re-read them (the path volumes are stored nt, so
+    // they do not evict them): KITTI census8, 8 pairs, 262 -> 249 us per pair in groups of
+    // 4.  Only where that leaves >= kMallMinPairs pairs per group and at
+    // most two groups per call (16 pairs: one group of 16 250 us, four of 4 256 us: the
+    // horizontal chains need the pairs for parallelism); the groups are balanced.
+    if (!sweep && !hybrid && elem_bytes(n) == 1 && !(ctx->dbg_flags & DBG_NO_MALL_GROUPS)) {
+        const size_t fit = kMallBudget / std::max<size_t>(cells, 1);
+        const size_t ngroups = fit ? ((size_t)npairs + fit - 1) / fit : 0;
+        if (fit >= (size_t)kMallMinPairs && fit < g && ngroups <= 2)
+            g = std::max<size_t>(1, ((size_t)npairs + ngroups - 1) / ngroups);
+    }
+    return (int)g;
 }
 
 int ensure_event(sm_ctx* ctx, hipEvent_t& e)

@@ -303,7 +303,8 @@ __device__ __forceinline__ void pack_words(const uint32_t (&in)[N], uint32_t (&w
 
 // store N values of T at byte offset `off` (N*sizeof(T) bytes), split in
 // naturally aligned chunks of gcd(N*sizeof(T), 16) bytes
-template <typename T, int N>
+// AUX: the buffer instruction's cache-policy operand (0 = default; 2 = nt)
+template <typename T, int N, int AUX = 0>
 __device__ __forceinline__ void bstore_n(rsrc_t r, uint32_t off, const uint32_t (&in)[N])
 {
     constexpr int BYTES = N * (int)sizeof(T);
@@ -315,26 +316,26 @@ __device__ __forceinline__ void bstore_n(rsrc_t r, uint32_t off, const uint32_t 
         for (int c = 0; c < BYTES / CH; c++) {
             if constexpr (CH == 16) {
                 const u32x4 v = {w[4 * c], w[4 * c + 1], w[4 * c + 2], w[4 * c + 3]};
-                __builtin_amdgcn_raw_buffer_store_b128(v, r, off + 16 * c, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(v, r, off + 16 * c, 0, AUX);
             } else if constexpr (CH == 8) {
                 const u32x2 v = {w[2 * c], w[2 * c + 1]};
-                __builtin_amdgcn_raw_buffer_store_b64(v, r, off + 8 * c, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b64(v, r, off + 8 * c, 0, AUX);
             } else {
-                __builtin_amdgcn_raw_buffer_store_b32(w[c], r, off + 4 * c, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b32(w[c], r, off + 4 * c, 0, AUX);
             }
         }
     } else if constexpr (CH == 2) {
         if constexpr (sizeof(T) == 2) {
 #pragma unroll
-            for (int i = 0; i < N; i++) __builtin_amdgcn_raw_buffer_store_b16((uint16_t)in[i], r, off + 2 * i, 0, 0);
+            for (int i = 0; i < N; i++) __builtin_amdgcn_raw_buffer_store_b16((uint16_t)in[i], r, off + 2 * i, 0, AUX);
         } else {
 #pragma unroll
             for (int i = 0; i < N / 2; i++)
-                __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(in[2 * i] | (in[2 * i + 1] << 8)), r, off + 2 * i, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(in[2 * i] | (in[2 * i + 1] << 8)), r, off + 2 * i, 0, AUX);
         }
     } else {
 #pragma unroll
-        for (int i = 0; i < N; i++) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)in[i], r, off + i, 0, 0);
+        for (int i = 0; i < N; i++) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)in[i], r, off + i, 0, AUX);
     }
 }
 

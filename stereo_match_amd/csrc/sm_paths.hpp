@@ -27,6 +27,14 @@
 
 namespace smk {
 
+// cache policy of the path-volume stores: nt (2), so the volumes streaming out do not
+// evict the launch group's cost volume from the Infinity Cache while the other directions
+// re-read it (census8 KITTI: WTA 80 -> 74 us per pair; with Infinity-Cache-sized groups
+// paths 156 -> 145, sm_api.hip group_size); -DPATHS_STORE_AUX=0 builds the default policy
+#ifndef PATHS_STORE_AUX
+#define PATHS_STORE_AUX 2
+#endif
+
 struct PathsArgs {
     const uint64_t* cl;  // census left  [pair][H][W]
     const uint64_t* cr;  // census right [pair][H][W]
@@ -140,7 +148,7 @@ __device__ __forceinline__ void horz_impl(const PathsArgs& a, int pair, int hb, 
                     for (int i = 0; i < DPL; i++) asm volatile("" : "+v"(C[i])::"memory");
                     ring[k].load(rc, s + PF < W1 ? (uint32_t)(off + PF * step_bytes) : kOOB);
                     const uint32_t mn = sgm_step<LANES, DPL>(Lp, minLp, C, P1, P2, Ln);
-                    bstore_n<LT, DPL>(rout, (line_ok && s < W1) ? (uint32_t)off : kOOB, Ln);
+                    bstore_n<LT, DPL, PATHS_STORE_AUX>(rout, (line_ok && s < W1) ? (uint32_t)off : kOOB, Ln);
                     off += step_bytes;
 #pragma unroll
                     for (int i = 0; i < DPL; i++) Lp[i] = Ln[i];
@@ -191,7 +199,7 @@ __device__ __forceinline__ void horz_impl(const PathsArgs& a, int pair, int hb, 
 #pragma unroll
                 for (int i = 0; i < DPL; i++) C[i] = (uint32_t)__popcll(clv ^ wnd[i]);
                 const uint32_t mn = sgm_step<LANES, DPL>(Lp, minLp, C, P1, P2, Ln);
-                bstore_n<LT, DPL>(rout, (line_ok && t < lim) ? (uint32_t)off : kOOB, Ln);
+                bstore_n<LT, DPL, PATHS_STORE_AUX>(rout, (line_ok && t < lim) ? (uint32_t)off : kOOB, Ln);
                 off += step_bytes;
 #pragma unroll
                 for (int i = 0; i < DPL; i++) Lp[i] = Ln[i];
@@ -228,7 +236,7 @@ __device__ __forceinline__ void horz_impl(const PathsArgs& a, int pair, int hb, 
                 ring[k].load(rc, s + PF < W1 ? (uint32_t)(coff + PF * cstep) : kOOB);
                 coff += cstep;
                 const uint32_t mn = sgm_step<LANES, DPL>(Lp, minLp, C, P1, P2, Ln);
-                bstore_n<LT, DPL>(rout, (line_ok && s < W1) ? (uint32_t)off : kOOB, Ln);
+                bstore_n<LT, DPL, PATHS_STORE_AUX>(rout, (line_ok && s < W1) ? (uint32_t)off : kOOB, Ln);
                 off += step_bytes;
 #pragma unroll
                 for (int i = 0; i < DPL; i++) Lp[i] = Ln[i];
@@ -338,7 +346,7 @@ __device__ __forceinline__ void vert_family(const PathsArgs& a, int pair, int vb
                 nxt.load(rc, (uint32_t)coff);  // out-of-range offsets read 0 (inactive lines only)
                 const uint32_t mn = sgm_step<VL, DPL>(Lp, minLp, C, P1, P2, Ln);
                 const bool active = line_ok && x1 >= 0 && x1 < W1;
-                bstore_n<LT, DPL>(rout, active ? (uint32_t)off : kOOB, Ln);
+                bstore_n<LT, DPL, PATHS_STORE_AUX>(rout, active ? (uint32_t)off : kOOB, Ln);
 #pragma unroll
                 for (int i = 0; i < DPL; i++) Lp[i] = Ln[i];
                 minLp = mn;
@@ -390,7 +398,7 @@ __device__ __forceinline__ void vert_family(const PathsArgs& a, int pair, int vb
             }
             const uint32_t mn = sgm_step<VL, DPL>(Lp, minLp, C, P1, P2, Ln);
             const bool active = line_ok && x1 >= 0 && x1 < W1;
-            bstore_n<LT, DPL>(rout, active ? (uint32_t)off : kOOB, Ln);
+            bstore_n<LT, DPL, PATHS_STORE_AUX>(rout, active ? (uint32_t)off : kOOB, Ln);
 #pragma unroll
             for (int i = 0; i < DPL; i++) Lp[i] = Ln[i];
             minLp = mn;
@@ -412,7 +420,7 @@ __device__ __forceinline__ void vert_family(const PathsArgs& a, int pair, int vb
             nxt.load(rc, (uint32_t)coff);  // out-of-range offsets read 0 (inactive lines only)
             const uint32_t mn = sgm_step<VL, DPL>(Lp, minLp, C, P1, P2, Ln);
             const bool active = line_ok && x1 >= 0 && x1 < W1;
-            bstore_n<LT, DPL>(rout, active ? (uint32_t)off : kOOB, Ln);
+            bstore_n<LT, DPL, PATHS_STORE_AUX>(rout, active ? (uint32_t)off : kOOB, Ln);
 #pragma unroll
             for (int i = 0; i < DPL; i++) Lp[i] = Ln[i];
             minLp = mn;

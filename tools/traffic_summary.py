@@ -38,7 +38,16 @@ for k, d in vals.items():
     if stage:
         summary.setdefault("stages", {})[stage] = {"kernel": k, "hbm_bytes_per_launch": (rd or 0) + (wr or 0),
                                                    "read_bytes": rd, "write_bytes": wr}
-summary["pairs_per_launch"] = 8  # bench.py default --pairs-per-gpu (one launch group)
+# pairs per launch of the profiled run, from the bench line it printed (launch groups can
+# be smaller than --pairs-per-gpu: sm_api.hip group_size)
+summary["pairs_per_launch"] = None
+for log in glob.glob(out + "/*.log"):
+    for line in open(log):
+        if line.startswith("{"):
+            try:
+                summary["pairs_per_launch"] = json.loads(line)["roofline"]["pairs_per_launch"]
+            except (ValueError, KeyError):
+                pass
 summary["engine"] = "sweep" if any("k_sweep" in n for n in vals) else "perdir"
 summary["src_sha16"] = bench.source_hash()
 json.dump(summary, open(out + "/summary.json", "w"), indent=1)
