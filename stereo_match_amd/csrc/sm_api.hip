@@ -476,6 +476,9 @@ int launch_paths_t(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs, int dir
 }
 
 // ---- stream B: WTA (or the fused horizontal + WTA row kernel) ----------------
+#ifndef WTA_NT
+#define WTA_NT 1024  // threads per k_wta workgroup (one image row each)
+#endif
 template <int DPLV, bool CENSUS>
 int launch_wta_t(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs)
 {
@@ -541,7 +544,7 @@ int launch_wta_t(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs)
     if (ctx->fb_guard)
         hipLaunchKernelGGL((smk::k_wta<DPLV, LT, 1024, true>), grid, dim3(1024), (size_t)g.W * 8, stream_b(ctx), wa);
     else
-        hipLaunchKernelGGL((smk::k_wta<DPLV, LT, 1024>), grid, dim3(1024), (size_t)g.W * 8, stream_b(ctx), wa);
+        hipLaunchKernelGGL((smk::k_wta<DPLV, LT, WTA_NT>), grid, dim3(WTA_NT), (size_t)g.W * 8, stream_b(ctx), wa);
     HIP_TRY(ctx, hipGetLastError());
     return SM_OK;
 }
