@@ -385,30 +385,31 @@ struct RawBytes {
     static constexpr int WORDS = (NB + 3) / 4;
     static constexpr int CH = (NB % 16 == 0) ? 16 : (NB % 8 == 0) ? 8 : (NB % 4 == 0) ? 4 : (NB % 2 == 0) ? 2 : 1;
     uint32_t w[WORDS];
+    template <int AUX = 0>  // cache-policy operand (2 = nt)
     __device__ __forceinline__ void load(rsrc_t r, uint32_t off)
     {
         if constexpr (CH == 16) {
 #pragma unroll
             for (int c = 0; c < NB / 16; c++) {
-                const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off + 16 * c, 0, 0);
+                const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off + 16 * c, 0, AUX);
                 w[4 * c] = v.x; w[4 * c + 1] = v.y; w[4 * c + 2] = v.z; w[4 * c + 3] = v.w;
             }
         } else if constexpr (CH == 8) {
 #pragma unroll
             for (int c = 0; c < NB / 8; c++) {
-                const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, off + 8 * c, 0, 0);
+                const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, off + 8 * c, 0, AUX);
                 w[2 * c] = v.x; w[2 * c + 1] = v.y;
             }
         } else if constexpr (CH == 4) {
 #pragma unroll
-            for (int c = 0; c < NB / 4; c++) w[c] = __builtin_amdgcn_raw_buffer_load_b32(r, off + 4 * c, 0, 0);
+            for (int c = 0; c < NB / 4; c++) w[c] = __builtin_amdgcn_raw_buffer_load_b32(r, off + 4 * c, 0, AUX);
         } else {
 #pragma unroll
             for (int c = 0; c < WORDS; c++) w[c] = 0;
 #pragma unroll
             for (int c = 0; c < NB / CH; c++) {
-                const uint32_t v = CH == 2 ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(r, off + 2 * c, 0, 0)
-                                           : (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(r, off + c, 0, 0);
+                const uint32_t v = CH == 2 ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(r, off + 2 * c, 0, AUX)
+                                           : (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(r, off + c, 0, AUX);
                 w[(c * CH) / 4] |= v << (8 * ((c * CH) % 4));
             }
         }

@@ -20,23 +20,27 @@
 
 namespace smk {
 
+#ifndef SWEEP_STREAM_AUX
+#define SWEEP_STREAM_AUX 2  // cache policy of the E/W stores: nt (sm_sweep.hpp)
+#endif
+
 // NP packed u16 pairs -> LT bytes at byte offset off (u8: truncating pack; u16: as is)
-template <typename LT, int NP>
+template <typename LT, int NP, int AUX = 0>
 __device__ __forceinline__ void store_pk(rsrc_t r, uint32_t off, const uint32_t (&w)[NP])
 {
     if constexpr (sizeof(LT) == 2) {
-        bstore_n<uint32_t, NP>(r, off, w);
+        bstore_n<uint32_t, NP, AUX>(r, off, w);
     } else {
         constexpr int NW = NP / 2;
         if constexpr (NW > 0) {
             uint32_t b[NW];
 #pragma unroll
             for (int j = 0; j < NW; j++) b[j] = __builtin_amdgcn_perm(w[2 * j + 1], w[2 * j], 0x06040200u);
-            bstore_n<uint32_t, NW>(r, off, b);
+            bstore_n<uint32_t, NW, AUX>(r, off, b);
         }
         if constexpr (NP % 2)
             __builtin_amdgcn_raw_buffer_store_b16((uint16_t)((w[NP - 1] & 0xFFu) | ((w[NP - 1] >> 8) & 0xFF00u)), r,
-                                                  off + 4 * NW, 0, 0);
+                                                  off + 4 * NW, 0, AUX);
     }
 }
 
@@ -91,7 +95,7 @@ __global__ void __launch_bounds__(256) k_ew(EwArgs a)
             ring[k].load(rc, s + PF < W1 ? (e + (uint32_t)PF * estep) * (uint32_t)sizeof(CT) : kOOB);
             uint32_t Ln[NP];
             const uint32_t mn = sweep_step_pk<VL, NP>(Lp, minLp, C, P1p, P2, Ln);
-            store_pk<LT, NP>(ro, (line_ok && s < W1) ? e * (uint32_t)sizeof(LT) : kOOB, Ln);
+            store_pk<LT, NP, SWEEP_STREAM_AUX>(ro, (line_ok && s < W1) ? e * (uint32_t)sizeof(LT) : kOOB, Ln);
             e += estep;
 #pragma unroll
             for (int i = 0; i < NP; i++) Lp[i] = Ln[i];

@@ -50,6 +50,13 @@ typedef __attribute__((address_space(1))) unsigned long long gu64;
 
 constexpr uint32_t SW_SPIN_LIMIT = 1u << 19;
 
+// cache policy of the sweeps' read-once streams (E/W and partial loads, partial and E/W
+// stores): nt (2) keeps them from evicting the cost volume the other passes re-read (census8
+// sweeps 259.5 -> 256.1, sgbm5 259.8 -> 257.9, sgbm8 328.7 -> 323.9 us per pair); 0 = default
+#ifndef SWEEP_STREAM_AUX
+#define SWEEP_STREAM_AUX 2
+#endif
+
 // build-time switch back to the u32 recurrence for every DPL (comparison builds)
 #ifndef SWEEP_U32
 #define SWEEP_U32 0
@@ -334,10 +341,10 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL>::THREADS)) k_sweep(SweepArg
         const uint32_t eo = own ? en : NONE;
         rc_[k].load(rc, boff(en, sizeof(CT)));
         if constexpr (WTA) {
-            re_[k].load(re, boff(eo, sizeof(CT)));
-            rw_[k].load(rw, boff(eo, sizeof(CT)));
+            re_[k].template load<SWEEP_STREAM_AUX>(re, boff(eo, sizeof(CT)));
+            rw_[k].template load<SWEEP_STREAM_AUX>(rw, boff(eo, sizeof(CT)));
         }
-        if constexpr (MODE == 2) rp_[k].load(rp, boff(eo, 2));
+        if constexpr (MODE == 2) rp_[k].template load<SWEEP_STREAM_AUX>(rp, boff(eo, 2));
     };
 #pragma unroll
     for (int k = 0; k < PF; k++) issue(k, k);
@@ -482,7 +489,7 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL>::THREADS)) k_sweep(SweepArg
                     }
                 }
                 if constexpr (MODE == 0) {
-                    bstore_n<uint32_t, NP>(rp, own ? boff(e, 2) : kOOB, out);
+                    bstore_n<uint32_t, NP, SWEEP_STREAM_AUX>(rp, own ? boff(e, 2) : kOOB, out);
                 } else {
                     const uint32_t px = (uint32_t)y * (uint32_t)a.W + (uint32_t)(x1 + a.minX1);
                     __builtin_amdgcn_raw_buffer_store_b32(recw, rrec, wpx ? px * 4 : kOOB, 0, 0);
@@ -619,7 +626,7 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL>::THREADS)) k_sweep(SweepArg
                 }
             }
             if constexpr (MODE == 0) {
-                bstore_n<uint16_t, DPL>(rp, own ? boff(e, 2) : kOOB, out);
+                bstore_n<uint16_t, DPL, SWEEP_STREAM_AUX>(rp, own ? boff(e, 2) : kOOB, out);
             } else {
                 const uint32_t px = (uint32_t)y * (uint32_t)a.W + (uint32_t)(x1 + a.minX1);
                 __builtin_amdgcn_raw_buffer_store_b32(recw, rrec, wpx ? px * 4 : kOOB, 0, 0);
