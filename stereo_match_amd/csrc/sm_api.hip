@@ -1390,6 +1390,27 @@ struct WlsNorm {
     float tab[256];
 };
 
+#ifndef WLS_IEEE_DIV
+#define WLS_IEEE_DIV 0  // 1: the smoother's pivots always through IEEE division
+#endif
+
+// one smoother pass (sm_wls.hpp k_fgs) along rows or columns; FAST: pivot reciprocals by
+// rcp + one FMA step (exact for pivots in [1, 2^24)).  A register-resident row variant (each
+// lane's 16-32 elements in VGPRs, no LDS tiles) was bit-exact but slower (960 vs 885 us per
+// single-pair WLS): the serial chain, not the LDS traffic, bounds the pass.
+template <int NR, bool FAST>
+void launch_fgs_t(bool rows, dim3 grid, hipStream_t st, const smk::FgsArgs& fa)
+{
+    if (rows) hipLaunchKernelGGL((smk::k_fgs<NR, true, FAST>), grid, dim3(64), 0, st, fa);
+    else hipLaunchKernelGGL((smk::k_fgs<NR, false, FAST>), grid, dim3(64), 0, st, fa);
+}
+
+void launch_fgs(int nrhs, bool fast, bool rows, dim3 grid, hipStream_t st, const smk::FgsArgs& fa)
+{
+    if (nrhs == 2) fast ? launch_fgs_t<2, true>(rows, grid, st, fa) : launch_fgs_t<2, false>(rows, grid, st, fa);
+    else fast ? launch_fgs_t<1, true>(rows, grid, st, fa) : launch_fgs_t<1, false>(rows, grid, st, fa);
+}
+
 int normalize_wls(sm_ctx* ctx, const sm_wls_params* p, int H, int W, WlsNorm& n)
 {
     if (!p) return fail(ctx, SM_E_ARG, "wls params is NULL");
@@ -1478,18 +1499,18 @@ int run_wls(sm_ctx* ctx, const int16_t* dl, const int16_t* dr, size_t disp_pair,
             fa.wp = wp;
             fa.dbg = ((ctx->dbg_flags & DBG_FGS_NO_SWEEP) ? 1 : 0) | ((ctx->dbg_flags & DBG_FGS_NO_MEM) ? 2 : 0);
             float lam = n.lam;
+            // every pivot of every iteration below 2^24 -> the FMA-corrected reciprocal (exact there)
+            bool fast = !WLS_IEEE_DIV;
+            for (int it = 0; it < n.num_iter; it++, lam = lam * n.att)
+                fast = fast && std::isfinite(lam) && 1.0 + 2.0 * (double)lam < 16777216.0;
+            lam = n.lam;
+            const int nrhs = n.use_conf ? 2 : 1;
             for (int it = 0; it < n.num_iter; it++) {
                 fa.lam = lam;
                 fa.C = ca.Ch;
-                if (n.use_conf)
-                    hipLaunchKernelGGL((smk::k_fgs<2, true>), dim3(hp / smk::FT, g), dim3(64), 0, ctx->stream, fa);
-                else
-                    hipLaunchKernelGGL((smk::k_fgs<1, true>), dim3(hp / smk::FT, g), dim3(64), 0, ctx->stream, fa);
+                launch_fgs(nrhs, fast, true, dim3(hp / smk::FT, g), ctx->stream, fa);
                 fa.C = ca.Cv;
-                if (n.use_conf)
-                    hipLaunchKernelGGL((smk::k_fgs<2, false>), dim3(wp / smk::FT, g), dim3(64), 0, ctx->stream, fa);
-                else
-                    hipLaunchKernelGGL((smk::k_fgs<1, false>), dim3(wp / smk::FT, g), dim3(64), 0, ctx->stream, fa);
+                launch_fgs(nrhs, fast, false, dim3(wp / smk::FT, g), ctx->stream, fa);
                 HIP_TRY(ctx, hipGetLastError());
                 lam = lam * n.att;
             }

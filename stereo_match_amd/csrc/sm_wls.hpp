@@ -172,6 +172,24 @@ struct FgsArgs {
 // registers while the current chunk is swept, so the per-chunk memory latency
 // hides behind the dependent reciprocal chain.  Zero-initialised carries
 // reproduce the oracle's first-element formulas exactly (x - 0*0 == x).
+// 1/t for the Thomas pivots t in [1, 2^24): v_rcp_f32 plus one FMA Newton step is the
+// correctly rounded reciprocal there (tools/ubench/rcp_exact.hip checks every float of
+// [1, 2^24) against IEEE 1.0f / t: 0 mismatches), 3 dependent operations instead of the
+// 10 of the IEEE division sequence.  The pivots of (I + lam L_w) are >= 1 (diagonally
+// dominant, weights in [-1, 0]) and <= 1 + 2 lam; the host enables this only when
+// 1 + 2 lam < 2^24 for every iteration (sm_api.hip run_wls).
+template <bool FAST>
+__device__ __forceinline__ float pivot_rcp(float t)
+{
+#pragma clang fp contract(off)
+    if constexpr (FAST) {
+        const float y = __builtin_amdgcn_rcpf(t);
+        return __builtin_fmaf(__builtin_fmaf(-t, y, 1.0f), y, y);
+    } else {
+        return 1.0f / t;
+    }
+}
+
 template <bool ROWS>
 struct TileMap {
     // load k (0..15) of lane -> local (line, pos) of the float4's first element;
@@ -246,7 +264,7 @@ __device__ inline void tile_store(rsrc_t rs, uint32_t voff, const float* T, int 
     }
 }
 
-template <int NRHS, bool ROWS>
+template <int NRHS, bool ROWS, bool FAST = false>
 __global__ void __launch_bounds__(64) k_fgs(FgsArgs a)
 {
 #pragma clang fp contract(off)
@@ -292,7 +310,7 @@ __global__ void __launch_bounds__(64) k_fgs(FgsArgs a)
             const float cj = Ct[t];
             const float tt = 1.0f - lam * (cp + cj);
             const float lcp = lam * cp;
-            const float r = 1.0f / (tt - lcp * ip);
+            const float r = pivot_rcp<FAST>(tt - lcp * ip);
             ip = (lam * cj) * r;
             IT[t] = ip;
             p0 = (U0[t] - lcp * p0) * r;

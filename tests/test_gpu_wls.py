@@ -159,6 +159,21 @@ def test_wls_radius_wider_than_map(eng, H, W, r):
     assert np.array_equal(out, wls_np.wls_filter(displ, guide, dispr, p))
 
 
+@pytest.mark.parametrize("lam", [0.0, 80000.0, 2.0e6, 1.0e7, 3.0e8])
+def test_wls_pivot_reciprocal_both_paths(eng, lam):
+    # pivots <= 1 + 2*lambda: below 2^24 the smoother uses rcp + one FMA step (exact there,
+    # tools/ubench/rcp_exact.hip), above it IEEE division; both must equal the oracle
+    H, W = 30, 160
+    rng = np.random.default_rng(int(lam) % 1000 + 7)
+    displ = rng.integers(-16, 40 * 16, (H, W)).astype(np.int16)
+    dispr = (-rng.integers(0, 40 * 16, (H, W))).astype(np.int16)
+    guide = rng.integers(0, 256, (H, W)).astype(np.uint8)
+    p = dict(lmbda=lam, sigma=1.2, lrc_thresh=24, radius=3, use_confidence=True, left_offset=20,
+             right_offset=0, top_offset=0, bottom_offset=0, num_iter=3, min_disp=0)
+    out = eng.wls_filter(displ, guide, dispr, wls_params(p, H, W))
+    assert np.array_equal(out, wls_np.wls_filter(displ, guide, dispr, p))
+
+
 from hypothesis import HealthCheck, given, settings, strategies as st  # noqa: E402
 
 
