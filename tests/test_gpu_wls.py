@@ -171,7 +171,9 @@ def test_wls_pivot_reciprocal_both_paths(eng, lam):
     p = dict(lmbda=lam, sigma=1.2, lrc_thresh=24, radius=3, use_confidence=True, left_offset=20,
              right_offset=0, top_offset=0, bottom_offset=0, num_iter=3, min_disp=0)
     out = eng.wls_filter(displ, guide, dispr, wls_params(p, H, W))
-    assert np.array_equal(out, wls_np.wls_filter(displ, guide, dispr, p))
+    with np.errstate(all="ignore"):  # lambda 3e8: float32 pivots cancel to 0 (inf/nan) in both
+        ref = wls_np.wls_filter(displ, guide, dispr, p)
+    assert np.array_equal(out, ref)
 
 
 from hypothesis import HealthCheck, given, settings, strategies as st  # noqa: E402
