@@ -391,7 +391,7 @@ def design_kernels(args, stages, H, W, D, p, P_dirs, sweep, bm):
                 "wta": ("k_bm_sad (column sums in LDS + WTA)", H * W * (2 + 2 + 4))}, ("wta",)
     if sweep:
         rec_b = 8 * H * width1  # WTA winner record + sub-pixel inputs per pixel
-        kern = {"horizontal": ("k_sgm_paths (E/W lines only)", 4 * vol * eb),
+        kern = {"horizontal": ("k_ew (packed E/W lines)" if eb == 1 else "k_sgm_paths (E/W lines only)", 4 * vol * eb),
                 "sweep": ("k_sweep down (S+SE+SW -> u16 partial)", vol * eb + 2 * vol),
                 "sweep_wta": ("k_sweep " + ("up (N+NE+NW" if P_dirs == 8 else "down (S+SE+SW")
                               + " + E + W" + (" + partial" if P_dirs == 8 else "") + " + WTA)",

@@ -300,19 +300,23 @@ long long sm_debug_fetch(sm_ctx* ctx, int what, void* host, size_t bytes);
  * (one path volume per direction + WTA kernel) instead of the fused sweeps,
  * so that sm_debug_fetch(1) has every direction; bit 13 (valid results) one
  * pair per fused-sweep launch; bit 14 (valid results) forces the fused sweeps
- * wherever their preconditions hold (by default census 8 paths and launch
- * groups of fewer than 3 pairs run on the per-direction engine); bit 23 (valid
+ * wherever their preconditions hold (by default launch groups of fewer
+ * than 3 pairs run on the per-direction engine); bit 19 (valid results) runs
+ * the fused sweeps on narrow strips (7 compute waves per workgroup) only (by
+ * default each pass picks narrow or wide strips, where built, by a model of
+ * its issue time); bit 23 (valid
  * results) flags every fused-sweep group as given up, so the guarded
  * per-direction fallback recomputes it; bit 31 drops the guarded fallback
  * launches (timing only); bit 15 (valid results, 8 paths) the hybrid engine: the down
  * sweep on a second stream beside a per-direction launch of the other five
- * directions; bits 16-19: launch-group size cap (0 = none); bit 8 (valid
+ * directions; bits 16-18: launch-group size cap (0 = none); bit 8 (valid
  * results) swaps the fused-sweep engine's E/W kernel (u8 costs: the row lines
  * instead of the packed k_ew; u16: k_ew instead of the row lines); bit 7
  * (valid results) runs the fused sweeps on k_sweep2 with 6 waves of 8
  * columns, bit 27 with 3 waves of 16 columns (u8 costs at D = 128); bit 22
- * (valid results) the tiled SGBM cost kernel; bit 20 (valid results)
- * XCD-aware pair mapping, bit 21 interleaved vertical directions;
+ * (valid results) the tiled SGBM cost kernel; bit 21 (valid results) the
+ * fused sweeps on wide strips wherever built, whatever the strip-width model
+ * prefers (bit 20 unused);
  * bits 24-26: fused-sweep timing ablations (results become wrong: 1 no poll
  * waits, 2 no polls, 4 no per-row barriers); bits 28-29: WLS smoother timing
  * ablations (results become wrong: 28 no sweeps, 29 no global loads/stores);

@@ -79,6 +79,9 @@ constexpr int DBG_OLD_EW = 256, DBG_SWEEP_V2 = 128, DBG_SWEEP2_NW = 1 << 27;
 constexpr int DBG_FGS_NO_SWEEP = 1 << 28, DBG_FGS_NO_MEM = 1 << 29;
 // 1 << 30 (valid results): no Infinity-Cache-sized launch groups (group_size)
 constexpr int DBG_NO_MALL_GROUPS = 1 << 30;
+// 1 << 19 (valid results): the fused sweeps on narrow strips (7 compute waves) everywhere;
+// 1 << 21: on wide strips wherever built and they fit, whatever sweep_model prefers
+constexpr int DBG_NARROW_SWEEPS = 1 << 19, DBG_WIDE_SWEEPS = 1 << 21;
 // 4096: per-direction engine (one path volume per direction + k_wta) instead of the fused sweeps
 constexpr int DBG_LEGACY = 4096, DBG_SWEEP1 = 8192, DBG_SWEEP8 = 16384, DBG_HYBRID = 32768;
 constexpr int DBG_COST_TILE = 1 << 22;
@@ -351,7 +354,14 @@ const int kVdy[6] = {1, 1, 1, -1, -1, -1};
 
 constexpr size_t kSetBudget = size_t(12) << 30;  // bytes of path volumes per buffer set
 constexpr int kMaxGroup = 16;
-constexpr int kSweepMinPairs = 3;  // smallest launch group the fused sweeps run by default
+// smallest launch group the fused sweeps run by default: their time per launch is nearly
+// flat until the strips fill the CUs, so few pairs run on the per-direction engine (KITTI
+// D = 128 per pair, sweeps vs per-direction: census8 6 pairs 285 vs 259 us, 8 pairs 217 vs
+// 249; sgbm5 3 pairs 440 vs 395, 4 pairs 348 vs 368; sgbm8 3 pairs 540 vs 537)
+int sweep_min_pairs(const Norm& n)
+{
+    return n.cost == SM_COST_CENSUS ? 7 : 3;
+}
 // u8 cost volumes of a per-direction launch group kept below this (MI355X Infinity Cache:
 // 256 MiB), at no fewer than kMallMinPairs pairs per group
 constexpr size_t kMallBudget = size_t(224) << 20;
@@ -449,15 +459,8 @@ int launch_paths_t(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs, int dir
         blocks += ((pa.v_nlines[k] + 8 * LPWV - 1) / (8 * LPWV)) * 2;
     }
     for (int k = pa.nv; k <= 6; k++) pa.v_blk_start[k] = blocks;
-    if (pa.dbg & (1 << 21)) {  // interleaved directions: every direction padded to the largest count
-        int mx = 0;
-        for (int k = 0; k < pa.nv; k++) mx = std::max(mx, pa.v_blk_start[k + 1] - pa.v_blk_start[k]);
-        blocks = mx * pa.nv;
-    }
-    if (g.G % 8) pa.dbg &= ~(1 << 20);  // XCD-aware pair mapping needs whole XCD rounds
     dim3 grid(2 * pa.hblocks + blocks, g.G);
     if (ctx->fb_guard) {  // guarded fallback: a small grid that walks every block if the sweep gave up
-        pa.dbg &= ~((1 << 20) | (1 << 21));
         pa.guard = ctx->fb_guard;
         pa.nblocks = (int)grid.x;
         pa.npairs = g.G;
@@ -606,15 +609,14 @@ bool use_hybrid(const sm_ctx* ctx, const Norm& n, int H)
     return use_sweep(&tmp, n, H);
 }
 
-// preconditions of the fused sweeps (run_pairs also requires kSweepMinPairs pairs per
+// preconditions of the fused sweeps (run_pairs also requires sweep_min_pairs pairs per
 // launch group unless flag 16384 forces them)
 bool use_sweep(const sm_ctx* ctx, const Norm& n, int H)
 {
     if (ctx->dbg_flags & (DBG_LEGACY | DBG_ROW)) return false;
-    // census 8 paths (u8 volumes): the per-direction engine is level with the sweeps
-    // and stays the default (flag 16384 selects the sweeps); u16 costs at 8 paths
-    // (OpenCV MODE_HH, mc-cnn volumes) run 1.3-1.6x faster on the sweeps
-    if (n.ndirs == 8 && n.cost == SM_COST_CENSUS && !(ctx->dbg_flags & DBG_SWEEP8)) return false;
+    // every configuration whose preconditions hold: with wide strips (sm_sweep.hpp SweepGeo)
+    // census 8 paths run 217 vs 249 us per KITTI pair against the per-direction engine, u16
+    // costs at 8 paths (OpenCV MODE_HH, mc-cnn volumes) 1.5-1.7x faster
     if (n.cost == SM_COST_CENSUS && !use_cost8(ctx, n)) return false;  // the sweeps read the u8 cost volume
     // packed u16 recurrence (sm_sweep.hpp): every L must stay <= 16383 (SGBM costs: normalize's domain check)
     const int cmax = n.cost == SM_COST_CENSUS ? 64 : n.cost == SM_COST_VOLUME ? smk::VOL_CMAX : 0;
@@ -657,31 +659,62 @@ int ensure_sweep_err(sm_ctx* ctx)
     return SM_OK;
 }
 
-// which fused-sweep kernel: k_sweep (0) by default; ablation flags select k_sweep2 (column-
-// per-lane layout, sm_sweep2.hpp; u8 costs at D = 128, k_sweep elsewhere): 128 -> 6 compute
-// waves of 8 columns, 1 << 27 -> 3 waves of 16 columns (slower at 8 pairs)
+// which fused-sweep kernel: k_sweep with wide strips where built (0, sm_sweep_host.hpp),
+// flag 1 << 19 the narrow strips (1); ablation flags select k_sweep2 (column-per-lane layout,
+// sm_sweep2.hpp; u8 costs at D = 128, k_sweep elsewhere): 128 -> 6 compute waves of 8
+// columns, 1 << 27 -> 3 waves of 16 columns (slower at 8 pairs)
 int sweep_variant(const sm_ctx* ctx)
 {
     if (ctx->dbg_flags & DBG_SWEEP_V2) return 6;
-    return (ctx->dbg_flags & DBG_SWEEP2_NW) ? 3 : 0;
+    if (ctx->dbg_flags & DBG_SWEEP2_NW) return 3;
+    return (ctx->dbg_flags & DBG_NARROW_SWEEPS) ? 1 : 0;
 }
 
-// one sweep pass (MODE 0/1/2, sm_sweep.hpp) over the job's G pairs, in launches
-// whose workgroups are all co-resident (strips of a pair wait on each other)
 // strips per pair (nwg) and co-resident workgroups the context's stream can hold (cap) for one
-// sweep mode; false when (D, cost type) is not built
-bool sweep_capacity(sm_ctx* ctx, const Norm& n, int mode, smk::SweepInfo& si, int& nwg, int& cap)
+// sweep mode and kernel variant; false when (D, cost type) is not built or the strips of a
+// pair cannot all be co-resident
+struct SweepFit {
+    smk::SweepInfo si{};
+    int nwg = 0, cap = 0, ncu = 0;
+};
+bool sweep_fit_variant(sm_ctx* ctx, const Norm& n, int mode, int variant, SweepFit& f)
 {
-    if (smk::sweep_info(n.D, (int)elem_bytes(n), mode, sweep_variant(ctx), ctx->device, &si) != hipSuccess)
-        return false;
+    if (smk::sweep_info(n.D, (int)elem_bytes(n), mode, variant, ctx->device, &f.si) != hipSuccess) return false;
     int ncu = 0;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess) return false;
-    ncu = stream_cus(ctx->stream, std::max(ncu, 1));  // a CU-masked stream only reaches its CUs
+    f.ncu = stream_cus(ctx->stream, std::max(ncu, 1));  // a CU-masked stream only reaches its CUs
     // the API's answer can be one block per CU high at >= 82 SGPRs (MI355X guide);
     // for 512-thread blocks SGPRs allow >= 3 per CU, so a margin is kept only above 2
-    const int per_cu = si.blocks_per_cu >= 3 ? si.blocks_per_cu - 1 : std::max(si.blocks_per_cu, 1);
-    cap = per_cu * ncu;
-    nwg = (n.width1 + si.cw - 1) / si.cw;
+    const int per_cu = f.si.blocks_per_cu >= 3 ? f.si.blocks_per_cu - 1 : std::max(f.si.blocks_per_cu, 1);
+    f.cap = per_cu * f.ncu;
+    f.nwg = (n.width1 + f.si.cw - 1) / f.si.cw;
+    return f.nwg <= f.cap;
+}
+
+// modelled time of G pairs on one variant: the sweeps are bound by the instruction issue of
+// the CU that holds the most strips, so (launches) x (strips per CU) x (compute waves per
+// strip).  Wide strips recompute fewer halo columns per own column, narrow strips spread a
+// few pairs over more CUs (KITTI D = 128 WTA sweep, 8 pairs: wide 95 vs narrow 108 us per
+// pair; 3 pairs: 31 wide strips per pair leave 163 of 256 CUs idle)
+double sweep_model(const SweepFit& f, int G)
+{
+    const int per_launch = std::max(1, std::min(G, f.cap / std::max(f.nwg, 1)));
+    const int launches = (G + per_launch - 1) / per_launch;
+    const int per_cu = (per_launch * f.nwg + f.ncu - 1) / std::max(f.ncu, 1);
+    return (double)launches * per_cu * (f.si.threads / 64 - 1);
+}
+
+// the kernel variant for one pass over G pairs (G = 0: any that fits, wide strips first)
+bool sweep_capacity(sm_ctx* ctx, const Norm& n, int mode, int G, SweepFit& f)
+{
+    const int variant = sweep_variant(ctx);
+    if (!sweep_fit_variant(ctx, n, mode, variant, f)) {
+        // wide strips that do not fit: the narrow ones may
+        return variant == 0 && f.si.impl == 1 && sweep_fit_variant(ctx, n, mode, 1, f);
+    }
+    if (variant != 0 || f.si.impl != 1 || G <= 0 || (ctx->dbg_flags & DBG_WIDE_SWEEPS)) return true;
+    SweepFit nf;
+    if (sweep_fit_variant(ctx, n, mode, 1, nf) && sweep_model(nf, G) < sweep_model(f, G)) f = nf;
     return true;
 }
 
@@ -694,21 +727,25 @@ bool sweeps_fit(sm_ctx* ctx, const Norm& n, bool hybrid)
     const int* modes = hybrid ? mh : n.ndirs == 8 ? m8 : m5;
     const int count = !hybrid && n.ndirs == 8 ? 2 : 1;
     for (int k = 0; k < count; k++) {
-        smk::SweepInfo si{};
-        int nwg = 0, cap = 0;
-        if (!sweep_capacity(ctx, n, modes[k], si, nwg, cap) || nwg > cap) return false;
+        SweepFit f;
+        if (!sweep_capacity(ctx, n, modes[k], 0, f)) return false;
     }
     return true;
 }
 
+// one sweep pass (MODE 0/1/2, sm_sweep.hpp) over the job's G pairs, in launches
+// whose workgroups are all co-resident (strips of a pair wait on each other)
 int sweep_pass(sm_ctx* ctx, const Norm& n, const Geo& g, const SweepJob& j, int mode)
 {
-    smk::SweepInfo si{};
-    int nwg = 0, cap = 0;
-    if (!sweep_capacity(ctx, n, mode, si, nwg, cap))
+    SweepFit f;
+    if (!sweep_capacity(ctx, n, mode, j.G, f)) {
+        if (f.nwg > f.cap)
+            return fail(ctx, SM_E_UNSUPPORTED, "sweep: %d strips exceed %d resident workgroups", f.nwg, f.cap);
         return fail(ctx, SM_E_UNSUPPORTED, "sweep: numDisparities %d not built", n.D);
+    }
+    const smk::SweepInfo& si = f.si;
+    const int nwg = f.nwg, cap = f.cap;
     const int nblk = (g.H + si.hb - 1) / si.hb;
-    if (nwg > cap) return fail(ctx, SM_E_UNSUPPORTED, "sweep: %d strips exceed %d resident workgroups", nwg, cap);
     // ablation / test flag 8192: one pair per sweep launch (exercises the chunked launches)
     const int per_launch = (ctx->dbg_flags & DBG_SWEEP1) ? 1 : std::max(1, std::min(j.G, cap / nwg));
     const size_t hop_pair = (size_t)nwg * 2 * nblk * si.ngr;
@@ -753,7 +790,7 @@ int sweep_pass(sm_ctx* ctx, const Norm& n, const Geo& g, const SweepJob& j, int 
         a.nwg = nwg;
         a.epoch = ctx->hop_epoch;
         a.dbg = (ctx->dbg_flags >> 24) & 7;  // timing ablations (results wrong): 1 no polls
-        HIP_TRY(ctx, smk::sweep_launch(n.D, (int)elem_bytes(n), mode, sweep_variant(ctx), a, np, ctx->stream));
+        HIP_TRY(ctx, smk::sweep_launch(n.D, (int)elem_bytes(n), mode, si.impl, a, np, ctx->stream));
     }
     return SM_OK;
 }
@@ -972,7 +1009,7 @@ int group_size(const sm_ctx* ctx, const Norm& n, int H, int npairs, bool sweep, 
     size_t g = std::max<size_t>(1, kSetBudget / std::max<size_t>(per, 1));
     // at least two groups per call when possible, so WTA(g) overlaps paths(g+1)
     const size_t half = overlap(ctx) ? std::max(1, (npairs + 1) / 2) : kMaxGroup;
-    const int cap = (ctx->dbg_flags >> 16) & 15;  // ablation: launch-group size cap (0 = none)
+    const int cap = (ctx->dbg_flags >> 16) & 7;  // ablation: launch-group size cap (0 = none)
     if (cap) return (int)std::min<size_t>({g, (size_t)cap, half});
     g = std::min<size_t>({g, (size_t)kMaxGroup, half});
     // per-direction engine, u8 costs: a group whose cost volumes fit the Infinity Cache keeps
@@ -1356,10 +1393,9 @@ int run_pairs(sm_ctx* ctx, const Src& src, int npairs, int H, int W, int stride,
     g.census_pair = (size_t)H * W;
     g.cost_pair = n.cost == SM_COST_CENSUS ? 0 : g.vol;
     int G = group_size(ctx, n, H, npairs, g.sweep, g.hybrid);
-    // the sweeps' parallelism is (strips x pairs): below kSweepMinPairs pairs per launch
-    // group the per-direction engine is faster (KITTI D=128, sgbm5: 521 vs 901 us for one
-    // pair, 459 vs 527 for two, 426 vs 416 for three); flag 16384 forces them
-    if (g.sweep && std::min(G, npairs) < kSweepMinPairs && !(ctx->dbg_flags & DBG_SWEEP8)) {
+    // the sweeps' parallelism is (strips x pairs): below sweep_min_pairs pairs per launch
+    // group the per-direction engine is faster; flag 16384 forces them
+    if (g.sweep && std::min(G, npairs) < sweep_min_pairs(n) && !(ctx->dbg_flags & DBG_SWEEP8)) {
         g.sweep = false;
         G = group_size(ctx, n, H, npairs, false, false);
     }

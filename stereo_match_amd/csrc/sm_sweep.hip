@@ -1,6 +1,10 @@
 // sm_sweep.hip — translation unit of the fused-sweep kernels (sm_sweep.hpp):
 // instantiates k_sweep for every built (D, cost type, mode) and exposes a
-// plain host interface to sm_api.hip, so the two units compile in parallel.
+// plain host interface to sm_api.hip, so the units compile in parallel.  Built
+// once per (SWEEP_MODE, SWEEP_WIDE): the narrow strips (NCW 7, every D, plus the
+// k_sweep2 ablation and k_lr_rows) and the wide strips (wide_ncw, where built).
+#include <algorithm>
+
 #include "sm_sweep.hpp"
 #include "sm_sweep2.hpp"
 #include "sm_sweep_host.hpp"
@@ -43,27 +47,48 @@ hipError_t with_d(int D, F& f)
 
 namespace {
 
+#ifndef SWEEP_WIDE
+#define SWEEP_WIDE 0
+#endif
+
+// compute waves of this unit's instance for (D, CT); 0 = not built here
+template <int D, typename CT>
+constexpr int unit_ncw()
+{
+    return SWEEP_WIDE ? wide_ncw(D, (int)sizeof(CT)) : kNarrowNcw;
+}
+
 struct InfoF {
     int device;
     SweepInfo* out;
     template <int VL, int DPL, typename CT, int MODE>
     hipError_t run()
     {
-        using SG = SweepGeo<VL, DPL>;
-        static int per_cu = -1;  // per instance (one device type per process)
-        if (per_cu < 0) {
-            int nb = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_sweep<VL, DPL, CT, MODE>, SG::THREADS, 0) !=
-                hipSuccess)
-                nb = 1;
-            per_cu = nb;
+        constexpr int NCW = unit_ncw<VL * DPL, CT>();
+        if constexpr (NCW == 0) {
+            return hipErrorInvalidValue;
+        } else {
+            using SG = SweepGeo<VL, DPL, NCW>;
+            auto kern = k_sweep<VL, DPL, CT, MODE, NCW>;
+            static int per_cu = -1;  // per instance (one device type per process)
+            if (per_cu < 0) {
+                int nb = 0;
+                if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, SG::THREADS, 0) != hipSuccess) nb = 0;
+                // a wide instance is used only if it runs without scratch and fits a CU
+                hipFuncAttributes fa{};
+                if (SWEEP_WIDE && (hipFuncGetAttributes(&fa, (const void*)kern) != hipSuccess || fa.localSizeBytes > 0))
+                    nb = 0;
+                per_cu = SWEEP_WIDE ? nb : std::max(nb, 1);
+            }
+            if (per_cu < 1) return hipErrorInvalidValue;
+            out->cw = SG::CW;
+            out->hb = SG::HB;
+            out->ngr = SG::NGR;
+            out->threads = SG::THREADS;
+            out->blocks_per_cu = per_cu;
+            out->impl = SWEEP_WIDE ? 1 : 0;
+            return hipSuccess;
         }
-        out->cw = SG::CW;
-        out->hb = SG::HB;
-        out->ngr = SG::NGR;
-        out->threads = SG::THREADS;
-        out->blocks_per_cu = per_cu;
-        return hipSuccess;
     }
 };
 
@@ -74,10 +99,18 @@ struct LaunchF {
     template <int VL, int DPL, typename CT, int MODE>
     hipError_t run()
     {
-        hipLaunchKernelGGL((k_sweep<VL, DPL, CT, MODE>), grid, dim3(SweepGeo<VL, DPL>::THREADS), 0, stream, *a);
-        return hipGetLastError();
+        constexpr int NCW = unit_ncw<VL * DPL, CT>();
+        if constexpr (NCW == 0) {
+            return hipErrorInvalidValue;
+        } else {
+            hipLaunchKernelGGL((k_sweep<VL, DPL, CT, MODE, NCW>), grid, dim3(SweepGeo<VL, DPL, NCW>::THREADS), 0,
+                               stream, *a);
+            return hipGetLastError();
+        }
     }
 };
+
+#if !SWEEP_WIDE
 
 // column-per-lane sweeps (sm_sweep2.hpp, a measured ablation): built for u8 (census) costs
 // at D = 128; variant = compute waves per workgroup: 3 (16 columns per wave), 6 (8 columns)
@@ -100,6 +133,7 @@ hipError_t sweep2_run(bool info, int device, SweepInfo* out, const SweepArgs* a,
         out->ngr = SG::NGR;
         out->threads = SG::THREADS;
         out->blocks_per_cu = per_cu;
+        out->impl = NW;
         return hipSuccess;
     }
     hipLaunchKernelGGL(kern, dim3(a->nwg, npairs), dim3(SG::THREADS), 0, stream, *a);
@@ -125,11 +159,27 @@ hipError_t sweep2(int D, int ct_bytes, int variant, bool info, int device, Sweep
     }
 }
 
+#endif  // !SWEEP_WIDE
+
 }  // namespace
 
 #define SW_CAT2(a, b) a##b
 #define SW_CAT(a, b) SW_CAT2(a, b)
 
+#if SWEEP_WIDE
+hipError_t SW_CAT(sweep_info_wide_m, SWEEP_MODE)(int D, int ct_bytes, int device, SweepInfo* out)
+{
+    InfoF f{device, out};
+    return with_sweep(D, ct_bytes, f);
+}
+
+hipError_t SW_CAT(sweep_launch_wide_m, SWEEP_MODE)(int D, int ct_bytes, const SweepArgs& a, int npairs,
+                                                   hipStream_t stream)
+{
+    LaunchF f{&a, dim3(a.nwg, npairs), stream};
+    return with_sweep(D, ct_bytes, f);
+}
+#else
 hipError_t SW_CAT(sweep_info_m, SWEEP_MODE)(int D, int ct_bytes, int variant, int device, SweepInfo* out)
 {
     if (variant && sweep2(D, ct_bytes, variant, true, device, out, nullptr, 0, nullptr) == hipSuccess)
@@ -148,8 +198,9 @@ hipError_t SW_CAT(sweep_launch_m, SWEEP_MODE)(int D, int ct_bytes, int variant, 
     LaunchF f{&a, dim3(a.nwg, npairs), stream};
     return with_sweep(D, ct_bytes, f);
 }
+#endif
 
-#if SWEEP_MODE == 0
+#if SWEEP_MODE == 0 && !SWEEP_WIDE
 hipError_t lr_rows_launch(const uint32_t* rec, const uint32_t* nb, int16_t* out, int G, int H, int W, int D, int minD,
                           int minX1, int maxX1, int disp12, hipStream_t stream)
 {

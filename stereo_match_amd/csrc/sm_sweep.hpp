@@ -62,13 +62,17 @@ constexpr uint32_t SW_SPIN_LIMIT = 1u << 19;
 #define SWEEP_U32 0
 #endif
 
-template <int VL, int DPL>
+// NCW: compute waves per workgroup (left halo, NCW-2 own, right halo).  Every strip
+// recomputes 2 halo waves' columns, so wider strips cost fewer instructions per own
+// column; they also hold more waves per workgroup (fewer blocks per CU) and give fewer
+// strips per pair.  Measured (KITTI D = 128, 8 pairs, profiles/r02/ablations/sweep_ncw_*):
+// census8 sweeps 244 -> 217 us per pair at NCW 7 -> 11, sgbm5 247 -> 235, sgbm8 321 -> 287
+// at NCW 13 (u16 costs); 9, 12, 14 and 15 are slower (the strip count against 256 CUs).
+constexpr int kNarrowNcw = 7;
+template <int VL, int DPL, int NCW_ = kNarrowNcw>
 struct SweepGeo {
     static constexpr int LPW = 64 / VL;             // columns per wave
-#ifndef SWEEP_NCW
-#define SWEEP_NCW 7
-#endif
-    static constexpr int NCW = SWEEP_NCW;           // compute waves: left halo, NCW-2 own, right halo
+    static constexpr int NCW = NCW_;                // compute waves: left halo, NCW-2 own, right halo
     static constexpr int THREADS = (NCW + 1) * 64;  // + the poller wave
     static constexpr int HB = LPW;                  // rows per block = halo width
     static constexpr int NCOL = NCW * LPW;          // columns held by the compute waves
@@ -79,6 +83,17 @@ struct SweepGeo {
     static constexpr int NGR = 64 * NG;             // granules per (strip, direction, block)
     static constexpr int PF = 4;                    // rows of inputs in flight per lane
 };
+
+// wide strips where every mode's instance keeps its registers at the wide block size
+// (12 waves: <= 168 VGPRs, 14 waves: <= 128; round-2 builds): NCW 11 for u8 costs, 13 for
+// u16 costs where it fits, else 11; 0 = not built (the host also checks for scratch and
+// occupancy before it picks a wide instance, sm_sweep.hip)
+constexpr int wide_ncw(int D, int ct_bytes)
+{
+    if (ct_bytes == 1) return (D <= 96 || D == 128 || D == 160 || D == 192) ? 11 : 0;
+    if (D == 16 || D == 32 || D == 96 || D == 128) return 13;
+    return (D == 48 || D == 80 || D == 160) ? 11 : 0;
+}
 
 // NP packed words of one lane <-> LDS (widest aligned chunks)
 template <int NP>
@@ -223,10 +238,10 @@ __device__ __forceinline__ void poll_granules(const gu64* src, bool need, uint32
     }
 }
 
-template <int VL, int DPL, typename CT, int MODE>
-__global__ void __launch_bounds__((SweepGeo<VL, DPL>::THREADS)) k_sweep(SweepArgs a)
+template <int VL, int DPL, typename CT, int MODE, int NCW_ = kNarrowNcw>
+__global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(SweepArgs a)
 {
-    using G = SweepGeo<VL, DPL>;
+    using G = SweepGeo<VL, DPL, NCW_>;
     constexpr bool UP = MODE == 2;
     constexpr bool WTA = MODE != 0;
     constexpr int LPW = G::LPW, NCW = G::NCW, HB = G::HB, NCOL = G::NCOL, COLS = G::COLS, CW = G::CW, D = G::D;
@@ -638,7 +653,7 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL>::THREADS)) k_sweep(SweepArg
     }
 }
 
-#if !defined(SWEEP_MODE) || SWEEP_MODE == 0  // one unit owns the non-template kernel
+#if !defined(SWEEP_MODE) || (SWEEP_MODE == 0 && !SWEEP_WIDE)  // one unit owns the non-template kernel
 // Winner's sub-pixel value, disp2 (right-view argmin, cv::StereoSGBM's
 // disp2/disp2cost) and the disp12MaxDiff check from the WTA sweep's per-pixel
 // records: the tail of k_wta (sm_paths.hpp) over one row per workgroup.

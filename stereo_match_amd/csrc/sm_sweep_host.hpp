@@ -34,35 +34,54 @@ struct SweepInfo {
     int ngr;            // halo granules per (strip, direction, block)
     int threads;        // threads per workgroup
     int blocks_per_cu;  // occupancy API answer for that block size
+    int impl;           // kernel: 0 k_sweep narrow strips, 1 k_sweep wide strips, 3 / 6 k_sweep2
 };
 
 template <typename CT, int MODE, class F>
 hipError_t with_d(int D, F& f);
 
 // per mode (one translation unit each); hipErrorInvalidValue when (D, ct_bytes) is not built.
-// variant 0: k_sweep (sm_sweep.hpp); 2 / 4: k_sweep2 (sm_sweep2.hpp) with that many compute
-// waves per workgroup where built (u8 costs, D = 64 / 128), k_sweep elsewhere.  sweep_info
-// and sweep_launch of one pass must get the same variant.
+// variant 0: k_sweep, wide strips where built and usable (no scratch, >= 1 block per CU),
+// narrow (7 compute waves) elsewhere; 1: narrow strips; 3 / 6: k_sweep2 (sm_sweep2.hpp) with
+// that many compute waves per workgroup where built (u8 costs, D = 128), k_sweep elsewhere.
+// sweep_info reports the kernel it picked in SweepInfo::impl; sweep_launch takes that impl.
 hipError_t sweep_info_m0(int D, int ct_bytes, int variant, int device, SweepInfo* out);
 hipError_t sweep_info_m1(int D, int ct_bytes, int variant, int device, SweepInfo* out);
 hipError_t sweep_info_m2(int D, int ct_bytes, int variant, int device, SweepInfo* out);
+hipError_t sweep_info_wide_m0(int D, int ct_bytes, int device, SweepInfo* out);
+hipError_t sweep_info_wide_m1(int D, int ct_bytes, int device, SweepInfo* out);
+hipError_t sweep_info_wide_m2(int D, int ct_bytes, int device, SweepInfo* out);
 // grid (a.nwg, npairs), SweepInfo::threads threads
 hipError_t sweep_launch_m0(int D, int ct_bytes, int variant, const SweepArgs& a, int npairs, hipStream_t stream);
 hipError_t sweep_launch_m1(int D, int ct_bytes, int variant, const SweepArgs& a, int npairs, hipStream_t stream);
 hipError_t sweep_launch_m2(int D, int ct_bytes, int variant, const SweepArgs& a, int npairs, hipStream_t stream);
+hipError_t sweep_launch_wide_m0(int D, int ct_bytes, const SweepArgs& a, int npairs, hipStream_t stream);
+hipError_t sweep_launch_wide_m1(int D, int ct_bytes, const SweepArgs& a, int npairs, hipStream_t stream);
+hipError_t sweep_launch_wide_m2(int D, int ct_bytes, const SweepArgs& a, int npairs, hipStream_t stream);
 
 inline hipError_t sweep_info(int D, int ct_bytes, int mode, int variant, int device, SweepInfo* out)
 {
-    return mode == 0 ? sweep_info_m0(D, ct_bytes, variant, device, out)
-         : mode == 1 ? sweep_info_m1(D, ct_bytes, variant, device, out)
-                     : sweep_info_m2(D, ct_bytes, variant, device, out);
+    if (variant == 0) {
+        const hipError_t e = mode == 0 ? sweep_info_wide_m0(D, ct_bytes, device, out)
+                           : mode == 1 ? sweep_info_wide_m1(D, ct_bytes, device, out)
+                                       : sweep_info_wide_m2(D, ct_bytes, device, out);
+        if (e == hipSuccess) return e;
+    }
+    const int v = variant == 1 ? 0 : variant;
+    return mode == 0 ? sweep_info_m0(D, ct_bytes, v, device, out)
+         : mode == 1 ? sweep_info_m1(D, ct_bytes, v, device, out)
+                     : sweep_info_m2(D, ct_bytes, v, device, out);
 }
-inline hipError_t sweep_launch(int D, int ct_bytes, int mode, int variant, const SweepArgs& a, int npairs,
+inline hipError_t sweep_launch(int D, int ct_bytes, int mode, int impl, const SweepArgs& a, int npairs,
                                hipStream_t stream)
 {
-    return mode == 0 ? sweep_launch_m0(D, ct_bytes, variant, a, npairs, stream)
-         : mode == 1 ? sweep_launch_m1(D, ct_bytes, variant, a, npairs, stream)
-                     : sweep_launch_m2(D, ct_bytes, variant, a, npairs, stream);
+    if (impl == 1)
+        return mode == 0 ? sweep_launch_wide_m0(D, ct_bytes, a, npairs, stream)
+             : mode == 1 ? sweep_launch_wide_m1(D, ct_bytes, a, npairs, stream)
+                         : sweep_launch_wide_m2(D, ct_bytes, a, npairs, stream);
+    return mode == 0 ? sweep_launch_m0(D, ct_bytes, impl, a, npairs, stream)
+         : mode == 1 ? sweep_launch_m1(D, ct_bytes, impl, a, npairs, stream)
+                     : sweep_launch_m2(D, ct_bytes, impl, a, npairs, stream);
 }
 // sub-pixel + disp2 + disp12MaxDiff check from the WTA sweep's records, one row per workgroup
 hipError_t lr_rows_launch(const uint32_t* rec, const uint32_t* nb, int16_t* out, int G, int H, int W, int D, int minD,

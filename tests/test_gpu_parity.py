@@ -88,12 +88,15 @@ for _i in range(36):
                       d12=int(_rng.choice([1, 2, 1000000])), seed=int(_rng.integers(0, 1 << 30))))
 
 
-@pytest.mark.parametrize("flags", [0, 4096, 16384, 32768], ids=["default", "perdir", "sweep8", "hybrid"])
+@pytest.mark.parametrize("flags", [0, 4096, 16384, 16384 | (1 << 19), 16384 | (1 << 21), 32768],
+                         ids=["default", "perdir", "sweep8", "sweep8narrow", "sweep8wide", "hybrid"])
 @pytest.mark.parametrize("c", CASES, ids=lambda c: "H{H}W{W}D{D}m{minD}c{cost}p{mode}".format(**c))
 def test_random_shapes_vs_c_oracle(eng, c, flags):
     """Default engines (one pair per call: per-direction), the per-direction
     engine (4096), the fused sweeps forced for every configuration (16384; by
-    default they need >= 3 pairs per launch group) and the hybrid engine
+    default they need >= 3 pairs per launch group; one pair picks narrow strips
+    where the strip-width model prefers them), on narrow strips everywhere
+    (1 << 19) and on wide strips wherever built (1 << 21), and the hybrid engine
     (32768, 5 and 8 paths)."""
     eng.set_debug_flags(flags)
     try:
@@ -141,7 +144,11 @@ def test_sgbm_cost_block_sizes(eng, bs, D, minD):
                                                   # sweep-engine E/W kernel swapped (256), k_sweep2 (128, 1 << 27)
                                                   ("kitti", 1, 8, 16384 | 256), ("kitti", 0, 5, 256),
                                                   ("kitti", 1, 8, 16384 | 128), ("kitti", 1, 8, 16384 | (1 << 27)),
-                                                  ("kitti", 1, 5, 128)])
+                                                  ("kitti", 1, 5, 128),
+                                                  # narrow (1 << 19) and wide (1 << 21) sweep strips
+                                                  ("kitti", 1, 8, 16384 | (1 << 19)), ("kitti", 0, 5, 16384 | (1 << 19)),
+                                                  ("kitti", 1, 8, 16384 | (1 << 21)), ("kitti", 0, 5, 16384 | (1 << 21)),
+                                                  ("kitti", 0, 8, 16384 | (1 << 21)), ("mccnn", 1, 8, 16384 | (1 << 21))])
 def test_full_size_bit_exact(eng, name, cost, mode, flags):
     H, W, D = synthetic.CONFIGS[name]
     left, right, gt = synthetic.random_dot_pair(H, W, D, seed=42)
@@ -474,3 +481,35 @@ def test_hypothesis_matcher_vs_c_oracle(eng, H, W, Dk, minD, cost, mode, bs, P1,
     # x86 saturating arithmetic, which the C oracle restates
     out = run(eng, left, right, p)
     assert np.array_equal(out, ref_c.compute(left, right, p))
+
+
+@pytest.mark.parametrize("cost,mode", [(1, 8), (0, 5), (0, 8)])
+def test_sweep_strip_widths_agree_on_a_kitti_batch(eng, cost, mode):
+    """8 KITTI pairs per call (the bench's launch group): the default sweeps (each
+    pass picks narrow or wide strips by its model), narrow (1 << 19) and wide
+    (1 << 21) strips forced, and the per-direction engine (4096) return the same
+    maps; pair 0 equals the C oracle."""
+    import torch
+
+    H, W, D = synthetic.CONFIGS["kitti"]
+    n = 8
+    pairs = [synthetic.random_dot_pair(H, W, D, seed=300 + s)[:2] for s in range(n)]
+    p = dict(synthetic.headline_params(D) if cost else synthetic.parity_params(D), mode=mode)
+    L = torch.tensor(np.stack([a for a, _ in pairs]), device="cuda")
+    R = torch.tensor(np.stack([b for _, b in pairs]), device="cuda")
+    outs = {}
+    for flags in (0, 1 << 19, 1 << 21, 4096):
+        out = torch.full((n, H, W), 12345, dtype=torch.int16, device="cuda")
+        eng.set_debug_flags(flags)
+        try:
+            eng.set_stream(torch.cuda.current_stream().cuda_stream)
+            eng.compute_batch_device(L.data_ptr(), R.data_ptr(), n, H * W, H, W, W, synthetic.to_sm_params(p),
+                                     out.data_ptr())
+            outs[flags] = out.cpu().numpy()
+            eng.synchronize()
+        finally:
+            eng.set_stream(None)
+            eng.set_debug_flags(0)
+    for flags, o in outs.items():
+        assert np.array_equal(o, outs[4096]), flags
+    assert np.array_equal(outs[0][0], ref_c.compute(pairs[0][0], pairs[0][1], p))

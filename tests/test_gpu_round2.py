@@ -226,8 +226,8 @@ def test_valid_result_flags_leave_compute_disparity_unchanged(eng, D):
     wf.setSigmaColor(s["sigma"])
     wp = wf.params(H, W)
     ref = eng.compute_disparity(gl, gr, prm, wp)
-    for f in (8, 64, 128, 256, 1 << 12, 1 << 13, 1 << 14, (1 << 14) | 128, (1 << 14) | 256, 1 << 15,
-              1 << 20, 1 << 22, 1 << 23, 1 << 27, 1 << 30, 2 << 16):
+    for f in (8, 64, 128, 256, 1 << 12, 1 << 13, 1 << 14, (1 << 14) | 128, (1 << 14) | 256, (1 << 14) | (1 << 19), 1 << 15,
+              1 << 19, 1 << 21, 1 << 22, 1 << 23, 1 << 27, 1 << 30, 2 << 16):
         eng.set_debug_flags(f)
         try:
             got = eng.compute_disparity(gl, gr, prm, wp)
