@@ -394,6 +394,16 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
                     if constexpr (MODE == 2) asm volatile("" : "+v"(Pin[i])::"memory");
                 }
                 issue(k, s + PF);
+                // E + W (+ the down partial): off the recurrences' dependency chain (saturating
+                // adds of non-negative values are associative, so the sum below is unchanged)
+                uint32_t EWP[NP];
+                if constexpr (WTA) {
+#pragma unroll
+                    for (int i = 0; i < NP; i++) {
+                        EWP[i] = pk_adds(Ein[i], Win[i]);
+                        if constexpr (MODE == 2) EWP[i] = pk_adds(EWP[i], Pin[i]);
+                    }
+                }
 
                 uint32_t nA[NP], nB[NP];
                 uint32_t mnA = 0, mnB = 0;
@@ -451,8 +461,7 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
                         uint32_t key = 0xFFFFFFFFu;
 #pragma unroll
                         for (int i = 0; i < NP; i++) {
-                            uint32_t t = pk_adds(pk_adds(pk_adds(pk_adds(nV[i], nA[i]), nB[i]), Ein[i]), Win[i]);
-                            if constexpr (MODE == 2) t = pk_adds(t, Pin[i]);
+                            uint32_t t = pk_adds(pk_adds(nV[i], nA[i]), pk_adds(nB[i], EWP[i]));
                             t = pk_min(t, 0x7FFF7FFFu);  // min(sum, 32767) (census sums stay below 2^11)
                             Sp[i] = t;
                             S[2 * i] = t & 0xFFFFu;

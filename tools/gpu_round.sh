@@ -29,7 +29,7 @@ if [ "$PART" = A ] || [ "$PART" = T ]; then
   step bench 400 python -u bench.py --traffic-file "$OUT/census8_traffic.json"
   step bench_sgbm5 400 python -u bench.py --mode sgbm5 --traffic-file "$OUT/sgbm5_traffic.json"
 else
-  step bench_census8_sweep 300 python -u bench.py --engine sweep --cpu-baseline-pairs 0 --host-surface-calls 0
+  step bench_census8_perdir 300 python -u bench.py --engine perdir --cpu-baseline-pairs 0 --host-surface-calls 0
   step bench_sgbm5_perdir 300 python -u bench.py --mode sgbm5 --engine perdir --cpu-baseline-pairs 0 --host-surface-calls 0
   for m in sgbm8 volume8 disparity5 bm; do step bench_$m 300 python -u bench.py --mode $m --host-surface-calls 0; done
   step bench_middlebury 400 python -u bench.py --config middlebury --pairs-per-gpu 4 --steps 40 --warmup 4 --cpu-baseline-pairs 0 --host-surface-calls 0

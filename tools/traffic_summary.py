@@ -28,11 +28,15 @@ for k, d in vals.items():
     wr = ws * 1024 if ws is not None else None
     summary["kernels"][k] = {"fetch_size_kb": fs, "write_size_kb": ws, "read_bytes_corrected": rd,
                              "write_bytes": wr, "hbm_bytes": (rd or 0) + (wr or 0)}
-    sweep = any("k_sweep" in n for n in vals)  # fused-sweep engine: k_sgm_paths runs the E/W lines only
-    if "k_sweep" in k:  # template argument list ends with the sweep mode (0 = down partial, 1/2 = with WTA)
-        stage = "sweep" if k.split(">")[0].rstrip().endswith(" 0") else "sweep_wta"
+    sweep = any("k_sweep" in n for n in vals)  # fused-sweep engine
+    targs = [t.strip() for t in k.split("<", 1)[1].split(">")[0].split(",")] if "<" in k else []
+    fallback = bool(targs) and targs[-1] == "true" and ("k_sgm_paths" in k or "k_wta" in k)  # guarded instances
+    if "k_sweep2<" in k or "k_sweep<" in k:  # sweep mode: 0 = down partial, 1/2 = with WTA
+        stage = "sweep" if targs[4 if "k_sweep2<" in k else 3] == "0" else "sweep_wta"
+    elif fallback:
+        stage = None
     else:
-        stage = (("horizontal" if sweep else "paths") if "k_sgm_paths" in k
+        stage = ("horizontal" if "k_ew<" in k or (sweep and "k_sgm_paths" in k) else "paths" if "k_sgm_paths" in k
                  else "wta" if ("k_wta" in k or "k_row_wta" in k)
                  else "cost" if any(c in k for c in ("k_census9x7", "k_sgbm_cost(", "k_cost_volume_f32")) else None)
     if stage:
