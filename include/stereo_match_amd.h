@@ -270,6 +270,12 @@ int sm_set_cu_mask(sm_ctx* ctx, const uint32_t* mask, int nwords);
  * sweep strip gave up waiting for its neighbours; see sm_get_counters) */
 #define SM_STAGE_FALLBACK 12
 #define SM_NUM_STAGES 13
+/* enable: 0 off, 1 every stage, SM_TIMING_ONLY | (1 << stage) | ... only those
+ * stages.  Every timed stage records two hipEvents per launch on its stream,
+ * which delays the stream (KITTI census8, 8 pairs per call: every stage timed
+ * costs about 12 us per pair of wall time), so a throughput measurement times
+ * only the stages it reports. */
+#define SM_TIMING_ONLY 0x40000000
 int sm_set_timing(sm_ctx* ctx, int enable);
 int sm_get_timing(sm_ctx* ctx, int stage, double* total_ms, long long* launches, long long* pairs);
 int sm_reset_timing(sm_ctx* ctx);

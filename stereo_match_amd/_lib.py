@@ -21,6 +21,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "stereo_match_amd.
 SM_OK, SM_E_ARG, SM_E_HIP, SM_E_UNSUPPORTED = 0, -1, -2, -4
 SM_COST_SGBM, SM_COST_CENSUS, SM_COST_VOLUME = 0, 1, 2
 SM_MODE_SGBM, SM_MODE_HH = 5, 8
+TIMING_ONLY = 0x40000000  # include/stereo_match_amd.h SM_TIMING_ONLY
 STAGES = ("cost", "paths", "wta", "median", "total", "wls", "speckle", "horizontal", "sweep", "sweep_wta", "h2d",
           "d2h", "fallback")
 
@@ -398,8 +399,15 @@ class Engine:
         self._check(self._lib.sm_set_cu_mask(self.ctx, words, nwords))
 
     # -- timing ---------------------------------------------------------------
-    def set_timing(self, on: bool):
-        self._check(self._lib.sm_set_timing(self.ctx, int(bool(on))))
+    def set_timing(self, on, stages=None):
+        """on: every stage; with ``stages`` (names from STAGES) only those stages
+        record events (each timed stage delays the stream a little)."""
+        v = int(bool(on))
+        if on and stages is not None:
+            v = TIMING_ONLY
+            for name in stages:
+                v |= 1 << STAGES.index(name)
+        self._check(self._lib.sm_set_timing(self.ctx, v))
 
     def reset_timing(self):
         self._check(self._lib.sm_reset_timing(self.ctx))

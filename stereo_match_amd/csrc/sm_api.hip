@@ -122,7 +122,7 @@ struct sm_ctx {
     int lastH = 0, lastW = 0, last_width1 = 0, lastD = 0, last_ndirs = 0, last_cost = 0, last_minD = 0;
     int last_minX1 = 0, last_index = 0, last_set = 0;
     size_t last_L_pair = 0;
-    bool timing = false;
+    uint32_t timing = 0;  // stages timed (bit = SM_STAGE_*), sm_set_timing
     int dbg_flags = 0;
     std::vector<TimedEvent> pending;
     std::vector<hipEvent_t> free_events;
@@ -243,14 +243,14 @@ struct StageTimer {
     hipEvent_t a = nullptr;
     StageTimer(sm_ctx* c, hipStream_t st, int stg, int np) : ctx(c), s(st), stage(stg), pairs(np)
     {
-        if (ctx->timing) {
+        if (ctx->timing & (1u << stage)) {
             a = get_event(ctx);
             (void)hipEventRecord(a, s);
         }
     }
     ~StageTimer()
     {
-        if (ctx->timing) {
+        if (a) {
             hipEvent_t b = get_event(ctx);
             (void)hipEventRecord(b, s);
             ctx->pending.push_back({stage, pairs, a, b});
@@ -2361,7 +2361,11 @@ int sm_set_timing(sm_ctx* ctx, int enable)
 {
     if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
     if (ctx->twin) sm_set_timing(ctx->twin, enable);
-    ctx->timing = enable != 0;
+    // 1: every stage; SM_TIMING_ONLY | stage bits: those stages only (each timed stage
+    // records two events per launch, which delay the stream by about a microsecond each)
+    ctx->timing = enable == 0 ? 0u
+                : (enable & SM_TIMING_ONLY) ? (uint32_t)enable & ((1u << SM_NUM_STAGES) - 1)
+                                            : (1u << SM_NUM_STAGES) - 1;
     return SM_OK;
 }
 

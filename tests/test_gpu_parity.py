@@ -306,6 +306,19 @@ def test_timing_counters(eng):
     t = eng.timing()
     eng.set_timing(False)
     assert t["paths"][1] == 2 and t["horizontal"][1] == 2 and t["sweep_wta"][1] == 2 and t["wta"][1] == 2
+    # only the named stages record events (SM_TIMING_ONLY: what bench.py's timed region uses)
+    eng.set_timing(True, stages=["sweep_wta"])
+    eng.reset_timing()
+    eng.set_debug_flags(16384)
+    try:
+        out = run(eng, left, right, synthetic.parity_params(64))
+    finally:
+        eng.set_debug_flags(0)
+    t = eng.timing()
+    eng.set_timing(False)
+    assert t["sweep_wta"][1] == 1 and t["sweep_wta"][0] > 0
+    assert all(v[1] == 0 for k, v in t.items() if k != "sweep_wta")
+    assert np.array_equal(out, ref_c.compute(left, right, synthetic.parity_params(64)))
 
 
 # ---------------------------------------------------------------- mc-cnn cost volume
