@@ -57,6 +57,15 @@ constexpr uint32_t SW_SPIN_LIMIT = 1u << 19;
 #define SWEEP_STREAM_AUX 2
 #endif
 
+// row synchronisation inside a block of HB rows: 1 = each wave waits for its two neighbours'
+// published rows (LDS counters; modes 0 and 2), 0 = a workgroup barrier per row
+#ifndef SWEEP_ROW_SYNC
+#define SWEEP_ROW_SYNC 1
+#endif
+#ifndef SWEEP_ROW_SLEEP
+#define SWEEP_ROW_SLEEP 1  // s_sleep between polls of the neighbours' row counters
+#endif
+
 // build-time switch back to the u32 recurrence for every DPL (comparison builds)
 #ifndef SWEEP_U32
 #define SWEEP_U32 0
@@ -244,6 +253,10 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
     using G = SweepGeo<VL, DPL, NCW_>;
     constexpr bool UP = MODE == 2;
     constexpr bool WTA = MODE != 0;
+    // neighbour-counter row sync: KITTI 8 pairs, down sweep census8 96.4 -> 92.0 us per pair,
+    // sgbm8 124.0 -> 120.8, census8 WTA sweep level (96.6 / 96.0); the 5-path WTA sweep is
+    // slower with it (95.3 -> 97.9) and keeps the row barriers
+    constexpr bool ROWSYNC = SWEEP_ROW_SYNC && MODE != 1;
     constexpr int LPW = G::LPW, NCW = G::NCW, HB = G::HB, NCOL = G::NCOL, COLS = G::COLS, CW = G::CW, D = G::D;
     constexpr int NG = G::NG, NGR = G::NGR, PF = G::PF;
     constexpr int CB = DPL * (int)sizeof(CT);  // cost / E / W bytes per lane and cell
@@ -252,10 +265,14 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
     // WTA sweeps: each own column's aggregated costs S of the current row
     // (wave-local; the line's first lane reads S[best-1], S[best+1] back)
     __shared__ __attribute__((aligned(16))) uint16_t srow[WTA ? NCW - 2 : 1][WTA ? LPW : 1][WTA ? D : 2];
+    // rows whose LDS state each compute wave has published (inside a block of HB rows the
+    // waves synchronise with their two neighbours only; SWEEP_ROW_SYNC)
+    __shared__ uint32_t rowcnt[NCW];
 
     for (int i = threadIdx.x; i < 2 * 2 * COLS * D / 2; i += G::THREADS)
         reinterpret_cast<uint32_t*>(&lv[0][0][0][0])[i] = 0;
     for (int i = threadIdx.x; i < 2 * 2 * COLS; i += G::THREADS) (&lmin[0][0][0])[i] = 0;
+    for (int i = threadIdx.x; i < NCW; i += G::THREADS) rowcnt[i] = 0;
     __syncthreads();
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -280,8 +297,12 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
         const int col = (dir == 0 ? pkl : NCOL - LPW + pkl) + 1;  // LDS column slot
         bool dead = (a.dbg & 1) != 0;
         for (int b = 0; b < nblk; b++) {
+            if (ROWSYNC) {
+                if (!(a.dbg & 4)) lds_barrier();  // the compute waves' end-of-block barrier
+            } else {
 #pragma unroll 1
-            for (int j = 0; j < HB; j++) if (!(a.dbg & 4)) lds_barrier();  // 4: timing only, no row barriers
+                for (int j = 0; j < HB; j++) if (!(a.dbg & 4)) lds_barrier();  // 4: timing only, no row barriers
+            }
             if (b + 1 < nblk) {
                 if ((has_left || has_right) && !(a.dbg & 2)) {  // wave-uniform
                     uint32_t v[GPL];
@@ -319,6 +340,39 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
     const int wx0 = wg * CW + wave * LPW - LPW;
     const bool wave_ragged = wx0 < 0 || wx0 + LPW > W1;  // wave-uniform: some column outside [0, W1)
     const uint32_t P1 = (uint32_t)a.P1, P2 = (uint32_t)a.P2;
+    // row hand-off inside a block: a wave's step s reads its neighbours' row s-1 state
+    // from one LDS buffer and writes its own row s into the other, which the neighbours
+    // read at their step s-1; so step s may start once both neighbours have published
+    // row s-1 (that also orders their reads of the buffer this step overwrites).  The
+    // block's last row ends with a workgroup barrier (the poller's halo snapshot).
+    const int wl = wave > 0 ? wave - 1 : wave, wr = wave < NCW - 1 ? wave + 1 : wave;
+    bool sync_dead = (a.dbg & 4) != 0;
+    auto publish_row = [&](int s) {
+        __hip_atomic_store(&rowcnt[wave], (uint32_t)(s + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    auto wait_row = [&](int s) {
+        if (sync_dead) return;
+        for (uint32_t spins = 0;; spins++) {
+            const uint32_t nl = __builtin_amdgcn_readfirstlane(
+                __hip_atomic_load(&rowcnt[wl], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+            const uint32_t nr = __builtin_amdgcn_readfirstlane(
+                __hip_atomic_load(&rowcnt[wr], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+            if (min(nl, nr) >= (uint32_t)s) return;
+            if (spins >= SW_SPIN_LIMIT) {  // never expected: report, let the guarded fallback recompute
+                if (lane == 0) atomicOr(a.err, 1u);
+                sync_dead = true;
+                return;
+            }
+            if (SWEEP_ROW_SLEEP) __builtin_amdgcn_s_sleep(SWEEP_ROW_SLEEP);
+        }
+    };
+    auto end_row = [&](int j, int s) {
+        if (!ROWSYNC || j == HB - 1) {
+            if (!(a.dbg & 4)) lds_barrier();
+        } else {
+            publish_row(s);
+        }
+    };
 
     const uint64_t cells = (uint64_t)H * W1 * D;
     const rsrc_t rc = make_rsrc(a.cost + (size_t)pair * a.cost_pair, cells * sizeof(CT));
@@ -405,6 +459,7 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
                     }
                 }
 
+                if (ROWSYNC && j > 0) wait_row(s);
                 uint32_t nA[NP], nB[NP];
                 uint32_t mnA = 0, mnB = 0;
                 if (!halo_r) {
@@ -519,7 +574,7 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
                     __builtin_amdgcn_raw_buffer_store_b32(recw, rrec, wpx ? px * 4 : kOOB, 0, 0);
                     __builtin_amdgcn_raw_buffer_store_b32(nbw, rnb, wpx ? px * 4 : kOOB, 0, 0);
                 }
-                if (!(a.dbg & 4)) lds_barrier();
+                end_row(j, s);
             }
             if (b + 1 < nblk) lds_barrier();
         }
@@ -554,6 +609,7 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
             }
             issue(k, s + PF);
 
+            if (ROWSYNC && j > 0) wait_row(s);
             // diagonal predecessors: column c-1 (A) and c+1 (B) of the previous row
             uint32_t nA[DPL], nB[DPL];  // a halo wave leaves its other direction unset (never read)
             uint32_t mnA = 0, mnB = 0;
@@ -656,7 +712,7 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
                 __builtin_amdgcn_raw_buffer_store_b32(recw, rrec, wpx ? px * 4 : kOOB, 0, 0);
                 __builtin_amdgcn_raw_buffer_store_b32(nbw, rnb, wpx ? px * 4 : kOOB, 0, 0);
             }
-            if (!(a.dbg & 4)) lds_barrier();
+            end_row(j, s);
         }
         if (b + 1 < nblk) lds_barrier();  // the poller has written the halo snapshot
     }
