@@ -949,6 +949,9 @@ int check_sweep_errors(sm_ctx* ctx)
 
 // SGBM cost volume, streaming form (sm_cost.hpp k_sgbm_cost2): one workgroup per
 // (TX-column strip, band of rows, pair)
+#ifndef SGBM_COST2_WGS
+#define SGBM_COST2_WGS 2048  // workgroups a launch aims for (bands = this / (strips x pairs))
+#endif
 template <int S, int CPT>
 int launch_cost2_s(sm_ctx* ctx, const Norm& n, const Geo& g, const smk::SgbmCostArgs& sc)
 {
@@ -972,7 +975,7 @@ int launch_cost2_s(sm_ctx* ctx, const Norm& n, const Geo& g, const smk::SgbmCost
     c2.Yc = sc.Yc;
     const int strips = (n.width1 + TX - 1) / TX;
     // enough workgroups to fill the chip; bands at least 8 rows (warm-up 2S rows each)
-    const int want = std::max(1, 2048 / std::max(1, strips * g.G));
+    const int want = std::max(1, SGBM_COST2_WGS / std::max(1, strips * g.G));
     c2.band = std::max({(sc.Yc + want - 1) / want, 8, 4 * S});
     const int bands = (sc.Yc + c2.band - 1) / c2.band;
     if (one)
@@ -1158,7 +1161,7 @@ int run_wide(sm_ctx* ctx, const Src& src, const Geo& g, const Norm& n, BufSet& b
         pf.stride = g.stride;
         pf.ftzero = n.ftzero;
         pf.cn = n.cn;
-        hipLaunchKernelGGL(smk::k_sgbm_prefilter, dim3((W + 255) / 256, H, 2 * G * n.cn), dim3(256), 0, ctx->stream,
+        hipLaunchKernelGGL(smk::k_sgbm_prefilter, dim3((W + 255) / 256, (H + smk::PF_ROWS - 1) / smk::PF_ROWS, 2 * G * n.cn), dim3(256), 0, ctx->stream,
                            pf);
         HIP_TRY(ctx, hipGetLastError());
         smk::WideArgs wa{};
@@ -1295,7 +1298,7 @@ int run_group(sm_ctx* ctx, const Src& src, const Geo& g, const Norm& n, int16_t*
             pf.stride = g.stride;
             pf.ftzero = n.ftzero;
             pf.cn = 1;
-            hipLaunchKernelGGL(smk::k_sgbm_prefilter, dim3((W + 255) / 256, H, 2 * G), dim3(256), 0, ctx->stream, pf);
+            hipLaunchKernelGGL(smk::k_sgbm_prefilter, dim3((W + 255) / 256, (H + smk::PF_ROWS - 1) / smk::PF_ROWS, 2 * G), dim3(256), 0, ctx->stream, pf);
             HIP_TRY(ctx, hipGetLastError());
             smk::SgbmCostArgs sc{};
             sc.planes = (const uint2*)ctx->planes.p;

@@ -22,8 +22,11 @@ struct CensusArgs {
 constexpr int CT_W = 64, CT_H = 16, CT_PY = 4;  // tile; pixels per thread (vertical)
 constexpr int CT_LW = CT_W + 12;                 // LDS row: 4 left halo + 64 + 4 right halo, dword padded
 
-// Bits are assembled MSB-first with acc = 2*acc + (I[n] < I[c]) so each
-// comparison is one compare + one add-with-carry; the 62 neighbours of a
+// Bits are assembled MSB-first: I[n] - I[c] (bytes, so bit 31 of the 32-bit
+// difference is I[n] < I[c]) shifted in by v_alignbit, acc = (acc << 1) | (diff >> 31):
+// two VALU ops per bit, the byte select folded into the subtract (SDWA), no
+// compare mask (a compare + select + shift + or, with hazard NOPs on the lane
+// mask, was ~4 per bit); the 62 neighbours of a
 // pixel are read as 3 aligned dwords per window row (bytes extracted by the
 // compiler), and a thread computes CT_PY vertically adjacent pixels so the
 // 7-row windows share their LDS reads.
@@ -62,14 +65,12 @@ __global__ void __launch_bounds__(256) k_census9x7(CensusArgs a)
 #pragma unroll
         for (int k = 61; k >= 32; k--) {
             const int n = k < 31 ? k : k + 1;
-            unsigned co;
-            hi = __builtin_addc(hi, hi, px(p + n / 9, n % 9) < c ? 1u : 0u, &co);
+            hi = __builtin_amdgcn_alignbit(hi, px(p + n / 9, n % 9) - c, 31);
         }
 #pragma unroll
         for (int k = 31; k >= 0; k--) {
             const int n = k < 31 ? k : k + 1;
-            unsigned co;
-            lo = __builtin_addc(lo, lo, px(p + n / 9, n % 9) < c ? 1u : 0u, &co);
+            lo = __builtin_amdgcn_alignbit(lo, px(p + n / 9, n % 9) - c, 31);
         }
         if (x < a.W && y < a.H)
             a.out[which][(size_t)pair * a.H * a.W + (size_t)y * a.W + x] = ((uint64_t)hi << 32) | lo;
@@ -91,7 +92,13 @@ struct Cost8Args {
     int H, W, width1, D, minD, minX1;
 };
 
-constexpr int C8_TX = 64, C8_RY = 4;
+#ifndef CENSUS_COST_NT
+#define CENSUS_COST_NT 1  // the cost volume leaves with nontemporal stores (0: default policy)
+#endif
+#ifndef CENSUS_COST_RY
+#define CENSUS_COST_RY 4  // image rows per k_census_cost8 workgroup
+#endif
+constexpr int C8_TX = 64, C8_RY = CENSUS_COST_RY;
 
 __global__ void __launch_bounds__(256) k_census_cost8(Cost8Args a)
 {
@@ -132,7 +139,13 @@ __global__ void __launch_bounds__(256) k_census_cost8(Cost8Args a)
         uint4* out = reinterpret_cast<uint4*>(a.C + pair * a.C_pair + ((size_t)y * a.width1 + x0) * D);
         for (int i = tid; i < nx * chunks; i += 256) {
             const int x = (int)(((uint32_t)i * M) >> 16), ch = i - x * chunks;
+#if CENSUS_COST_NT
+            typedef unsigned v4u __attribute__((ext_vector_type(4)));
+            const uint4 t = tile[x * pitch + ch];
+            __builtin_nontemporal_store(v4u{t.x, t.y, t.z, t.w}, reinterpret_cast<v4u*>(out + i));
+#else
             out[i] = tile[x * pitch + ch];
+#endif
         }
     }
 }
@@ -181,56 +194,73 @@ struct PrefilterArgs {
 // min/max over the half-pixel neighbours as calcPixelCostBT); blockIdx.z =
 // (2*pair + view)*cn + channel (colour: one plane per channel, as OpenCV's
 // calcPixelCostBT keeps a derivative and a raw row per channel).
+#ifndef PREFILTER_ROWS
+#define PREFILTER_ROWS 8  // image rows per k_sgbm_prefilter workgroup
+#endif
+constexpr int PF_ROWS = PREFILTER_ROWS;
+
+// One workgroup per (256 columns, PF_ROWS rows, view): the PF_ROWS + 2 image rows
+// (+2 halo columns each side) and the clipped Sobel of columns x0-1 .. x0+256 of each
+// output row in LDS (a row of workgroups per image row re-read every input row 3x and
+// left the launch dominated by its 2*H*pairs tiny workgroups).
 __global__ void __launch_bounds__(256) k_sgbm_prefilter(PrefilterArgs a)
 {
-    // one workgroup per (256 columns, row, view): the three image rows (+2 halo
-    // columns each side) and the clipped Sobel of columns x0-1 .. x0+256 in LDS
-    __shared__ uint8_t rows[3][260];
-    __shared__ int gs[258];
+    __shared__ uint8_t rows[PF_ROWS + 2][260];
+    __shared__ int gs[PF_ROWS][258];
     const int cn = a.cn > 0 ? a.cn : 1;
     const int ch = blockIdx.z % cn, view = blockIdx.z / cn;
-    const int x0 = blockIdx.x * 256, y = blockIdx.y, im = view & 1, pair = view >> 1;
+    const int x0 = blockIdx.x * 256, y0 = blockIdx.y * PF_ROWS, im = view & 1, pair = view >> 1;
     const int W = a.W, H = a.H, ft = a.ftzero, tid = threadIdx.x;
     const uint8_t* img = a.img[im] + (size_t)pair * a.in_pair + ch;
-    for (int i = tid; i < 3 * 260; i += 256) {
-        const int r = i / 260, c = i - r * 260;
-        rows[r][c] = img[(size_t)min(max(y - 1 + r, 0), H - 1) * a.stride + (size_t)min(max(x0 - 2 + c, 0), W - 1) * cn];
+#pragma unroll
+    for (int r = 0; r < PF_ROWS + 2; r++) {
+        const uint8_t* row = img + (size_t)min(max(y0 - 1 + r, 0), H - 1) * a.stride;
+        for (int c = tid; c < 260; c += 256) rows[r][c] = row[(size_t)min(max(x0 - 2 + c, 0), W - 1) * cn];
     }
     __syncthreads();
-    for (int i = tid; i < 258; i += 256) {  // column xx = x0 - 1 + i sits at rows[.][i + 1]
-        const int xx = x0 - 1 + i, c = i + 1;
-        int v = ft;
-        if (xx > 0 && xx < W - 1) {
-            v = (rows[1][c + 1] - rows[1][c - 1]) * 2 + rows[0][c + 1] - rows[0][c - 1] + rows[2][c + 1] - rows[2][c - 1];
-            v = min(max(v, -ft), ft) + ft;
+#pragma unroll
+    for (int r = 0; r < PF_ROWS; r++) {
+        for (int i = tid; i < 258; i += 256) {  // column xx = x0 - 1 + i sits at rows[.][i + 1]
+            const int xx = x0 - 1 + i, c = i + 1;
+            int v = ft;
+            if (xx > 0 && xx < W - 1) {
+                v = (rows[r + 1][c + 1] - rows[r + 1][c - 1]) * 2 + rows[r][c + 1] - rows[r][c - 1] + rows[r + 2][c + 1] -
+                    rows[r + 2][c - 1];
+                v = min(max(v, -ft), ft) + ft;
+            }
+            gs[r][i] = v;
         }
-        gs[i] = v;
     }
     __syncthreads();
     const int x = x0 + tid;
     if (x >= W) return;
-    auto raw = [&](int xx) { return (xx <= 0 || xx >= W - 1) ? ft : (int)rows[1][xx - x0 + 2]; };
-    uint32_t b[6];
-    {
-        const int v = gs[tid + 1];
-        const int vl = x > 0 ? (v + gs[tid]) / 2 : v;
-        const int vr = x < W - 1 ? (v + gs[tid + 2]) / 2 : v;
-        b[0] = (uint32_t)v;
-        b[1] = (uint32_t)min(min(vl, vr), v);
-        b[2] = (uint32_t)max(max(vl, vr), v);
+#pragma unroll
+    for (int r = 0; r < PF_ROWS; r++) {
+        const int y = y0 + r;
+        if (y >= H) break;
+        auto raw = [&](int xx) { return (xx <= 0 || xx >= W - 1) ? ft : (int)rows[r + 1][xx - x0 + 2]; };
+        uint32_t b[6];
+        {
+            const int v = gs[r][tid + 1];
+            const int vl = x > 0 ? (v + gs[r][tid]) / 2 : v;
+            const int vr = x < W - 1 ? (v + gs[r][tid + 2]) / 2 : v;
+            b[0] = (uint32_t)v;
+            b[1] = (uint32_t)min(min(vl, vr), v);
+            b[2] = (uint32_t)max(max(vl, vr), v);
+        }
+        {
+            const int v = raw(x);
+            const int vl = x > 0 ? (v + raw(x - 1)) / 2 : v;
+            const int vr = x < W - 1 ? (v + raw(x + 1)) / 2 : v;
+            b[3] = (uint32_t)v;
+            b[4] = (uint32_t)min(min(vl, vr), v);
+            b[5] = (uint32_t)max(max(vl, vr), v);
+        }
+        uint2 w;
+        w.x = b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
+        w.y = b[4] | (b[5] << 8);
+        reinterpret_cast<uint2*>(a.planes)[((size_t)blockIdx.z * H + y) * W + x] = w;
     }
-    {
-        const int v = raw(x);
-        const int vl = x > 0 ? (v + raw(x - 1)) / 2 : v;
-        const int vr = x < W - 1 ? (v + raw(x + 1)) / 2 : v;
-        b[3] = (uint32_t)v;
-        b[4] = (uint32_t)min(min(vl, vr), v);
-        b[5] = (uint32_t)max(max(vl, vr), v);
-    }
-    uint2 w;
-    w.x = b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
-    w.y = b[4] | (b[5] << 8);
-    reinterpret_cast<uint2*>(a.planes)[((size_t)blockIdx.z * H + y) * W + x] = w;
 }
 
 // C_true[y][x1][d] for the rows OpenCV's incremental box filter actually
@@ -413,6 +443,9 @@ __global__ void __launch_bounds__(256) k_sgbm_cost(SgbmCostArgs a)
 // halo rows, and a wave stores whole 256-byte d-rows (NP = D/2 lanes per
 // column).  Sums are u16 pairs in u32 lanes: every subtracted term was added
 // before, so no borrow crosses lanes.  Bands start 2S rows early (warm-up).
+#ifndef SGBM_COST_AUX
+#define SGBM_COST_AUX 2  // cache policy of k_sgbm_cost2's cost-volume stores: nt (0: default)
+#endif
 struct SgbmCost2Args {
     const uint2* planes;  // packed, [pair][view][H][W]
     uint16_t* C;          // [pair][H][width1][D]
@@ -584,7 +617,7 @@ __global__ void __launch_bounds__(256) k_sgbm_cost2(SgbmCost2Args a)
                     vs[i] += h;
                     ring[q][i] = h;
                     // column step as the scalar offset: one voffset for all CPT stores
-                    if (i < nval) __builtin_amdgcn_raw_buffer_store_b32(vs[i], rc, ob, i * 2 * D, 0);
+                    if (i < nval) __builtin_amdgcn_raw_buffer_store_b32(vs[i], rc, ob, i * 2 * D, SGBM_COST_AUX);
                     vs[i] -= ring[(q + 1) % R][i];  // row r - 2S leaves the window
                 }
             }
@@ -614,6 +647,9 @@ __global__ void __launch_bounds__(256) k_sgbm_cost_tail(uint16_t* C, size_t C_pa
 // sgm_np.quantize_volume).  (c + offset) * scale cannot be contracted into an
 // FMA, so the two IEEE roundings match the oracle's.
 constexpr int VOL_CMAX = 4095;
+#ifndef VOL_COST_NT
+#define VOL_COST_NT 1  // the quantised volume leaves with nontemporal stores (0: default policy)
+#endif
 
 
 struct VolArgs {
@@ -680,7 +716,11 @@ __global__ void __launch_bounds__(256) k_cost_volume_f32(VolArgs a)
     const int total = nx * half;
     for (int i = threadIdx.x; i < total; i += 256) {
         const int xl = i / half, j = i - xl * half;
+#if VOL_COST_NT
+        __builtin_nontemporal_store(tile[xl * rowdw + j], out + i);
+#else
         out[i] = tile[xl * rowdw + j];
+#endif
     }
 }
 

@@ -57,6 +57,11 @@ constexpr uint32_t SW_SPIN_LIMIT = 1u << 19;
 #define SWEEP_STREAM_AUX 2
 #endif
 
+// cache policy of the WTA sweep's cost loads (the cost volume's last reader): 0 = default
+#ifndef SWEEP_COST_AUX
+#define SWEEP_COST_AUX 0
+#endif
+
 // row synchronisation inside a block of HB rows: 1 = each wave waits for its two neighbours'
 // published rows (LDS counters; modes 0 and 2), 0 = a workgroup barrier per row
 #ifndef SWEEP_ROW_SYNC
@@ -408,7 +413,7 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
     auto issue = [&](int k, int s) {  // loads of step s into ring slot k (rows past the end read 0)
         const uint32_t en = s < H ? cell(UP ? H - 1 - s : s) : NONE;
         const uint32_t eo = own ? en : NONE;
-        rc_[k].load(rc, boff(en, sizeof(CT)));
+        rc_[k].template load<WTA ? SWEEP_COST_AUX : 0>(rc, boff(en, sizeof(CT)));
         if constexpr (WTA) {
             re_[k].template load<SWEEP_STREAM_AUX>(re, boff(eo, sizeof(CT)));
             rw_[k].template load<SWEEP_STREAM_AUX>(rw, boff(eo, sizeof(CT)));

@@ -56,6 +56,10 @@ def main():
             same[f] = same[f] and bool(torch.equal(out, ref))
             res[f].append({k: v[0] * 1e3 / max(v[2], 1) for k, v in t.items()})
     eng.set_debug_flags(0)
+    import hashlib
+    # digest of the default engine's maps: equal across builds = the same results
+    print(json.dumps({"lib": os.path.basename(_lib.LIB_PATH), "mode": args.mode,
+                      "out_sha16": hashlib.sha256(ref.cpu().numpy().tobytes()).hexdigest()[:16]}))
     for f in flags:
         med = {k: float(np.median([x[k] for x in res[f]])) for k in res[f][0]}
         print(json.dumps({"flags": f, "same_as_0": same[f],
