@@ -947,6 +947,16 @@ int check_sweep_errors(sm_ctx* ctx)
     return SM_OK;
 }
 
+// Cost volumes leave with nontemporal stores when the launch group's volume cannot stay in
+// the 256 MB Infinity Cache anyway (census8, 8 KITTI pairs: 227.3 -> 219.9 us per pair, the
+// sweeps after the cost faster too); a group that fits (one pair per call, the per-direction
+// engine's cache-sized groups) keeps default stores, so its readers hit the cache
+// (single-pair compute_disparity 1.98 vs 2.33 ms with nt).  DESIGN.md §4.1 "Cost stage".
+int cost_nt(const Geo& g, size_t elem_bytes)
+{
+    return (size_t)g.G * g.vol * elem_bytes > ((size_t)224 << 20) ? 1 : 0;
+}
+
 // SGBM cost volume, streaming form (sm_cost.hpp k_sgbm_cost2): one workgroup per
 // (TX-column strip, band of rows, pair)
 #ifndef SGBM_COST2_WGS
@@ -973,6 +983,7 @@ int launch_cost2_s(sm_ctx* ctx, const Norm& n, const Geo& g, const smk::SgbmCost
     c2.minD = sc.minD;
     c2.minX1 = sc.minX1;
     c2.Yc = sc.Yc;
+    c2.nt = cost_nt(g, 2);
     const int strips = (n.width1 + TX - 1) / TX;
     // enough workgroups to fill the chip; bands at least 8 rows (warm-up 2S rows each)
     const int want = std::max(1, SGBM_COST2_WGS / std::max(1, strips * g.G));
@@ -1261,6 +1272,7 @@ int run_group(sm_ctx* ctx, const Src& src, const Geo& g, const Norm& n, int16_t*
                 c8.D = n.D;
                 c8.minD = n.minD;
                 c8.minX1 = n.minX1;
+                c8.nt = cost_nt(g, 1);
                 hipLaunchKernelGGL(smk::k_census_cost8,
                                    dim3((n.width1 + smk::C8_TX - 1) / smk::C8_TX, (H + smk::C8_RY - 1) / smk::C8_RY, G),
                                    dim3(256),
@@ -1281,6 +1293,7 @@ int run_group(sm_ctx* ctx, const Src& src, const Geo& g, const Norm& n, int16_t*
             va.minX1 = n.minX1;
             va.offset = src.offset;
             va.scale = src.scale;
+            va.nt = cost_nt(g, 2);
             // 64-column tiles measured faster than 128 (117 vs 130 us/pair at D=192)
             hipLaunchKernelGGL(smk::k_cost_volume_f32<64>, dim3((n.width1 + 63) / 64, H, G), dim3(256),
                                (size_t)64 * (n.D / 2 + 1) * 4, ctx->stream, va);

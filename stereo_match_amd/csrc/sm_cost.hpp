@@ -90,11 +90,9 @@ struct Cost8Args {
     uint8_t* C;
     size_t C_pair;
     int H, W, width1, D, minD, minX1;
+    int nt;  // 1: nontemporal stores (the launch group's volume exceeds the Infinity Cache)
 };
 
-#ifndef CENSUS_COST_NT
-#define CENSUS_COST_NT 1  // the cost volume leaves with nontemporal stores (0: default policy)
-#endif
 #ifndef CENSUS_COST_RY
 #define CENSUS_COST_RY 4  // image rows per k_census_cost8 workgroup
 #endif
@@ -139,13 +137,13 @@ __global__ void __launch_bounds__(256) k_census_cost8(Cost8Args a)
         uint4* out = reinterpret_cast<uint4*>(a.C + pair * a.C_pair + ((size_t)y * a.width1 + x0) * D);
         for (int i = tid; i < nx * chunks; i += 256) {
             const int x = (int)(((uint32_t)i * M) >> 16), ch = i - x * chunks;
-#if CENSUS_COST_NT
-            typedef unsigned v4u __attribute__((ext_vector_type(4)));
-            const uint4 t = tile[x * pitch + ch];
-            __builtin_nontemporal_store(v4u{t.x, t.y, t.z, t.w}, reinterpret_cast<v4u*>(out + i));
-#else
-            out[i] = tile[x * pitch + ch];
-#endif
+            if (a.nt) {  // workgroup-uniform
+                typedef unsigned v4u __attribute__((ext_vector_type(4)));
+                const uint4 t = tile[x * pitch + ch];
+                __builtin_nontemporal_store(v4u{t.x, t.y, t.z, t.w}, reinterpret_cast<v4u*>(out + i));
+            } else {
+                out[i] = tile[x * pitch + ch];
+            }
         }
     }
 }
@@ -443,14 +441,12 @@ __global__ void __launch_bounds__(256) k_sgbm_cost(SgbmCostArgs a)
 // halo rows, and a wave stores whole 256-byte d-rows (NP = D/2 lanes per
 // column).  Sums are u16 pairs in u32 lanes: every subtracted term was added
 // before, so no borrow crosses lanes.  Bands start 2S rows early (warm-up).
-#ifndef SGBM_COST_AUX
-#define SGBM_COST_AUX 2  // cache policy of k_sgbm_cost2's cost-volume stores: nt (0: default)
-#endif
 struct SgbmCost2Args {
     const uint2* planes;  // packed, [pair][view][H][W]
     uint16_t* C;          // [pair][H][width1][D]
     size_t C_pair;
     int H, W, width1, D, minD, minX1, Yc, band;
+    int nt;  // 1: nontemporal stores (the launch group's volume exceeds the Infinity Cache)
 };
 
 template <int S, int CPT, int NLR>
@@ -617,7 +613,10 @@ __global__ void __launch_bounds__(256) k_sgbm_cost2(SgbmCost2Args a)
                     vs[i] += h;
                     ring[q][i] = h;
                     // column step as the scalar offset: one voffset for all CPT stores
-                    if (i < nval) __builtin_amdgcn_raw_buffer_store_b32(vs[i], rc, ob, i * 2 * D, SGBM_COST_AUX);
+                    if (i < nval) {
+                        if (a.nt) __builtin_amdgcn_raw_buffer_store_b32(vs[i], rc, ob, i * 2 * D, 2);
+                        else __builtin_amdgcn_raw_buffer_store_b32(vs[i], rc, ob, i * 2 * D, 0);
+                    }
                     vs[i] -= ring[(q + 1) % R][i];  // row r - 2S leaves the window
                 }
             }
@@ -647,9 +646,6 @@ __global__ void __launch_bounds__(256) k_sgbm_cost_tail(uint16_t* C, size_t C_pa
 // sgm_np.quantize_volume).  (c + offset) * scale cannot be contracted into an
 // FMA, so the two IEEE roundings match the oracle's.
 constexpr int VOL_CMAX = 4095;
-#ifndef VOL_COST_NT
-#define VOL_COST_NT 1  // the quantised volume leaves with nontemporal stores (0: default policy)
-#endif
 
 
 struct VolArgs {
@@ -658,6 +654,7 @@ struct VolArgs {
     uint16_t* C;
     size_t C_pair;  // elements between pairs
     int H, W, width1, D, minX1;
+    int nt;  // 1: nontemporal stores (the launch group's volume exceeds the Infinity Cache)
     float offset, scale;
 };
 
@@ -716,11 +713,8 @@ __global__ void __launch_bounds__(256) k_cost_volume_f32(VolArgs a)
     const int total = nx * half;
     for (int i = threadIdx.x; i < total; i += 256) {
         const int xl = i / half, j = i - xl * half;
-#if VOL_COST_NT
-        __builtin_nontemporal_store(tile[xl * rowdw + j], out + i);
-#else
-        out[i] = tile[xl * rowdw + j];
-#endif
+        if (a.nt) __builtin_nontemporal_store(tile[xl * rowdw + j], out + i);
+        else out[i] = tile[xl * rowdw + j];
     }
 }
 
