@@ -40,7 +40,20 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
-METRIC = "stereo pairs/sec + Mpix·disp/sec, KITTI 1242×375 D=128 SGM, 1/2/4/8 GPU"
+METRIC = "stereo pairs/sec + Mpix·disp/sec, KITTI 1242×375 D=128 SGM, 1/2/4/8 GPU"  # BASELINE.json metric
+CONFIG_NAMES = {"tsukuba": "Tsukuba", "kitti": "KITTI", "middlebury": "Middlebury-v3 full-res",
+                "mccnn": "KITTI-size mc-cnn cost volume"}
+
+
+def metric_for(config: str) -> str:
+    """BASELINE.json's metric string for its headline config (KITTI); the same
+    wording with the workload named for the other configs."""
+    if config == "kitti":
+        return METRIC
+    from stereo_match_amd import synthetic
+
+    H, W, D = synthetic.CONFIGS[config]
+    return f"stereo pairs/sec + Mpix·disp/sec, {CONFIG_NAMES[config]} {W}×{H} D={D} SGM, 1/2/4/8 GPU"
 
 
 def parse():
@@ -57,6 +70,9 @@ def parse():
                          "bm = StereoBM(numDisparities=D, blockSize=21), the method='BM' matcher")
     ap.add_argument("--pairs-per-gpu", type=int, default=8)
     ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--dist", action="store_true",
+                    help="initialise the process group (RCCL on the GPU) and run the gather even at world size 1, "
+                         "so the multi-rank code path runs on one GPU")
     ap.add_argument("--engine", default="auto", choices=["auto", "perdir", "sweep"],
                     help="auto: the library's default per configuration; perdir / sweep force one engine "
                          "(DESIGN.md §4)")
@@ -69,7 +85,8 @@ def parse():
                          "settings.ini, KITTI size); 0 = skip")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
     ap.add_argument("--selftest-cpu", action="store_true",
-                    help="launcher self-test: gloo on CPU, a stand-in step (no disparity computed, not a measurement)")
+                    help="rank-path self-test: main's own sharding / timing / gather / JSON code over gloo on CPU with "
+                         "a stand-in step (no disparity computed, not a measurement)")
     return ap.parse_args()
 
 
@@ -157,181 +174,162 @@ def model_stage_bytes(stage: str, mode: str, H: int, W: int, D: int, P: int, swe
 
 
 # ---------------------------------------------------------------------------
-def main():
-    args = parse()
-    if args.config is None:
-        args.config = "mccnn" if args.mode == "volume8" else "kitti"
-    world_env = os.environ.get("WORLD_SIZE")
-    if world_env is None and args.gpus > 1:
-        sys.exit(launch_ranks(args.gpus))
-    world = int(world_env or "1")
-    if world != args.gpus:
-        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} (launch N ranks for --gpus N)")
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.selftest_cpu:
-        return selftest_cpu(args, world, rank)
+# the rank path: one process per GPU (or a gloo stand-in on CPU)
+# ---------------------------------------------------------------------------
+class GpuWorkload:
+    """The hot path on this rank's GPU: its block of synthetic pairs resident in
+    HBM, one ``step`` = one engine call over the block (census8: cost, E/W and
+    the two fused sweeps, LR check, median)."""
 
-    import torch
-    import torch.distributed as dist
+    backend = "nccl"
 
-    from stereo_match_amd import _lib, synthetic
-    from stereo_match_amd.batch import gather_to_root, shard_range
+    def __init__(self, args, local_rank):
+        import torch
 
-    if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    dev = torch.device("cuda", local_rank)
-    torch.cuda.set_device(dev)
+        from stereo_match_amd import _lib, synthetic
 
-    H, W, D = synthetic.CONFIGS[args.config]
-    volume = args.mode == "volume8"
-    full = args.mode == "disparity5"
-    bm = args.mode == "bm"
-    if args.mode == "census8":
-        p = synthetic.headline_params(D)
-    elif volume:
-        p = synthetic.cost_volume_params(D)
-    else:
-        p = synthetic.parity_params(D)
-        if args.mode == "sgbm8":  # OpenCV cost, 8 paths (MODE_HH)
-            p = dict(p, mode=8)
-    prm = synthetic.to_sm_params(p)
-    if bm:
-        prm = _lib.SmBmParams()
-        _lib.load().sm_bm_default_params(D, 21, prm)
-    gpairs = args.pairs_per_gpu * world
-    first, P = shard_range(gpairs, rank, world)
-
-    # synthetic inputs for this rank's block of pairs, resident in HBM before timing
-    lefts, rights = [], []
-    for i in range(first, first + P):
-        l, r, _ = synthetic.random_dot_pair(H, W, D, seed=1000 + i)
-        lefts.append(l)
-        rights.append(r)
-    dL = torch.tensor(np.stack(lefts), device=dev)
-    dR = torch.tensor(np.stack(rights), device=dev)
-    dOut = torch.empty((P, H, W), dtype=torch.int16, device=dev)
-    dOutR = dFilt = wprm = None
-    if full:  # compute_disparity: settings.ini lambda/sigma, createDisparityWLSFilter defaults
-        dOutR = torch.empty_like(dOut)
-        dFilt = torch.empty_like(dOut)
-        wprm = _lib.wls_default_params(prm)
-        wprm.lambda_, wprm.sigma_color = 80000.0, 1.2
-    vols = None
-    if volume:  # config C: (1, D, H, W) float32 cost per pair, resident in HBM
-        vols = torch.empty((P, D, H, W), dtype=torch.float32, device=dev)
-        for i in range(P):
-            vols[i].copy_(torch.from_numpy(synthetic.absdiff_volume(lefts[i], rights[i], D)[0]))
-
-    eng = _lib.Engine(local_rank)
-    stream = torch.cuda.current_stream(dev)
-    eng.set_stream(stream.cuda_stream)
-    flags = {"auto": 0, "perdir": 4096, "sweep": 16384}[args.engine]
-    if flags:
-        eng.set_debug_flags(flags)
-    gather = world > 1 and not args.no_gather
-    gather_events = []
-
-    def step(timed=False):
-        if full:
-            eng.compute_disparity_batch_device(dL.data_ptr(), dR.data_ptr(), P, H * W, H, W, W, prm, wprm,
-                                               dOut.data_ptr(), dOutR.data_ptr(), dFilt.data_ptr())
-        elif bm:
-            eng.bm_compute_batch_device(dL.data_ptr(), dR.data_ptr(), P, H * W, H, W, W, prm, dOut.data_ptr())
-        elif volume:
-            eng.aggregate_cost_f32_device(vols.data_ptr(), P, D * H * W, D, H, W, prm, 0.0, synthetic.VOLUME_SCALE,
-                                          dOut.data_ptr())
+        self.args, self.torch, self._lib, self.synthetic = args, torch, _lib, synthetic
+        self.dev = torch.device("cuda", local_rank)
+        torch.cuda.set_device(self.dev)
+        self.local_rank = local_rank
+        self.H, self.W, self.D = synthetic.CONFIGS[args.config]
+        self.volume = args.mode == "volume8"
+        self.full = args.mode == "disparity5"
+        self.bm = args.mode == "bm"
+        if args.mode == "census8":
+            p = synthetic.headline_params(self.D)
+        elif self.volume:
+            p = synthetic.cost_volume_params(self.D)
         else:
-            eng.compute_batch_device(dL.data_ptr(), dR.data_ptr(), P, H * W, H, W, W, prm, dOut.data_ptr())
-        if gather:
-            if timed:
-                e0 = torch.cuda.Event(enable_timing=True)
-                e0.record(stream)
-            gather_to_root(dOut, gpairs)
-            if timed:
-                e1 = torch.cuda.Event(enable_timing=True)
-                e1.record(stream)
-                gather_events.append((e0, e1))
+            p = synthetic.parity_params(self.D)
+            if args.mode == "sgbm8":  # OpenCV cost, 8 paths (MODE_HH)
+                p = dict(p, mode=8)
+        self.p = p
+        self.prm = synthetic.to_sm_params(p)
+        if self.bm:
+            self.prm = _lib.SmBmParams()
+            _lib.load().sm_bm_default_params(self.D, 21, self.prm)
 
-    # untimed warmup; its second half (at least one step) with every stage timed: the
-    # per-stage profile (stage_us_per_pair) and the choice of the dominant kernel come from
-    # it (the first steps allocate the engine's buffers)
-    n_prof = max(1, args.warmup // 2)
-    for _ in range(args.warmup - n_prof):
-        step()
-    eng.synchronize()
-    eng.set_timing(True)
-    eng.reset_timing()
-    for _ in range(n_prof):
-        step()
-    eng.synchronize()  # device-side failures (sweep hand-off timeouts) fail the run here
-    torch.cuda.synchronize(dev)
-    profile = eng.timing()
-    sweep = profile["sweep_wta"][1] > 0  # fused-sweep engine ran (its stages have launches)
-    P_dirs = 5 if args.mode in ("sgbm5", "disparity5") else 8
-    kern, cands = design_kernels(args, profile, H, W, D, p, P_dirs, sweep, bm)
-    dom = max(cands, key=lambda k: profile[k][0])  # dominant kernel = the stage with the largest device time
-    # timed region: only the dominant kernel's stage records events (every timed stage
-    # delays the stream, about 12 us per KITTI pair with all of them: include/stereo_match_amd.h)
-    eng.set_timing(True, stages=[dom])
-    eng.reset_timing()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(timed=True)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    eng.synchronize()
-    elapsed = t1 - t0
-    stages = eng.timing()
-    eng.set_timing(False)
-    gather_ms = sum(a.elapsed_time(b) for a, b in gather_events)
-    if world > 1:
-        t = torch.tensor([elapsed, gather_ms], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, gather_ms_max = float(t[0].item()), float(t[1].item())
-    else:
-        gather_ms_max = 0.0
+    def init_dist(self):
+        import torch.distributed as dist
 
-    # correctness spot check of the last step (cheap, outside the timed region)
-    out0 = dOut[0].cpu().numpy()
-    valid_frac = float((out0 >= 0).mean())
+        dist.init_process_group("nccl", device_id=self.dev)
 
-    if rank == 0:
-        K = args.steps
-        value = gpairs * K / elapsed
+    def setup(self, first, P):
+        torch, synthetic, _lib = self.torch, self.synthetic, self._lib
+        H, W, D, dev = self.H, self.W, self.D, self.dev
+        self.P = P
+        # synthetic inputs for this rank's block of pairs, resident in HBM before timing
+        self.lefts, self.rights = [], []
+        for i in range(first, first + P):
+            l, r, _ = synthetic.random_dot_pair(H, W, D, seed=1000 + i)
+            self.lefts.append(l)
+            self.rights.append(r)
+        self.dL = torch.tensor(np.stack(self.lefts), device=dev)
+        self.dR = torch.tensor(np.stack(self.rights), device=dev)
+        self.out = torch.empty((P, H, W), dtype=torch.int16, device=dev)
+        self.dOutR = self.dFilt = self.wprm = None
+        if self.full:  # compute_disparity: settings.ini lambda/sigma, createDisparityWLSFilter defaults
+            self.dOutR = torch.empty_like(self.out)
+            self.dFilt = torch.empty_like(self.out)
+            self.wprm = _lib.wls_default_params(self.prm)
+            self.wprm.lambda_, self.wprm.sigma_color = 80000.0, 1.2
+        self.vols = None
+        if self.volume:  # config C: (1, D, H, W) float32 cost per pair, resident in HBM
+            self.vols = torch.empty((P, D, H, W), dtype=torch.float32, device=dev)
+            for i in range(P):
+                self.vols[i].copy_(torch.from_numpy(synthetic.absdiff_volume(self.lefts[i], self.rights[i], D)[0]))
+        self.eng = _lib.Engine(self.local_rank)
+        self.stream = torch.cuda.current_stream(dev)
+        self.eng.set_stream(self.stream.cuda_stream)
+        flags = {"auto": 0, "perdir": 4096, "sweep": 16384}[self.args.engine]
+        if flags:
+            self.eng.set_debug_flags(flags)
+
+    def step(self):
+        e, P, H, W, prm = self.eng, self.P, self.H, self.W, self.prm
+        if self.full:
+            e.compute_disparity_batch_device(self.dL.data_ptr(), self.dR.data_ptr(), P, H * W, H, W, W, prm, self.wprm,
+                                             self.out.data_ptr(), self.dOutR.data_ptr(), self.dFilt.data_ptr())
+        elif self.bm:
+            e.bm_compute_batch_device(self.dL.data_ptr(), self.dR.data_ptr(), P, H * W, H, W, W, prm,
+                                      self.out.data_ptr())
+        elif self.volume:
+            e.aggregate_cost_f32_device(self.vols.data_ptr(), P, self.D * H * W, self.D, H, W, prm, 0.0,
+                                        self.synthetic.VOLUME_SCALE, self.out.data_ptr())
+        else:
+            e.compute_batch_device(self.dL.data_ptr(), self.dR.data_ptr(), P, H * W, H, W, W, prm,
+                                   self.out.data_ptr())
+
+    def sync(self):
+        self.torch.cuda.synchronize(self.dev)
+
+    def marker(self):
+        ev = self.torch.cuda.Event(enable_timing=True)
+        ev.record(self.stream)
+        return ev
+
+    @staticmethod
+    def span_ms(a, b):
+        return a.elapsed_time(b)
+
+    def reduce_tensor(self, vals):
+        return self.torch.tensor(vals, device=self.dev, dtype=self.torch.float64)
+
+    # untimed warmup; its second half (at least one step) with every stage timed: the per-stage
+    # profile (stage_us_per_pair) and the choice of the dominant kernel come from it (the first
+    # steps allocate the engine's buffers)
+    def profile_begin(self):
+        self.eng.synchronize()
+        self.eng.set_timing(True)
+        self.eng.reset_timing()
+
+    def profile_end(self, n_prof):
+        self.eng.synchronize()  # device-side failures (sweep hand-off timeouts) fail the run here
+        self.sync()
+        self.n_prof = n_prof
+        self.profile = self.eng.timing()
+        args = self.args
+        self.sweep = self.profile["sweep_wta"][1] > 0  # fused-sweep engine ran (its stages have launches)
+        self.P_dirs = 5 if args.mode in ("sgbm5", "disparity5") else 8
+        self.kern, cands = design_kernels(args, self.profile, self.H, self.W, self.D, self.p, self.P_dirs, self.sweep,
+                                          self.bm)
+        self.dom = max(cands, key=lambda k: self.profile[k][0])  # the stage with the largest device time
+
+    def timed_begin(self):
+        # timed region: only the dominant kernel's stage records events (every timed stage
+        # delays the stream, about 12 us per KITTI pair with all of them: include/stereo_match_amd.h)
+        self.eng.set_timing(True, stages=[self.dom])
+        self.eng.reset_timing()
+
+    def timed_end(self):
+        self.eng.synchronize()
+        self.stages = self.eng.timing()
+        self.eng.set_timing(False)
+
+    def report(self, elapsed, K, gpairs, world):
+        """The bench line's workload-specific fields (rank 0)."""
+        args, H, W, D, P = self.args, self.H, self.W, self.D, self.P
+        out0 = self.out[0].cpu().numpy()
         cells = H * W * D
-        dom_ms, dom_launches, dom_pairs = stages[dom]
+        dom, kern, sweep, P_dirs = self.dom, self.kern, self.sweep, self.P_dirs
+        dom_ms, dom_launches, dom_pairs = self.stages[dom]
         launch_s = dom_ms / 1e3 / max(dom_launches, 1)
         pairs_per_launch = dom_pairs / max(dom_launches, 1)
         alg_bytes = model_stage_bytes(dom, args.mode, H, W, D, P_dirs, sweep) * pairs_per_launch
         design_bytes = kern[dom][1] * pairs_per_launch
         achieved = alg_bytes / launch_s / 1e9 if launch_s > 0 else None
         traffic, traffic_note = read_traffic(args, dom, kern[dom][0], pairs_per_launch, sweep)
-        survey_bytes = model_pair_bytes(args.mode, H, W, D, P_dirs) * (2 if full else 1)
+        valu = read_valu(args, dom, pairs_per_launch, sweep, launch_s, H, W, D)
+        survey_bytes = model_pair_bytes(args.mode, H, W, D, P_dirs) * (2 if self.full else 1)
         # this rank's wall time per pair over the timed region (every call's device work and
         # the gaps between its kernels; per reference pair in disparity5: 2 matchers + WLS)
         pair_s = elapsed / max(K * P, 1)
         line = {
-            "metric": METRIC,
-            "value": value,
-            "unit": "pairs/s",
-            "n_gpus": world,
-            "steps": K,
-            "warmup": args.warmup,
-            "ms_per_step": elapsed / K * 1e3,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
             "dtype": {"census8": "u8", "sgbm5": "i16", "sgbm8": "i16", "volume8": "f32->u16", "disparity5": "i16+f32",
                       "bm": "i32"}[args.mode],
             "data": "synthetic random-dot pairs (no dataset in the image)"
-                    + ("; f32 cost = 3x3-smoothed |L-R|/255 volume per pair" if volume else ""),
+                    + ("; f32 cost = 3x3-smoothed |L-R|/255 volume per pair" if self.volume else ""),
             "config": {
                 "engine": "fused sweeps" if sweep else "per-direction",
                 "workload": f"{args.config} {W}x{H} D={D} "
@@ -340,10 +338,8 @@ def main():
                                "volume8": "f32 cost volume (mc-cnn) + 8-path SGM",
                                "disparity5": "compute_disparity: left+right OpenCV-SGBM 5-path + WLS",
                                "bm": "OpenCV StereoBM blockSize 21 (X-Sobel prefilter)"}[args.mode],
-                "pairs_per_gpu": args.pairs_per_gpu, "global_batch": gpairs, "H": H, "W": W, "D": D,
-                "gather": gather, "parallelism": f"pairs/dp{world}",
             },
-            "mpix_disp_per_s": value * cells / 1e6,
+            "mpix_disp_per_s": gpairs * K / elapsed * cells / 1e6,
             "roofline": {
                 "kernel": kern[dom][0],
                 "bound": "hbm",
@@ -358,37 +354,211 @@ def main():
                 "design_achieved_GBs": design_bytes / launch_s / 1e9 if launch_s > 0 else None,
                 "traffic_over_alg": (traffic / alg_bytes) if traffic and alg_bytes else None,
                 "traffic_note": traffic_note,
+                "valu": valu,
                 "pairs_per_launch": pairs_per_launch,
                 "avg_launch_us": launch_s * 1e6,
             },
             "pipeline_roofline": {
-                "model": "SURVEY §8d " + ("H·W·D·(4P+8)" if volume else "H·W·(2+4+2+4) (no volume)" if bm
+                "model": "SURVEY §8d " + ("H·W·D·(4P+8)" if self.volume else "H·W·(2+4+2+4) (no volume)" if self.bm
                                           else "H·W·D·(1+P+4)+I/O")
-                         + (" x2 matchers" if full else "") + " per pair",
+                         + (" x2 matchers" if self.full else "") + " per pair",
                 "bytes_per_pair": survey_bytes,
                 "wall_us_per_pair": pair_s * 1e6,
                 "achieved_GBs": survey_bytes / pair_s / 1e9 if pair_s > 0 else None,
                 "frac": survey_bytes / pair_s / 1e9 / HBM_PEAK_GBS if pair_s > 0 else None,
             },
-            "stage_us_per_pair": {k: v[0] * 1e3 / max(v[2], 1) for k, v in profile.items()},
-            "stage_profile": f"last {n_prof} warmup steps, every stage timed; the timed region times only "
+            "stage_us_per_pair": {k: v[0] * 1e3 / max(v[2], 1) for k, v in self.profile.items()},
+            "stage_profile": f"last {self.n_prof} warmup steps, every stage timed; the timed region times only "
                              f"the dominant kernel's stage",
-            "valid_frac_pair0": valid_frac,
+            "valid_frac_pair0": float((out0 >= 0).mean()),
         }
-        if world > 1:
+        hs_pair = None
+        if world == 1 and args.host_surface_calls > 0 and args.config == "kitti":
+            line["host_surface"], hs_pair = host_surface(args, self.local_rank)
+        if world == 1 and args.cpu_baseline_pairs > 0:
+            line["cpu_baseline"] = cpu_baseline(args, H, W, D, self.p, self.lefts, self.rights, out0, self.volume,
+                                                self.full, hs_pair)
+        return line
+
+
+class StandInWorkload:
+    """CPU stand-in for ``GpuWorkload`` (--selftest-cpu): the same rank path over
+    gloo; the step widens the left images to int16 x16 (no disparity computed),
+    so the gathered maps are known per pair index.  Not a measurement."""
+
+    backend = "gloo"
+
+    def __init__(self, args, local_rank):
+        import torch
+
+        from stereo_match_amd import synthetic
+
+        self.torch, self.args = torch, args
+        self.H, self.W, self.D = synthetic.CONFIGS[args.config]
+
+    def init_dist(self):
+        import torch.distributed as dist
+
+        dist.init_process_group("gloo")
+
+    def setup(self, first, P):
+        torch = self.torch
+        self.P = P
+        self.dL = torch.stack([torch.full((self.H, self.W), i % 251, dtype=torch.uint8)
+                               for i in range(first, first + P)]) if P else \
+            torch.empty((0, self.H, self.W), dtype=torch.uint8)
+        self.out = torch.empty((P, self.H, self.W), dtype=torch.int16)
+
+    def expected(self, gpairs):
+        torch = self.torch
+        return torch.stack([torch.full((self.H, self.W), (i % 251) * 16, dtype=torch.int16) for i in range(gpairs)])
+
+    def step(self):
+        self.out.copy_(self.dL.to(self.torch.int16) * 16)
+
+    def sync(self):
+        pass
+
+    def marker(self):
+        return time.perf_counter()
+
+    @staticmethod
+    def span_ms(a, b):
+        return (b - a) * 1e3
+
+    def reduce_tensor(self, vals):
+        return self.torch.tensor(vals, dtype=self.torch.float64)
+
+    def profile_begin(self):
+        pass
+
+    def profile_end(self, n_prof):
+        pass
+
+    def timed_begin(self):
+        pass
+
+    def timed_end(self):
+        pass
+
+    def report(self, elapsed, K, gpairs, world):
+        return {"value": None, "dtype": None,
+                "data": "rank-path self-test: gloo on CPU, stand-in step (no disparity computed, not a measurement)",
+                "config": {"engine": "stand-in"}}
+
+
+def main():
+    args = parse()
+    if args.config is None:
+        args.config = "mccnn" if args.mode == "volume8" else "kitti"
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    world = int(world_env or "1")
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} (launch N ranks for --gpus N)")
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    wl = (StandInWorkload if args.selftest_cpu else GpuWorkload)(args, local_rank)
+    run_rank(args, wl, world, rank)
+
+
+def run_rank(args, wl, world, rank):
+    """One rank: shard, warm up, time K steps between barriers + device syncs,
+    max over ranks, gather to rank 0, print the JSON line on rank 0.  The same
+    code for the GPU workload and the CPU stand-in (--selftest-cpu)."""
+    import torch
+    import torch.distributed as dist
+
+    from stereo_match_amd.batch import gather_to_root, shard_range
+
+    dist_on = world > 1 or args.dist
+    if dist_on:
+        if world == 1 and "MASTER_ADDR" not in os.environ:  # --dist without a launcher: a one-rank group
+            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0", WORLD_SIZE="1")
+        wl.init_dist()
+    gpairs = args.pairs_per_gpu * world
+    first, P = shard_range(gpairs, rank, world)
+    wl.setup(first, P)
+    gather = dist_on and not args.no_gather
+    gather_marks = []
+
+    def step(timed=False):
+        wl.step()
+        if gather:
+            a = wl.marker() if timed else None
+            gather_to_root(wl.out, gpairs)
+            if timed:
+                gather_marks.append((a, wl.marker()))
+
+    n_prof = max(1, args.warmup // 2)
+    for _ in range(args.warmup - n_prof):
+        step()
+    wl.profile_begin()
+    for _ in range(n_prof):
+        step()
+    wl.profile_end(n_prof)
+    wl.timed_begin()
+    if dist_on:
+        dist.barrier()
+    wl.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(timed=True)
+    wl.sync()
+    if dist_on:
+        dist.barrier()
+    t1 = time.perf_counter()
+    wl.timed_end()
+    elapsed = t1 - t0
+    gather_ms = sum(wl.span_ms(a, b) for a, b in gather_marks)
+    gather_ms_max = gather_ms
+    if dist_on:
+        t = wl.reduce_tensor([elapsed, gather_ms])
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, gather_ms_max = float(t[0].item()), float(t[1].item())
+    gather_check = None
+    if gather:  # untimed: gather once more and check the maps arrived in pair order
+        gathered = gather_to_root(wl.out, gpairs)
+        # per-pair checksums (int64 -> 4 int16 words) travel the same way, so rank 0 can check
+        # every rank's block, not only its own
+        sums = wl.out.reshape(P, -1).to(torch.int64).sum(1).contiguous()
+        gsums = gather_to_root(sums.view(torch.int16).view(P, 1, 4), gpairs)
+        if rank == 0:
+            want = gathered.reshape(gpairs, -1).to(torch.int64).sum(1)
+            gather_check = bool(torch.equal(gsums.reshape(gpairs, 4).contiguous().view(torch.int64).reshape(-1), want)
+                                and torch.equal(gathered[first:first + P], wl.out))
+            if isinstance(wl, StandInWorkload):
+                gather_check = gather_check and bool(torch.equal(gathered, wl.expected(gpairs)))
+    if rank == 0:
+        K = args.steps
+        line = {
+            "metric": metric_for(args.config),
+            "value": gpairs * K / elapsed,
+            "unit": "pairs/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / K * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+        }
+        extra = wl.report(elapsed, K, gpairs, world)
+        cfg = extra.pop("config", {})
+        line.update(extra)
+        line["config"] = dict(cfg, pairs_per_gpu=args.pairs_per_gpu, global_batch=gpairs, H=wl.H, W=wl.W, D=wl.D,
+                              gather=gather, parallelism=f"pairs/dp{world}")
+        if dist_on:
             line["distributed"] = {
                 "backend": dist.get_backend(), "world_size": dist.get_world_size(),
                 "gather_ms_per_step_rank0": gather_ms / K, "gather_ms_per_step_max": gather_ms_max / K,
-                "gather_bytes_to_root": gpairs * H * W * 2,
+                "gather_bytes_to_root": gpairs * wl.H * wl.W * 2 if gather else 0,
+                "gathered_in_pair_order": gather_check,
                 "compute_ms_per_step": (elapsed * 1e3 - gather_ms) / K,
             }
-        hs_pair = None
-        if world == 1 and args.host_surface_calls > 0 and args.config == "kitti":
-            line["host_surface"], hs_pair = host_surface(args, local_rank)
-        if world == 1 and args.cpu_baseline_pairs > 0:
-            line["cpu_baseline"] = cpu_baseline(args, H, W, D, p, lefts, rights, out0, volume, full, hs_pair)
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 
@@ -436,6 +606,45 @@ def read_traffic(args, dom, kernel_label, pairs_per_launch, sweep):
     if not st:
         return None, f"traffic file has no stage {dom!r}"
     return st.get("hbm_bytes_per_launch"), f"PMC FETCH_SIZE/WRITE_SIZE, {os.path.relpath(args.traffic_file, ROOT)}"
+
+
+def read_valu(args, dom, pairs_per_launch, sweep, launch_s, H, W, D, path=None):
+    """VALU issue of the dominant kernel from the SQ-counter summary
+    (tools/valu.sh -> profiles/valu_latest.json), used only when it was collected
+    on the same sources, configuration, mode, engine and launch size as this run.
+    ``frac`` = SQ_INSTS_VALU x 4 cycles / (1024 SIMDs x the profiled launch's
+    cycles); ``frac_live`` divides by this run's launch time at 2.4 GHz."""
+    path = path or os.path.join(ROOT, "profiles", "valu_latest.json")
+    if not os.path.exists(path):
+        return {"note": "no VALU counter file"}
+    try:
+        with open(path) as f:
+            vs = json.load(f)
+    except (OSError, ValueError):
+        return {"note": "unreadable VALU counter file"}
+    want = {"config": args.config, "mode": args.mode, "engine": "sweep" if sweep else "perdir",
+            "src_sha16": source_hash(), "pairs_per_launch": pairs_per_launch}
+    for k, v in want.items():
+        if vs.get(k) != v:
+            return {"note": f"VALU file {os.path.relpath(path, ROOT)} is for {k}={vs.get(k)!r}, this run has {v!r}: "
+                            f"dropped"}
+    st = vs.get("stages", {}).get(dom)
+    if not st:
+        return {"note": f"VALU file has no stage {dom!r}"}
+    insts = st["sq_insts_valu"]
+    cyc = vs["issue_cycles_per_instr"]
+    cells = H * (W - D) * D * pairs_per_launch  # minDisparity 0: width1 = W - D
+    return {
+        "bound": "valu",
+        "insts_per_launch": insts,
+        "issue_cycles_per_instr": cyc,
+        "frac": st.get("valu_issue_frac"),
+        "frac_live": insts * cyc / (vs["simds"] * launch_s * 2.4e9) if launch_s > 0 else None,
+        "wave_insts_per_cell": insts / cells,
+        "lane_ops_per_cell": insts * 64 / cells,
+        "wait_any_frac": st.get("wait_any_frac"),
+        "note": f"SQ_INSTS_VALU, {os.path.relpath(path, ROOT)} (tools/valu.sh)",
+    }
 
 
 def host_surface(args, device):
@@ -493,10 +702,15 @@ def host_surface(args, device):
         "value": 1.0 / med, "unit": "pairs/s", "ms_per_call_median": med * 1e3,
         "ms_per_call_mean": float(np.mean(ts)) * 1e3,
         "h2d_ms_per_call": st["h2d"][0] / n, "d2h_ms_per_call": st["d2h"][0] / n,
+        # the Python surface makes three synchronous calls (left, right, WLS), so their device
+        # spans add up; the one-call ABI below runs the matchers concurrently and reports the
+        # call's own span on the caller's stream (SM_STAGE_CALL)
         "device_ms_per_call": (st["total"][0] + st["wls"][0]) / n,
+        "wls_ms_per_call": st["wls"][0] / n,
         "one_call_abi": {"entry": "sm_compute_disparity", "value": 1.0 / med1, "ms_per_call_median": med1 * 1e3,
                          "h2d_ms_per_call": st1["h2d"][0] / n, "d2h_ms_per_call": st1["d2h"][0] / n,
-                         "device_ms_per_call": (st1["total"][0] + st1["wls"][0]) / n,
+                         "device_ms_per_call": st1["call"][0] / n,
+                         "wls_ms_per_call": st1["wls"][0] / n,
                          "same_as_python_surface": bool(np.array_equal(d1, displ) and np.array_equal(f1, filt))},
     }, (gl, gr, s, displ, filt)
 
@@ -611,52 +825,6 @@ def _wls_oracle_params(p, D):
     """createDisparityWLSFilter(left) defaults for the numpy WLS restatement."""
     return dict(lmbda=80000.0, sigma=1.2, radius=(p["blockSize"] + 1) // 2, min_disp=p["minDisparity"],
                 left_offset=max(0, p["minDisparity"] + D), right_offset=max(0, -p["minDisparity"]))
-
-
-# ---------------------------------------------------------------------------
-def selftest_cpu(args, world, rank):
-    """The multi-rank plumbing of ``main`` on CPU (gloo): same sharding, same
-    gather, same max-over-ranks timing and JSON keys; the step is a stand-in
-    (left image widened to int16), so nothing here is a measurement."""
-    import torch
-    import torch.distributed as dist
-
-    from stereo_match_amd import synthetic
-    from stereo_match_amd.batch import gather_to_root, shard_range
-
-    if world > 1:
-        dist.init_process_group("gloo")
-    H, W, D = synthetic.CONFIGS[args.config]
-    gpairs = args.pairs_per_gpu * world
-    first, P = shard_range(gpairs, rank, world)
-    dL = torch.stack([torch.full((H, W), i % 251, dtype=torch.uint8) for i in range(first, first + P)])
-    gathered = None
-    gather_s = 0.0
-    for k in range(args.warmup + args.steps):
-        out = dL.to(torch.int16) * 16
-        if world > 1 and not args.no_gather:
-            tg = time.perf_counter()
-            gathered = gather_to_root(out, gpairs)
-            if k >= args.warmup:
-                gather_s += time.perf_counter() - tg
-    if world > 1:
-        dist.barrier()
-    ok = True
-    if rank == 0 and gathered is not None:
-        want = torch.stack([torch.full((H, W), (i % 251) * 16, dtype=torch.int16) for i in range(gpairs)])
-        ok = bool(torch.equal(gathered, want))
-    if rank == 0:
-        print(json.dumps({"metric": METRIC, "value": None, "unit": "pairs/s", "n_gpus": world,
-                          "steps": args.steps, "warmup": args.warmup, "higher_is_better": True, "scaling": "weak",
-                          "data": "launcher self-test: gloo on CPU, stand-in step (no disparity computed)",
-                          "config": {"workload": args.config, "pairs_per_gpu": args.pairs_per_gpu,
-                                     "global_batch": gpairs, "parallelism": f"pairs/dp{world}"},
-                          "distributed": {"backend": dist.get_backend() if world > 1 else None,
-                                          "world_size": dist.get_world_size() if world > 1 else 1,
-                                          "gather_ms_per_step_rank0": gather_s * 1e3 / max(args.steps, 1),
-                                          "gathered_in_pair_order": ok}}), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -70,9 +70,13 @@ int sm_reset_stream(sm_ctx* ctx);
 /* StereoSGBM::compute(left, right) on host buffers (uint8, row stride in
  * bytes >= W).  disp_out: int16[H*W], disparity x16, invalid = (minD-1)*16.
  * Replaces stereo_vision/stereo_vision.py:178 (and :179 with the right
- * matcher's params, see sm_right_matcher_params). */
+ * matcher's params, see sm_right_matcher_params).
+ * wta_out (nullable): int16[H*W] raw integer WTA index, i.e. OpenCV's
+ * bestDisp in [0, numDisparities) for pixels in [minX1, maxX1) that pass the
+ * uniqueness test (and whose aggregated cost is not saturated), -1 elsewhere;
+ * taken before the sub-pixel step, the disp12MaxDiff check and the median. */
 int sm_compute(sm_ctx* ctx, const uint8_t* left, const uint8_t* right, int H, int W, int stride,
-               const sm_params* p, int16_t* disp_out);
+               const sm_params* p, int16_t* disp_out, int16_t* wta_out);
 
 /* Same on device pointers already resident in HBM; enqueued on the context
  * stream, returns before completion. */
@@ -87,6 +91,12 @@ int sm_compute_device(sm_ctx* ctx, const uint8_t* d_left, const uint8_t* d_right
 int sm_compute_batch_device(sm_ctx* ctx, const uint8_t* d_left, const uint8_t* d_right, int npairs,
                             size_t pair_stride_bytes, int H, int W, int stride, const sm_params* p,
                             int16_t* d_disp_out);
+
+/* sm_compute_batch_device plus the integer WTA index of every pair (as sm_compute's
+ * wta_out) at d_wta_out + i*H*W (int16; may be NULL).  Gray images. */
+int sm_compute_wta_batch_device(sm_ctx* ctx, const uint8_t* d_left, const uint8_t* d_right, int npairs,
+                                size_t pair_stride_bytes, int H, int W, int stride, const sm_params* p,
+                                int16_t* d_disp_out, int16_t* d_wta_out);
 
 /* The same two entry points for cn-channel images (OpenCV's StereoSGBM takes
  * gray or BGR; the reference's try_try.py:56-57,81 passes cv2.imread BGR
@@ -269,7 +279,11 @@ int sm_set_cu_mask(sm_ctx* ctx, const uint32_t* mask, int nwords);
 /* guarded per-direction recomputation after the fused sweeps (near zero unless a
  * sweep strip gave up waiting for its neighbours; see sm_get_counters) */
 #define SM_STAGE_FALLBACK 12
-#define SM_NUM_STAGES 13
+/* one whole compute_disparity call (sm_compute_disparity[_batch_device]): fork of the
+ * right matcher, both matchers, join, WLS, on the caller's stream; the two matchers
+ * run concurrently, so this (not the sum of their stages) is the call's device time */
+#define SM_STAGE_CALL 13
+#define SM_NUM_STAGES 14
 /* enable: 0 off, 1 every stage, SM_TIMING_ONLY | (1 << stage) | ... only those
  * stages.  Every timed stage records two hipEvents per launch on its stream,
  * which delays the stream (KITTI census8, 8 pairs per call: every stage timed

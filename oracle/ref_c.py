@@ -38,6 +38,10 @@ def load():
         lib.sgm_ref_compute.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                         ctypes.c_int, ctypes.POINTER(SgmRefParams), ctypes.c_void_p,
                                         ctypes.c_int]
+        lib.sgm_ref_compute_wta.restype = ctypes.c_int
+        lib.sgm_ref_compute_wta.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                            ctypes.c_int, ctypes.POINTER(SgmRefParams), ctypes.c_void_p,
+                                            ctypes.c_void_p, ctypes.c_int]
         lib.sgm_ref_compute_cn.restype = ctypes.c_int
         lib.sgm_ref_compute_cn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                            ctypes.c_int, ctypes.c_int, ctypes.POINTER(SgmRefParams),
@@ -82,6 +86,26 @@ def compute(left: np.ndarray, right: np.ndarray, params: dict, median: bool = Tr
     if rc != 0:
         raise ValueError(f"sgm_ref_compute failed ({rc})")
     return out
+
+
+def compute_wta(left: np.ndarray, right: np.ndarray, params: dict, median: bool = True):
+    """(disparity int16 [H, W], integer WTA index int16 [H, W]) of a gray pair: the index is
+    OpenCV's bestDisp in [0, D) where the pixel passes the uniqueness test, -1 elsewhere
+    (before the sub-pixel step, the disp12MaxDiff check and the median)."""
+    lib = load()
+    left = np.ascontiguousarray(left, np.uint8)
+    right = np.ascontiguousarray(right, np.uint8)
+    if left.shape != right.shape or left.ndim != 2:
+        raise ValueError("left/right must be same-size uint8 [H, W]")
+    H, W = left.shape
+    out = np.empty((H, W), np.int16)
+    wta = np.empty((H, W), np.int16)
+    prm = make_params(params)
+    rc = lib.sgm_ref_compute_wta(left.ctypes.data, right.ctypes.data, H, W, W, ctypes.byref(prm), out.ctypes.data,
+                                 wta.ctypes.data, int(bool(median)))
+    if rc != 0:
+        raise ValueError(f"sgm_ref_compute_wta failed ({rc})")
+    return out, wta
 
 
 def cost_volume(left: np.ndarray, right: np.ndarray, params: dict) -> np.ndarray:

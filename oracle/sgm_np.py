@@ -418,6 +418,25 @@ def wta(S: np.ndarray, H, W, prm):
     return disp.astype(np.int16)
 
 
+def wta_index(S: np.ndarray, H, W, prm) -> np.ndarray:
+    """The integer WTA index (int16 [H, W]): bestDisp in [0, D) where the pixel passes
+    the uniqueness test and S is not saturated (App. A.6), -1 elsewhere and outside
+    [minX1, maxX1); before the sub-pixel step, the disp12MaxDiff check and the median.
+    The quantity BASELINE.json's north_star states its bit-exact bar on."""
+    minD, D = prm["minD"], prm["D"]
+    minX1, maxX1 = geometry(W, minD, D)
+    out = np.full((H, W), -1, np.int64)
+    if maxX1 <= minX1:
+        return out.astype(np.int16)
+    u = prm["uniq"]
+    best = wta_best(S, prm["mode"])
+    minS = S.min(-1)
+    bad = ((S * (100 - u) < (minS * 100)[..., None])
+           & (np.abs(best[..., None] - np.arange(D)) > 1)).any(-1)
+    out[:, minX1:maxX1] = np.where(~bad & (minS < MAX_COST), best, -1)
+    return out.astype(np.int16)
+
+
 def median3(disp: np.ndarray) -> np.ndarray:
     """cv::medianBlur(ksize=3) on int16 with replicate border."""
     H, W = disp.shape
@@ -461,7 +480,7 @@ def compute(left: np.ndarray, right: np.ndarray, params: dict, *, median=True,
         out = filter_speckles(out, (prm["minD"] - 1) * DISP_SCALE, prm["speckle_ws"],
                               DISP_SCALE * prm["speckle_range"])
     if return_stages:
-        return out, dict(C=C, S=S, raw=raw)
+        return out, dict(C=C, S=S, raw=raw, wta=wta_index(S, H, W, prm))
     return out
 
 

@@ -228,7 +228,7 @@ static inline int l_step(const CostType* Lp, int d, int P1, int delta, int Cpd)
 
 static int compute_core(const uint8_t* img1, const uint8_t* img2, int H, int W, int stride, int cn,
                         const float* vol, float vol_offset, float vol_scale, const sgm_ref_params* prm,
-                        int16_t* disp1, int apply_median, int16_t* dumpC)
+                        int16_t* disp1, int apply_median, int16_t* dumpC, int16_t* wta)
 {
     if ((!vol && (!img1 || !img2 || (cn != 1 && cn != 3) || stride < W * cn)) || !disp1 || !prm || H <= 0 ||
         W <= 0)
@@ -254,6 +254,8 @@ static int compute_core(const uint8_t* img1, const uint8_t* img2, int H, int W, 
 
     int16_t* out = apply_median ? (int16_t*)malloc(sizeof(int16_t) * (size_t)H * W) : disp1;
     for (size_t i = 0; i < (size_t)H * W; i++) out[i] = (int16_t)INVALID;
+    if (wta)
+        for (size_t i = 0; i < (size_t)H * W; i++) wta[i] = -1;
     if (minX1 >= maxX1) goto done;
 
     {
@@ -450,6 +452,7 @@ static int compute_core(const uint8_t* img1, const uint8_t* img2, int H, int W, 
                         if (d < D) continue;
                         d = bestDisp;
                         if (d < 0) continue; /* all S saturated: OpenCV leaves the pixel invalid */
+                        if (wta) wta[(size_t)y * W + x + minX1] = (int16_t)d; /* the integer WTA index */
                         int _x2 = x + minX1 - d - minD;
                         if (disp2cost[_x2] > minS) {
                             disp2cost[_x2] = (CostType)minS;
@@ -498,21 +501,30 @@ done:
 int sgm_ref_compute(const uint8_t* img1, const uint8_t* img2, int H, int W, int stride,
                     const sgm_ref_params* prm, int16_t* disp1, int apply_median)
 {
-    return compute_core(img1, img2, H, W, stride, 1, NULL, 0.f, 1.f, prm, disp1, apply_median, NULL);
+    return compute_core(img1, img2, H, W, stride, 1, NULL, 0.f, 1.f, prm, disp1, apply_median, NULL, NULL);
+}
+
+/* as sgm_ref_compute, plus the integer WTA index wta[H][W] (bestDisp in [0, D) of pixels
+ * that pass the uniqueness test and are not saturated, -1 elsewhere; before the sub-pixel
+ * step, the disp12MaxDiff check and the median) */
+int sgm_ref_compute_wta(const uint8_t* img1, const uint8_t* img2, int H, int W, int stride,
+                        const sgm_ref_params* prm, int16_t* disp1, int16_t* wta, int apply_median)
+{
+    return compute_core(img1, img2, H, W, stride, 1, NULL, 0.f, 1.f, prm, disp1, apply_median, NULL, wta);
 }
 
 /* cn-channel input (1 gray, 3 BGR interleaved), stride in bytes */
 int sgm_ref_compute_cn(const uint8_t* img1, const uint8_t* img2, int H, int W, int stride, int cn,
                        const sgm_ref_params* prm, int16_t* disp1, int apply_median)
 {
-    return compute_core(img1, img2, H, W, stride, cn, NULL, 0.f, 1.f, prm, disp1, apply_median, NULL);
+    return compute_core(img1, img2, H, W, stride, cn, NULL, 0.f, 1.f, prm, disp1, apply_median, NULL, NULL);
 }
 
 /* the cost volume C[H][width1][D] as OpenCV holds it for each row (int16, P2 seed included) */
 int sgm_ref_cost_volume_cn(const uint8_t* img1, const uint8_t* img2, int H, int W, int stride, int cn,
                            const sgm_ref_params* prm, int16_t* C, int16_t* disp1)
 {
-    return compute_core(img1, img2, H, W, stride, cn, NULL, 0.f, 1.f, prm, disp1, 0, C);
+    return compute_core(img1, img2, H, W, stride, cn, NULL, 0.f, 1.f, prm, disp1, 0, C, NULL);
 }
 
 /* SGM over an external d-major float32 cost volume vol[D][H][W] (mc-cnn). */
@@ -520,5 +532,5 @@ int sgm_ref_compute_volume(const float* vol, int H, int W, const sgm_ref_params*
                            int16_t* disp1, int apply_median)
 {
     if (!vol) return -1;
-    return compute_core(NULL, NULL, H, W, W, 1, vol, offset, scale, prm, disp1, apply_median, NULL);
+    return compute_core(NULL, NULL, H, W, W, 1, vol, offset, scale, prm, disp1, apply_median, NULL, NULL);
 }

@@ -23,7 +23,7 @@ SM_COST_SGBM, SM_COST_CENSUS, SM_COST_VOLUME = 0, 1, 2
 SM_MODE_SGBM, SM_MODE_HH = 5, 8
 TIMING_ONLY = 0x40000000  # include/stereo_match_amd.h SM_TIMING_ONLY
 STAGES = ("cost", "paths", "wta", "median", "total", "wls", "speckle", "horizontal", "sweep", "sweep_wta", "h2d",
-          "d2h", "fallback")
+          "d2h", "fallback", "call")
 
 
 class SmParams(ctypes.Structure):
@@ -68,7 +68,10 @@ _SIGS = {
     "sm_set_stream": (_c.c_int, [_c.c_void_p, _c.c_void_p]),
     "sm_reset_stream": (_c.c_int, [_c.c_void_p]),
     "sm_compute": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_int, _c.c_int, _c.c_int,
-                              _c.POINTER(SmParams), _c.c_void_p]),
+                              _c.POINTER(SmParams), _c.c_void_p, _c.c_void_p]),
+    "sm_compute_wta_batch_device": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_int, _c.c_size_t,
+                                               _c.c_int, _c.c_int, _c.c_int, _c.POINTER(SmParams), _c.c_void_p,
+                                               _c.c_void_p]),
     "sm_compute_device": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_int, _c.c_int, _c.c_int,
                                      _c.POINTER(SmParams), _c.c_void_p]),
     "sm_compute_batch_device": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_int, _c.c_size_t,
@@ -247,7 +250,28 @@ class Engine:
                                             ctypes.byref(params), out.ctypes.data))
         return out
 
+    def compute_wta(self, left: np.ndarray, right: np.ndarray, params: SmParams):
+        """Gray pair -> (int16 [H, W] disparity x16, int16 [H, W] integer WTA index): the
+        index is OpenCV's bestDisp in [0, D) where the uniqueness test passes, -1 elsewhere,
+        before the sub-pixel step, the LR check and the median (sm_compute's wta_out)."""
+        left = np.ascontiguousarray(left, np.uint8)
+        right = np.ascontiguousarray(right, np.uint8)
+        if left.ndim != 2:
+            raise ValueError("compute_wta takes gray [H, W] images")
+        H, W = left.shape
+        out = np.empty((H, W), np.int16)
+        wta = np.empty((H, W), np.int16)
+        self._check(self._lib.sm_compute(self.ctx, left.ctypes.data, right.ctypes.data, H, W, W,
+                                         ctypes.byref(params), out.ctypes.data, wta.ctypes.data))
+        return out, wta
+
     # -- device pointers (e.g. torch tensors' data_ptr()) -------------------
+    def compute_wta_batch_device(self, d_left: int, d_right: int, npairs: int, pair_stride: int, H: int, W: int,
+                                 stride: int, params: SmParams, d_out: int, d_wta: int):
+        self._check(self._lib.sm_compute_wta_batch_device(
+            self.ctx, ctypes.c_void_p(d_left), ctypes.c_void_p(d_right), npairs, pair_stride, H, W, stride,
+            ctypes.byref(params), ctypes.c_void_p(d_out), ctypes.c_void_p(d_wta)))
+
     def compute_device(self, d_left: int, d_right: int, H: int, W: int, stride: int, params: SmParams,
                        d_out: int):
         self._check(self._lib.sm_compute_device(self.ctx, ctypes.c_void_p(d_left), ctypes.c_void_p(d_right),

@@ -116,6 +116,7 @@ struct sm_ctx {
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;  // sweep engine: E/W kernel on the side stream
     const uint32_t* fb_guard = nullptr;  // set while enqueuing a group's guarded per-direction fallback
     hipStream_t wta_override = nullptr;  // stream of the WTA launch when it is not stream_b()
+    int16_t* wta_dst = nullptr;  // integer WTA index of the current launch group (sm_compute_wta_*), or null
     BufSet set[2];
     int next_set = 0;
     // geometry of the last computation (for sm_debug_fetch): its last pair
@@ -490,6 +491,7 @@ int launch_wta_t(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs)
     StageTimer t(ctx, stream_b(ctx), ctx->fb_guard ? SM_STAGE_FALLBACK : SM_STAGE_WTA, g.G);
     if constexpr (D % 64 == 0) {
         if (row_mode(ctx, n) && !ctx->fb_guard) {
+            if (ctx->wta_dst) return fail(ctx, SM_E_UNSUPPORTED, "the row-WTA ablation has no WTA-index output");
             smk::RowArgs ra{};
             ra.cl = (const uint64_t*)bs.census[0].p;
             ra.cr = (const uint64_t*)bs.census[1].p;
@@ -536,8 +538,10 @@ int launch_wta_t(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs)
     wa.uniq = n.uniq;
     wa.disp12 = n.disp12;
     wa.disp = (int16_t*)bs.raw.p;
+    wa.wta = ctx->wta_dst;
     wa.lane8 = n.ndirs == 5;
     dim3 grid(g.H, g.G);
+    const size_t smem = (size_t)g.W * (ctx->wta_dst ? 10 : 8) + 16;
     if (ctx->fb_guard) {
         wa.guard = ctx->fb_guard;
         wa.fallbacks = (uint32_t*)ctx->sweep_err.p + ERR_FALLBACKS;
@@ -545,9 +549,9 @@ int launch_wta_t(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs)
         grid = dim3(std::min(g.H * g.G, 64), 1);
     }
     if (ctx->fb_guard)
-        hipLaunchKernelGGL((smk::k_wta<DPLV, LT, 1024, true>), grid, dim3(1024), (size_t)g.W * 8, stream_b(ctx), wa);
+        hipLaunchKernelGGL((smk::k_wta<DPLV, LT, 1024, true>), grid, dim3(1024), smem, stream_b(ctx), wa);
     else
-        hipLaunchKernelGGL((smk::k_wta<DPLV, LT, WTA_NT>), grid, dim3(WTA_NT), (size_t)g.W * 8, stream_b(ctx), wa);
+        hipLaunchKernelGGL((smk::k_wta<DPLV, LT, WTA_NT>), grid, dim3(WTA_NT), smem, stream_b(ctx), wa);
     HIP_TRY(ctx, hipGetLastError());
     return SM_OK;
 }
@@ -889,8 +893,8 @@ int run_sweep(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs, hipStream_t 
         StageTimer ts(ctx, ctx->stream, SM_STAGE_SWEEP_WTA, G);
         if ((rc = sweep_pass(ctx, n, g, j, n.ndirs == 8 ? 2 : 1)) != SM_OK) return rc;
     }
-    HIP_TRY(ctx, smk::lr_rows_launch((const uint32_t*)bs.key2.p, (const uint32_t*)bs.pre.p, (int16_t*)bs.raw.p, G,
-                                     g.H, g.W, n.D, n.minD, n.minX1, n.maxX1, n.disp12, ctx->stream));
+    HIP_TRY(ctx, smk::lr_rows_launch((const uint32_t*)bs.key2.p, (const uint32_t*)bs.pre.p, (int16_t*)bs.raw.p,
+                                     ctx->wta_dst, G, g.H, g.W, n.D, n.minD, n.minX1, n.maxX1, n.disp12, ctx->stream));
     return SM_OK;
 }
 
@@ -1147,8 +1151,10 @@ int wide_paths_wta(sm_ctx* ctx, const Geo& g, const Norm& n, BufSet& bs)
     wa.disp12 = n.disp12;
     wa.ndirs = n.ndirs;
     wa.disp = (int16_t*)bs.raw.p;
+    wa.wta = ctx->wta_dst;
     StageTimer t(ctx, ctx->stream, SM_STAGE_WTA, g.G);
-    hipLaunchKernelGGL((smk::k_wide_wta<DPL, 1024>), dim3(g.H, g.G), dim3(1024), (size_t)g.W * 8, ctx->stream, wa);
+    hipLaunchKernelGGL((smk::k_wide_wta<DPL, 1024>), dim3(g.H, g.G), dim3(1024), (size_t)g.W * (wa.wta ? 10 : 8) + 16,
+                       ctx->stream, wa);
     HIP_TRY(ctx, hipGetLastError());
     return SM_OK;
 }
@@ -1229,6 +1235,11 @@ int run_group(sm_ctx* ctx, const Src& src, const Geo& g, const Norm& n, int16_t*
             hipLaunchKernelGGL(smk::k_fill16, dim3(grid_for((size_t)H * W)), dim3(256), 0, ctx->stream,
                                d_out + (size_t)i * H * W, (size_t)H * W, (int16_t)INVALID);
             HIP_TRY(ctx, hipGetLastError());
+            if (ctx->wta_dst) {
+                hipLaunchKernelGGL(smk::k_fill16, dim3(grid_for((size_t)H * W)), dim3(256), 0, ctx->stream,
+                                   ctx->wta_dst + (size_t)i * H * W, (size_t)H * W, (int16_t)-1);
+                HIP_TRY(ctx, hipGetLastError());
+            }
         }
         bs.pending = false;
         ctx->last_width1 = 0;
@@ -1386,7 +1397,9 @@ int run_group(sm_ctx* ctx, const Src& src, const Geo& g, const Norm& n, int16_t*
     return finish_group(ctx, g, n, bs, s, d_out, sb);
 }
 
-int run_pairs(sm_ctx* ctx, const Src& src, int npairs, int H, int W, int stride, const Norm& n, int16_t* d_out)
+// d_wta (may be null): the integer WTA index of every pair, [npairs][H][W] int16
+int run_pairs(sm_ctx* ctx, const Src& src, int npairs, int H, int W, int stride, const Norm& n, int16_t* d_out,
+              int16_t* d_wta = nullptr)
 {
     ctx->lastH = H;
     ctx->lastW = W;
@@ -1421,8 +1434,10 @@ int run_pairs(sm_ctx* ctx, const Src& src, int npairs, int H, int W, int stride,
         StageTimer total(ctx, ctx->stream, SM_STAGE_TOTAL, npairs);
         for (int i = 0; i < npairs && rc == SM_OK; i += G) {
             g.G = std::min(G, npairs - i);
+            ctx->wta_dst = d_wta ? d_wta + (size_t)i * H * W : nullptr;
             rc = run_group(ctx, src.advance(i), g, n, d_out + (size_t)i * H * W);
         }
+        ctx->wta_dst = nullptr;
         // join stream B back into the caller's stream
         for (auto& bs : ctx->set)
             if (bs.pending) {
@@ -1836,6 +1851,24 @@ int sm_compute_device(sm_ctx* ctx, const uint8_t* dL, const uint8_t* dR, int H, 
     return run_pairs(ctx, src, 1, H, W, stride, n, d_out);
 }
 
+int sm_compute_wta_batch_device(sm_ctx* ctx, const uint8_t* dL, const uint8_t* dR, int npairs, size_t pair_stride,
+                                int H, int W, int stride, const sm_params* p, int16_t* d_out, int16_t* d_wta)
+{
+    if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
+    if (npairs < 0) return fail(ctx, SM_E_ARG, "npairs < 0");
+    if (!dL || !dR || !d_out) return fail(ctx, SM_E_ARG, "NULL image/output pointer");
+    Norm n;
+    int rc = normalize(ctx, p, H, W, n);
+    if (rc != SM_OK) return rc;
+    if (stride < W) return fail(ctx, SM_E_ARG, "stride %d < width %d", stride, W);
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    Src src;
+    src.L = dL;
+    src.R = dR;
+    src.pair_stride = pair_stride;
+    return run_pairs(ctx, src, npairs, H, W, stride, n, d_out, d_wta);
+}
+
 int sm_compute_batch_device_cn(sm_ctx* ctx, const uint8_t* dL, const uint8_t* dR, int npairs, size_t pair_stride,
                                int H, int W, int stride, int channels, const sm_params* p, int16_t* d_out)
 {
@@ -1860,8 +1893,10 @@ int sm_compute_batch_device(sm_ctx* ctx, const uint8_t* dL, const uint8_t* dR, i
     return sm_compute_batch_device_cn(ctx, dL, dR, npairs, pair_stride, H, W, stride, 1, p, d_out);
 }
 
-int sm_compute_cn(sm_ctx* ctx, const uint8_t* L, const uint8_t* R, int H, int W, int stride, int channels,
-                  const sm_params* p, int16_t* disp_out)
+namespace {
+// host-pointer matcher call: pinned staging in, one pair, maps (+ the WTA index) out
+int compute_host(sm_ctx* ctx, const uint8_t* L, const uint8_t* R, int H, int W, int stride, int channels,
+                 const sm_params* p, int16_t* disp_out, int16_t* wta_out)
 {
     if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
     if (!L || !R || !disp_out) return fail(ctx, SM_E_ARG, "NULL image/output pointer");
@@ -1871,28 +1906,37 @@ int sm_compute_cn(sm_ctx* ctx, const uint8_t* L, const uint8_t* R, int H, int W,
     const size_t row = (size_t)W * channels;
     if ((size_t)stride < row) return fail(ctx, SM_E_ARG, "stride %d < width %d x %d channels", stride, W, channels);
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    const size_t img = (size_t)H * row;
+    const size_t img = (size_t)H * row, maps = (size_t)H * W * 2;
     for (int i = 0; i < 2; i++)
         if ((rc = ensure(ctx, ctx->img[i], img)) != SM_OK) return rc;
-    if ((rc = ensure(ctx, ctx->out, (size_t)H * W * 2)) != SM_OK) return rc;
+    if ((rc = ensure(ctx, ctx->out, maps * (wta_out ? 2 : 1))) != SM_OK) return rc;
     HostStage hs(ctx);
-    if ((rc = hs.reserve(stage_bytes(img, 2) + stage_bytes((size_t)H * W * 2))) != SM_OK) return rc;
+    if ((rc = hs.reserve(stage_bytes(img, 2) + stage_bytes(maps, 2))) != SM_OK) return rc;
     if ((rc = hs.in(ctx->img[0].p, L, H, row, stride)) != SM_OK) return rc;
     if ((rc = hs.in(ctx->img[1].p, R, H, row, stride)) != SM_OK) return rc;
     Src src;
     src.L = (const uint8_t*)ctx->img[0].p;
     src.R = (const uint8_t*)ctx->img[1].p;
-    rc = run_pairs(ctx, src, 1, H, W, (int)row, n, (int16_t*)ctx->out.p);
+    int16_t* d_wta = wta_out ? (int16_t*)ctx->out.p + (size_t)H * W : nullptr;
+    rc = run_pairs(ctx, src, 1, H, W, (int)row, n, (int16_t*)ctx->out.p, d_wta);
     if (rc != SM_OK) return rc;
-    if ((rc = hs.out(disp_out, ctx->out.p, (size_t)H * W * 2)) != SM_OK) return rc;
+    if ((rc = hs.out(disp_out, ctx->out.p, maps)) != SM_OK) return rc;
+    if (wta_out && (rc = hs.out(wta_out, d_wta, maps)) != SM_OK) return rc;
     if ((rc = hs.finish()) != SM_OK) return rc;
     return check_sweep_errors(ctx);
 }
+}  // namespace
+
+int sm_compute_cn(sm_ctx* ctx, const uint8_t* L, const uint8_t* R, int H, int W, int stride, int channels,
+                  const sm_params* p, int16_t* disp_out)
+{
+    return compute_host(ctx, L, R, H, W, stride, channels, p, disp_out, nullptr);
+}
 
 int sm_compute(sm_ctx* ctx, const uint8_t* L, const uint8_t* R, int H, int W, int stride, const sm_params* p,
-               int16_t* disp_out)
+               int16_t* disp_out, int16_t* wta_out)
 {
-    return sm_compute_cn(ctx, L, R, H, W, stride, 1, p, disp_out);
+    return compute_host(ctx, L, R, H, W, stride, 1, p, disp_out, wta_out);
 }
 
 int sm_aggregate_cost_f32_device(sm_ctx* ctx, const float* d_cost, int npairs, size_t pair_stride_elems, int D,
@@ -2042,6 +2086,7 @@ int sm_compute_disparity_batch_device(sm_ctx* ctx, const uint8_t* dL, const uint
     if ((rc = ensure_event(ctx, ctx->ev_lr_fork)) != SM_OK) return rc;
     if ((rc = ensure_event(ctx, ctx->ev_lr_join)) != SM_OK) return rc;
     sm_ctx* tw = ctx->twin;
+    StageTimer call(ctx, ctx->stream, SM_STAGE_CALL, npairs);
     HIP_TRY(ctx, hipEventRecord(ctx->ev_lr_fork, ctx->stream));
     HIP_TRY(ctx, hipStreamWaitEvent(tw->stream, ctx->ev_lr_fork, 0));
     rc = sm_compute_batch_device(tw, dR, dL, npairs, pair_stride, H, W, stride, &rm, d_dispr);

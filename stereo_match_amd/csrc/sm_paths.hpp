@@ -476,6 +476,7 @@ struct WtaArgs {
     int nslots;
     int H, W, width1, D, minD, minX1, uniq, disp12;
     int16_t* disp;  // [pair][H][W] pre-median
+    int16_t* wta;   // [pair][H][W] integer WTA index (best, -1 rejected / outside the domain), or null
     const uint16_t* part;  // hybrid engine: u16 S + SE + SW sums [pair][H][width1][D], or null
     size_t part_pair;      // elements
     int lane8;             // 5 paths: OpenCV's SIMD tie-break among equal minima (wta_rank)
@@ -494,9 +495,11 @@ __device__ __forceinline__ void wta_row(const WtaArgs& a, const int y, const int
     const int INVALID = (minD - 1) * 16;
     uint32_t* key2 = smem;
     int* drow = reinterpret_cast<int*>(smem + W);
+    int16_t* brow = reinterpret_cast<int16_t*>(smem + 2 * W);  // integer WTA index (only with a.wta)
     for (int i = threadIdx.x; i < W; i += NT) {
         key2[i] = 0xFFFFFFFFu;
         drow[i] = INVALID;
+        if (a.wta) brow[i] = -1;
     }
     __syncthreads();
     const int g = threadIdx.x & 15;
@@ -596,6 +599,7 @@ __device__ __forceinline__ void wta_row(const WtaArgs& a, const int y, const int
                 d16 = best * 16;
             }
             drow[X] = d16 + minD * 16;
+            if (a.wta) brow[X] = (int16_t)best;
         }
     }
     __syncthreads();
@@ -619,6 +623,7 @@ __device__ __forceinline__ void wta_row(const WtaArgs& a, const int y, const int
             if (rej1 && rej2) d1 = INVALID;
         }
         out[X] = (int16_t)d1;
+        if (a.wta) a.wta[(size_t)pair * a.H * W + (size_t)y * W + X] = brow[X];
     }
 }
 

@@ -731,9 +731,11 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
 // nb = S[best-1] | S[best+1] << 16.  Columns outside [minX1, maxX1) are
 // INVALID.  blockIdx = (y, pair); dynamic LDS = 4*W bytes (disp2 keys) + 2*W
 // (the row's sub-pixel disparities).
+// wta (may be null): the integer WTA index per pixel (best, or -1 where rejected or outside
+// [minX1, maxX1)), before the sub-pixel step, the LR check and the median.
 __global__ void __launch_bounds__(256) k_lr_rows(const uint32_t* __restrict__ rec, const uint32_t* __restrict__ nbs,
-                                                 int16_t* __restrict__ out, int H, int W, int D, int minD, int minX1,
-                                                 int maxX1, int disp12)
+                                                 int16_t* __restrict__ out, int16_t* __restrict__ wta, int H, int W,
+                                                 int D, int minD, int minX1, int maxX1, int disp12)
 {
     extern __shared__ uint32_t key2[];
     int16_t* drow = reinterpret_cast<int16_t*>(key2 + W);
@@ -743,10 +745,12 @@ __global__ void __launch_bounds__(256) k_lr_rows(const uint32_t* __restrict__ re
     for (int X = threadIdx.x; X < W; X += 256) {
         key2[X] = 0xFFFFFFFFu;
         drow[X] = (int16_t)INVALID;
+        if (wta && (X < minX1 || X >= maxX1)) wta[row + X] = -1;
     }
     __syncthreads();
     for (int X = minX1 + (int)threadIdx.x; X < maxX1; X += 256) {
         const uint32_t r = rec[row + X];
+        if (wta) wta[row + X] = r != 0xFFFFFFFFu ? (int16_t)(r & 0xFFFF) : (int16_t)-1;
         if (r != 0xFFFFFFFFu) {
             const int best = (int)(r & 0xFFFF), minS = (int)(r >> 16);
             atomicMin(&key2[X - best - minD], (r & 0xFFFF0000u) | (uint32_t)(0xFFFF - X));

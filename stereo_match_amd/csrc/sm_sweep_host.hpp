@@ -83,9 +83,10 @@ inline hipError_t sweep_launch(int D, int ct_bytes, int mode, int impl, const Sw
          : mode == 1 ? sweep_launch_m1(D, ct_bytes, impl, a, npairs, stream)
                      : sweep_launch_m2(D, ct_bytes, impl, a, npairs, stream);
 }
-// sub-pixel + disp2 + disp12MaxDiff check from the WTA sweep's records, one row per workgroup
-hipError_t lr_rows_launch(const uint32_t* rec, const uint32_t* nb, int16_t* out, int G, int H, int W, int D, int minD,
-                          int minX1, int maxX1, int disp12, hipStream_t stream);
+// sub-pixel + disp2 + disp12MaxDiff check from the WTA sweep's records, one row per workgroup;
+// wta (may be null): the integer WTA index [pair][H][W] (-1: rejected / outside the domain)
+hipError_t lr_rows_launch(const uint32_t* rec, const uint32_t* nb, int16_t* out, int16_t* wta, int G, int H, int W,
+                          int D, int minD, int minX1, int maxX1, int disp12, hipStream_t stream);
 
 // horizontal (E, W) path volumes, packed recurrence (sm_ew.hpp / sm_ew.hip)
 struct EwArgs {

@@ -183,6 +183,7 @@ struct WideWtaArgs {
     size_t slot_bytes, L_pair_bytes;
     int H, W, width1, D, minD, minX1, uniq, disp12, ndirs;
     int16_t* disp;  // [pair][H][W] pre-median
+    int16_t* wta;   // [pair][H][W] integer WTA index (best, -1 rejected / outside the domain), or null
 };
 
 // S in OpenCV's saturating order, WTA (MODE_SGBM: SIMD lane tie-break), the
@@ -197,9 +198,11 @@ __global__ void __launch_bounds__(NT) k_wide_wta(WideWtaArgs a)
     const int y = blockIdx.x, pair = blockIdx.y;
     uint32_t* key2 = smem;
     int* drow = reinterpret_cast<int*>(smem + W);
+    int16_t* brow = reinterpret_cast<int16_t*>(smem + 2 * W);  // integer WTA index (only with a.wta)
     for (int i = threadIdx.x; i < W; i += NT) {
         key2[i] = 0xFFFFFFFFu;
         drow[i] = INVALID;
+        if (a.wta) brow[i] = -1;
     }
     __syncthreads();
     const int g = threadIdx.x & 15, grp = threadIdx.x >> 4;
@@ -245,6 +248,7 @@ __global__ void __launch_bounds__(NT) k_wide_wta(WideWtaArgs a)
                 d16 += ((Sm - Sq) * 16 + den) / (den * 2);  // C truncation
             }
             drow[X] = d16 + minD * 16;
+            if (a.wta) brow[X] = (int16_t)best;
         }
     }
     __syncthreads();
@@ -268,6 +272,7 @@ __global__ void __launch_bounds__(NT) k_wide_wta(WideWtaArgs a)
             if (rej1 && rej2) d1 = INVALID;
         }
         out[X] = (int16_t)d1;
+        if (a.wta) a.wta[(size_t)pair * a.H * W + (size_t)y * W + X] = brow[X];
     }
 }
 

@@ -41,6 +41,34 @@ def test_launcher_spawns_two_ranks():
     assert d["distributed"]["gathered_in_pair_order"] is True
 
 
+def test_selftest_runs_mains_rank_path_three_ranks():
+    # uneven shards of the same code path (3 ranks x 2 pairs), gathered in pair order
+    r = _run(["--gpus", "3", "--selftest-cpu", "--steps", "2", "--warmup", "2", "--config", "tsukuba",
+              "--pairs-per-gpu", "2"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_line(r.stdout)
+    assert d["distributed"]["world_size"] == 3
+    assert d["distributed"]["gather_bytes_to_root"] == 6 * 288 * 384 * 2
+    assert d["distributed"]["gathered_in_pair_order"] is True
+
+
+def test_dist_flag_one_rank():
+    # --dist: the process group and the gather at world size 1 (what the GPU test runs over RCCL)
+    r = _run(["--gpus", "1", "--dist", "--selftest-cpu", "--steps", "2", "--warmup", "1", "--config", "tsukuba"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_line(r.stdout)
+    assert d["n_gpus"] == 1
+    assert d["distributed"]["backend"] == "gloo" and d["distributed"]["world_size"] == 1
+    assert d["distributed"]["gather_bytes_to_root"] == 8 * 288 * 384 * 2
+    assert d["distributed"]["gathered_in_pair_order"] is True
+
+
+def test_metric_names_the_config():
+    assert bench.metric_for("kitti") == json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
+    assert "Middlebury" in bench.metric_for("middlebury") and "2880×1988 D=256" in bench.metric_for("middlebury")
+    assert "Tsukuba 384×288 D=16" in bench.metric_for("tsukuba")
+
+
 def test_gpus_must_match_world_size():
     r = _run(["--gpus", "2", "--selftest-cpu"], env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode != 0

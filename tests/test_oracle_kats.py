@@ -177,10 +177,30 @@ def test_k6_numpy_c_bit_exact(H, W, D, minD, bs, mode, cost, uniq, d12, pfc, see
     if cost == 1:
         p.update(P1=10, P2=120)
     try:
-        a = sgm_np.compute(left, right, p)
+        a, stg = sgm_np.compute(left, right, p, return_stages=True)
     except ValueError:
         return
-    assert np.array_equal(a, ref_c.compute(left, right, p))
+    c, cw = ref_c.compute_wta(left, right, p)
+    assert np.array_equal(a, c)
+    if stg:  # the integer WTA index (SURVEY §8b wta_out): both restatements agree
+        assert np.array_equal(stg["wta"], cw)
+    else:
+        assert (cw == -1).all()
+
+
+def test_wta_index_kat():
+    """K10: the integer WTA index on a constant shift is the shift on the interior, -1 on
+    the border band x < minX1, and rejected pixels (uniqueness) carry -1 while their
+    disparity is INVALID before the LR check."""
+    left, right = synthetic.shifted_pair(40, 120, 5, seed=3)
+    p = dict(minDisparity=0, numDisparities=16, blockSize=5, P1=600, P2=2400, disp12MaxDiff=1, uniquenessRatio=15,
+             preFilterCap=63, mode=5, cost=0)
+    raw, wta = ref_c.compute_wta(left, right, p, median=False)
+    assert (wta[:, :16] == -1).all()
+    inner = wta[4:-4, 20:-4]
+    assert (inner == 5).mean() > 0.99
+    # -1 exactly where the pre-LR map would be invalid: the LR check only removes more
+    assert ((wta == -1) <= (raw == -16)).all()
 
 
 def test_speckle_filter_matches_c():
