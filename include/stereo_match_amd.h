@@ -303,46 +303,24 @@ int sm_reset_timing(sm_ctx* ctx);
  * Returns the byte size when host == NULL. */
 long long sm_debug_fetch(sm_ctx* ctx, int what, void* host, size_t bytes);
 
-/* Timing ablations ONLY (results become wrong): bit 0 skips the horizontal
- * path family, bit 1 the vertical/diagonal family, bit 2 drops every path
- * store; bit 3 (valid results) selects 16-lane instead of 8-lane vertical
- * lines at D = 128; bit 5 (valid results, D % 64 == 0) replaces the
- * horizontal family + WTA with the experimental fused row kernel (W path
- * kept on chip); bit 4 (valid results) makes that kernel store the W path
- * volume too, so sm_debug_fetch(1) returns every direction; bit 6 (valid
- * results) runs WTA + median on a second internal stream, overlapped with
- * the next launch group's path aggregation (double-buffered volumes);
- * bit 9 (valid results, D % 64 == 0) uses 64-lane horizontal lines (one row
- * per wave) instead of 16-lane lines (4 rows per wave); bit 10 (valid
- * results, census) computes Hamming costs on the fly in every direction
- * instead of reading the precomputed u8 cost volume, bit 11 only in the
- * horizontal family; bit 12 (valid results) uses the per-direction engine
- * (one path volume per direction + WTA kernel) instead of the fused sweeps,
- * so that sm_debug_fetch(1) has every direction; bit 13 (valid results) one
- * pair per fused-sweep launch; bit 14 (valid results) forces the fused sweeps
- * wherever their preconditions hold (by default launch groups of fewer
- * than 3 pairs run on the per-direction engine); bit 19 (valid results) runs
- * the fused sweeps on narrow strips (7 compute waves per workgroup) only (by
- * default each pass picks narrow or wide strips, where built, by a model of
- * its issue time); bit 23 (valid
- * results) flags every fused-sweep group as given up, so the guarded
- * per-direction fallback recomputes it; bit 31 drops the guarded fallback
- * launches (timing only); bit 15 (valid results, 8 paths) the hybrid engine: the down
- * sweep on a second stream beside a per-direction launch of the other five
- * directions; bits 16-18: launch-group size cap (0 = none); bit 8 (valid
- * results) swaps the fused-sweep engine's E/W kernel (u8 costs: the row lines
- * instead of the packed k_ew; u16: k_ew instead of the row lines); bit 7
- * (valid results) runs the fused sweeps on k_sweep2 with 6 waves of 8
- * columns, bit 27 with 3 waves of 16 columns (u8 costs at D = 128); bit 22
- * (valid results) the tiled SGBM cost kernel; bit 21 (valid results) the
- * fused sweeps on wide strips wherever built, whatever the strip-width model
- * prefers (bit 20 unused);
- * bits 24-26: fused-sweep timing ablations (results become wrong: 1 no poll
- * waits, 2 no polls, 4 no per-row barriers); bits 28-29: WLS smoother timing
- * ablations (results become wrong: 28 no sweeps, 29 no global loads/stores);
- * bit 30 (valid results): no Infinity-Cache-sized launch groups for the
- * per-direction engine with u8 costs.
- * 0 = normal operation. */
+/* Engine selection for measurements and parity debugging; every flag below gives
+ * the same disparities as 0 (normal operation):
+ *   4096     per-direction engine (one path volume per direction + WTA kernel), so
+ *            sm_debug_fetch(1) returns every direction;
+ *   16384    the fused sweeps wherever their preconditions hold (by default launch
+ *            groups below 7 census / 3 other pairs run per-direction);
+ *   8192     one pair per fused-sweep launch;  1 << 19 narrow sweep strips only;
+ *   1 << 21  wide sweep strips wherever built;  256 the other E/W kernel of the sweeps;
+ *   1 << 23  flag every sweep group as given up (the guarded fallback recomputes it);
+ *   64       WTA + median on a second stream, overlapped with the next launch group;
+ *   8, 512   16-lane vertical / 64-lane horizontal lines in the per-direction engine;
+ *   1024, 2048  census Hamming costs on the fly (all / horizontal directions);
+ *   1 << 22  tiled SGBM cost kernel;  bits 16-18 launch-group size cap;
+ *   1 << 30  no Infinity-Cache-sized launch groups for the per-direction engine.
+ * The measured ablations (row-WTA kernel 16/32, k_sweep2 128 / 1 << 27, hybrid engine
+ * 32768) and the timing switches whose results are wrong (1, 2, 4, 1 << 24..26,
+ * 1 << 28, 1 << 29, 1 << 31) exist only in the ablation build (make ablation ->
+ * libstereo_match_amd_ablate.so); this library returns SM_E_UNSUPPORTED for them. */
 int sm_set_debug_flags(sm_ctx* ctx, int flags);
 
 /* Last error text of ctx (or of the calling thread when ctx == NULL). */

@@ -29,7 +29,6 @@
 #include "sm_cost.hpp"
 #include "sm_paths.hpp"
 #include "sm_post.hpp"
-#include "sm_rowwta.hpp"
 #include "sm_wls.hpp"
 #include "sm_speckle.hpp"
 #include "sm_reproject.hpp"
@@ -37,7 +36,18 @@
 #include "sm_wide.hpp"
 #include "sm_sweep_host.hpp"
 
-#define SM_VERSION "stereo_match_amd 0.2.0 (gfx950)"
+// SM_ABLATIONS=1 (make ablation -> libstereo_match_amd_ablate.so) also builds the measured
+// ablations that the product library leaves out: the row-WTA kernel (sm_rowwta.hpp), the
+// hybrid engine, k_sweep2 (sm_sweep.hip) and the timing switches whose results are wrong
+#ifndef SM_ABLATIONS
+#define SM_ABLATIONS 0
+#endif
+#if SM_ABLATIONS
+#include "sm_rowwta.hpp"
+#define SM_VERSION "stereo_match_amd 0.3.0 (gfx950, ablation build)"
+#else
+#define SM_VERSION "stereo_match_amd 0.3.0 (gfx950)"
+#endif
 
 namespace {
 
@@ -94,6 +104,11 @@ constexpr int DBG_FORCE_FALLBACK = 1 << 23;
 constexpr int ERR_GROUP0 = 0, ERR_STICKY = 32, ERR_FALLBACKS = 48;
 // timing ablation: no guarded fallback launches after the sweeps
 constexpr int DBG_NO_FALLBACK = (int)0x80000000u;
+// flags only the ablation build (SM_ABLATIONS) accepts: timing switches whose results are
+// wrong (1, 2, 4 in the path kernels; 1 << 24..26 in the sweeps; 1 << 28, 1 << 29 in the WLS
+// smoother; 1 << 31), the row-WTA kernel (16, 32), k_sweep2 (128, 1 << 27), the hybrid engine
+constexpr int kAblationFlags = 1 | 2 | 4 | DBG_STORE_W | DBG_ROW | DBG_SWEEP_V2 | DBG_SWEEP2_NW | DBG_HYBRID |
+                               (7 << 24) | DBG_FGS_NO_SWEEP | DBG_FGS_NO_MEM | DBG_NO_FALLBACK;
 
 }  // namespace
 
@@ -104,6 +119,9 @@ struct sm_ctx {
     hipStream_t side = nullptr;    // stream B
     DevBuf img[2], planes, out, dbg, volbuf, sp_parent, sp_count, rp_in, rp_out, rp_min, bm_pre[2], bm_cost;
     DevBuf wls_num, wls_den, wls_inter, wls_w, wls_disp[2], wls_out;  // WLS scratch
+    DevBuf wls_R, wls_IT;         // WLS: Thomas pivots / elimination factors of every pass
+    hipStream_t wls_stream = nullptr;  // compute_disparity: WLS weights + pivots beside the matchers
+    hipEvent_t ev_wls_fork = nullptr, ev_wls_ready = nullptr;
     DevBuf hop, sweep_err;  // sweep engine: strip-boundary granules, device error word
     void* pin = nullptr;    // page-locked host staging of the host-pointer entry points (HostStage)
     size_t pin_n = 0;
@@ -394,7 +412,7 @@ struct Geo {  // per-group geometry shared by the launches
     bool hybrid;  // 8 paths: down sweep (u16 partial) beside a per-direction launch of E, W, NE, N, NW
 };
 
-bool row_mode(const sm_ctx* ctx, const Norm& n) { return (ctx->dbg_flags & DBG_ROW) && n.D % 64 == 0; }
+bool row_mode(const sm_ctx* ctx, const Norm& n) { return SM_ABLATIONS && (ctx->dbg_flags & DBG_ROW) && n.D % 64 == 0; }
 bool overlap(const sm_ctx* ctx) { return (ctx->dbg_flags & DBG_OVERLAP) != 0; }
 // census mode: the path kernels read a precomputed u8 Hamming cost volume
 // (k_census_cost8) instead of computing popcounts per direction; ablation
@@ -487,8 +505,9 @@ template <int DPLV, bool CENSUS>
 int launch_wta_t(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs)
 {
     using LT = typename std::conditional<CENSUS, uint8_t, uint16_t>::type;
-    constexpr int D = 16 * DPLV;
     StageTimer t(ctx, stream_b(ctx), ctx->fb_guard ? SM_STAGE_FALLBACK : SM_STAGE_WTA, g.G);
+#if SM_ABLATIONS
+    constexpr int D = 16 * DPLV;
     if constexpr (D % 64 == 0) {
         if (row_mode(ctx, n) && !ctx->fb_guard) {
             if (ctx->wta_dst) return fail(ctx, SM_E_UNSUPPORTED, "the row-WTA ablation has no WTA-index output");
@@ -522,6 +541,7 @@ int launch_wta_t(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs)
             return SM_OK;
         }
     }
+#endif
     smk::WtaArgs wa{};
     wa.L = (const uint8_t*)bs.L.p;
     wa.slot_bytes = g.slot_bytes;
@@ -606,7 +626,8 @@ int hybrid_slots(const Norm& n) { return n.ndirs == 8 ? 5 : 2; }
 
 bool use_hybrid(const sm_ctx* ctx, const Norm& n, int H)
 {
-    if ((n.ndirs != 8 && n.ndirs != 5) || !(ctx->dbg_flags & DBG_HYBRID) || (ctx->dbg_flags & (DBG_LEGACY | DBG_SWEEP8)))
+    if (!SM_ABLATIONS || (n.ndirs != 8 && n.ndirs != 5) || !(ctx->dbg_flags & DBG_HYBRID) ||
+        (ctx->dbg_flags & (DBG_LEGACY | DBG_SWEEP8)))
         return false;
     sm_ctx tmp = *ctx;
     tmp.dbg_flags = (ctx->dbg_flags & ~DBG_HYBRID) | DBG_SWEEP8;  // same preconditions as the sweeps
@@ -669,8 +690,8 @@ int ensure_sweep_err(sm_ctx* ctx)
 // columns, 1 << 27 -> 3 waves of 16 columns (slower at 8 pairs)
 int sweep_variant(const sm_ctx* ctx)
 {
-    if (ctx->dbg_flags & DBG_SWEEP_V2) return 6;
-    if (ctx->dbg_flags & DBG_SWEEP2_NW) return 3;
+    if (SM_ABLATIONS && (ctx->dbg_flags & DBG_SWEEP_V2)) return 6;
+    if (SM_ABLATIONS && (ctx->dbg_flags & DBG_SWEEP2_NW)) return 3;
     return (ctx->dbg_flags & DBG_NARROW_SWEEPS) ? 1 : 0;
 }
 
@@ -1460,6 +1481,7 @@ struct WlsNorm {
 #ifndef WLS_IEEE_DIV
 #define WLS_IEEE_DIV 0  // 1: the smoother's pivots always through IEEE division
 #endif
+constexpr int kWlsMaxPivotIters = 8;  // FgsPivotArgs::lam
 
 // one smoother pass (sm_wls.hpp k_fgs) along rows or columns; FAST: pivot reciprocals by
 // rcp + one FMA step (exact for pivots in [1, 2^24)).  A register-resident row variant (each
@@ -1506,29 +1528,133 @@ int normalize_wls(sm_ctx* ctx, const sm_wls_params* p, int H, int W, WlsNorm& n)
     return SM_OK;
 }
 
+// WLS scratch geometry: padded ROI (FT-multiple pitch) and the pairs per chunk
+struct WlsGeo {
+    bool roi;
+    int wp, hp;
+    size_t roi_elems;
+    int G;  // pairs per chunk
+};
+
+WlsGeo wls_geo(const WlsNorm& n, int npairs)
+{
+    WlsGeo w{};
+    w.roi = n.w > 0 && n.h > 0;
+    w.wp = w.roi ? (n.w + smk::FT - 1) / smk::FT * smk::FT : 0;
+    w.hp = w.roi ? (n.h + smk::FT - 1) / smk::FT * smk::FT : 0;
+    w.roi_elems = (size_t)w.wp * w.hp;
+    // scratch per pair: num, den, Ch, Cv, old-path inter, + rows/cols pivots and factors
+    // of every iteration (4 * num_iter): floats of the ROI
+    const size_t per = w.roi_elems * 4 * (5 + 4 * (size_t)std::min(n.num_iter, kWlsMaxPivotIters));
+    w.G = (int)std::max<size_t>(1, std::min<size_t>(npairs, (size_t(6) << 30) / std::max<size_t>(per, 1)));
+    return w;
+}
+
+// every pivot's reciprocal in [1, 2^24) -> the FMA-corrected reciprocal (exact there)
+bool wls_fast(const WlsNorm& n)
+{
+    bool fast = !WLS_IEEE_DIV;
+    float lam = n.lam;
+    for (int it = 0; it < n.num_iter; it++, lam = lam * n.att)
+        fast = fast && std::isfinite(lam) && 1.0 + 2.0 * (double)lam < 16777216.0;
+    return fast;
+}
+
+int ensure_wls(sm_ctx* ctx, const WlsGeo& wg, const WlsNorm& n)
+{
+    if (!wg.roi) return SM_OK;
+    const size_t e = (size_t)wg.G * wg.roi_elems * 4;
+    int rc;
+    if ((rc = ensure(ctx, ctx->wls_num, e)) != SM_OK) return rc;
+    if ((rc = ensure(ctx, ctx->wls_den, e)) != SM_OK) return rc;
+    if ((rc = ensure(ctx, ctx->wls_w, 2 * e)) != SM_OK) return rc;
+    if (n.num_iter <= kWlsMaxPivotIters) {
+        if ((rc = ensure(ctx, ctx->wls_R, 2 * (size_t)n.num_iter * e)) != SM_OK) return rc;
+        if ((rc = ensure(ctx, ctx->wls_IT, 2 * (size_t)n.num_iter * e)) != SM_OK) return rc;
+    } else if ((rc = ensure(ctx, ctx->wls_inter, e)) != SM_OK) {
+        return rc;
+    }
+    return SM_OK;
+}
+
+// The part of the WLS filter that depends on the guide alone: the smoother's edge
+// weights and (num_iter <= kWlsMaxPivotIters) the Thomas pivots of every pass
+// (sm_wls.hpp k_fgs_pivots), for the g pairs of one chunk, on stream st.
+int wls_prepare(sm_ctx* ctx, const uint8_t* guide, size_t guide_pair, int guide_stride, int g, const WlsNorm& n,
+                const WlsGeo& wg, hipStream_t st)
+{
+    if (!wg.roi) return SM_OK;
+    smk::WlsConfArgs ca{};
+    ca.guide = guide;
+    ca.guide_pair = guide_pair;
+    ca.guide_stride = guide_stride;
+    ca.Ch = (float*)ctx->wls_w.p;
+    ca.Cv = (float*)ctx->wls_w.p + (size_t)wg.G * wg.roi_elems;
+    ca.roi_pair = wg.roi_elems;
+    ca.x0 = n.x0;
+    ca.y0 = n.y0;
+    ca.w = n.w;
+    ca.h = n.h;
+    ca.wp = wg.wp;
+    std::memcpy(ca.tab, n.tab, sizeof ca.tab);
+    hipLaunchKernelGGL(smk::k_wls_weights, dim3(wg.hp, g), dim3(256), 0, st, ca);
+    HIP_TRY(ctx, hipGetLastError());
+    if (n.num_iter > kWlsMaxPivotIters) return SM_OK;
+    const bool fast = wls_fast(n);
+    const size_t var = (size_t)g * wg.roi_elems, dirv = (size_t)n.num_iter * var;
+    for (int dir = 0; dir < 2; dir++) {  // 0: rows (Ch), 1: columns (Cv)
+        smk::FgsPivotArgs pa{};
+        pa.C = dir == 0 ? ca.Ch : ca.Cv;
+        pa.R = (float*)ctx->wls_R.p + dir * dirv;
+        pa.IT = (float*)ctx->wls_IT.p + dir * dirv;
+        pa.roi_pair = wg.roi_elems;
+        pa.var_stride = var;
+        pa.w = n.w;
+        pa.h = n.h;
+        pa.wp = wg.wp;
+        float lam = n.lam;
+        for (int it = 0; it < n.num_iter; it++, lam = lam * n.att) pa.lam[it] = lam;
+        const dim3 grid((dir == 0 ? wg.hp : wg.wp) / smk::FT, n.num_iter, g);
+        if (dir == 0 && fast) hipLaunchKernelGGL((smk::k_fgs_pivots<true, true>), grid, dim3(64), 0, st, pa);
+        else if (dir == 0) hipLaunchKernelGGL((smk::k_fgs_pivots<true, false>), grid, dim3(64), 0, st, pa);
+        else if (fast) hipLaunchKernelGGL((smk::k_fgs_pivots<false, true>), grid, dim3(64), 0, st, pa);
+        else hipLaunchKernelGGL((smk::k_fgs_pivots<false, false>), grid, dim3(64), 0, st, pa);
+        HIP_TRY(ctx, hipGetLastError());
+    }
+    return SM_OK;
+}
+
+template <int NRHS>
+void launch_fgs_solve(bool rows, dim3 grid, hipStream_t st, const smk::FgsSolveArgs& fa)
+{
+    if (rows) hipLaunchKernelGGL((smk::k_fgs_solve<NRHS, true>), grid, dim3(64), 0, st, fa);
+    else hipLaunchKernelGGL((smk::k_fgs_solve<NRHS, false>), grid, dim3(64), 0, st, fa);
+}
+
 // npairs maps; pair i: displ/dispr at +i*disp_pair elements, guide at +i*guide_pair bytes.
+// prepared: wls_prepare already ran for these pairs (one chunk holds them all).
 int run_wls(sm_ctx* ctx, const int16_t* dl, const int16_t* dr, size_t disp_pair, const uint8_t* guide,
-            size_t guide_pair, int guide_stride, int npairs, int H, int W, const WlsNorm& n, int16_t* d_out)
+            size_t guide_pair, int guide_stride, int npairs, int H, int W, const WlsNorm& n, int16_t* d_out,
+            bool prepared = false)
 {
     if (npairs <= 0) return SM_OK;
-    const bool roi = n.w > 0 && n.h > 0;
-    const int wp = roi ? (n.w + smk::FT - 1) / smk::FT * smk::FT : 0;
-    const int hp = roi ? (n.h + smk::FT - 1) / smk::FT * smk::FT : 0;
-    const size_t roi_elems = (size_t)wp * hp;
-    // scratch: num, den, inter, Ch, Cv floats per pair
-    const int G = (int)std::max<size_t>(
-        1, std::min<size_t>(npairs, (size_t(6) << 30) / std::max<size_t>(roi_elems * 20, 1)));
+    const WlsGeo wg = wls_geo(n, npairs);
+    const int G = wg.G;
+    const bool roi = wg.roi;
+    const int wp = wg.wp, hp = wg.hp;
+    const size_t roi_elems = wg.roi_elems;
     int rc;
-    if (roi) {
-        if ((rc = ensure(ctx, ctx->wls_num, (size_t)G * roi_elems * 4)) != SM_OK) return rc;
-        if ((rc = ensure(ctx, ctx->wls_den, (size_t)G * roi_elems * 4)) != SM_OK) return rc;
-        if ((rc = ensure(ctx, ctx->wls_inter, (size_t)G * roi_elems * 4)) != SM_OK) return rc;
-        if ((rc = ensure(ctx, ctx->wls_w, (size_t)G * roi_elems * 8)) != SM_OK) return rc;
-    }
+    if ((rc = ensure_wls(ctx, wg, n)) != SM_OK) return rc;
+    if (prepared && G < npairs) return fail(ctx, SM_E_ARG, "internal: prepared WLS batch exceeds one chunk");
     StageTimer t(ctx, ctx->stream, SM_STAGE_WLS, npairs);
+    const bool pivots = n.num_iter <= kWlsMaxPivotIters;
     for (int p0 = 0; p0 < npairs; p0 += G) {
         const int g = std::min(G, npairs - p0);
         if (roi) {
+            if (!prepared &&
+                (rc = wls_prepare(ctx, guide + (size_t)p0 * guide_pair, guide_pair, guide_stride, g, n, wg,
+                                  ctx->stream)) != SM_OK)
+                return rc;
             smk::WlsConfArgs ca{};
             ca.dl = dl + (size_t)p0 * disp_pair;
             ca.dr = dr ? dr + (size_t)p0 * disp_pair : nullptr;
@@ -1553,33 +1679,53 @@ int run_wls(sm_ctx* ctx, const int16_t* dl, const int16_t* dr, size_t disp_pair,
             ca.lrc_thresh = n.lrc;
             ca.roll_off = n.roll_off;
             ca.use_confidence = n.use_conf;
+            ca.weights = 0;  // wls_prepare wrote Ch / Cv
             std::memcpy(ca.tab, n.tab, sizeof ca.tab);
             hipLaunchKernelGGL(smk::k_wls_conf, dim3(hp, g), dim3(256), (size_t)(256 + n.w) * 4, ctx->stream, ca);
             HIP_TRY(ctx, hipGetLastError());
-            smk::FgsArgs fa{};
-            fa.u[0] = ca.num;
-            fa.u[1] = ca.den;
-            fa.inter = (float*)ctx->wls_inter.p;
-            fa.roi_pair = roi_elems;
-            fa.w = n.w;
-            fa.h = n.h;
-            fa.wp = wp;
-            fa.dbg = ((ctx->dbg_flags & DBG_FGS_NO_SWEEP) ? 1 : 0) | ((ctx->dbg_flags & DBG_FGS_NO_MEM) ? 2 : 0);
-            float lam = n.lam;
-            // every pivot of every iteration below 2^24 -> the FMA-corrected reciprocal (exact there)
-            bool fast = !WLS_IEEE_DIV;
-            for (int it = 0; it < n.num_iter; it++, lam = lam * n.att)
-                fast = fast && std::isfinite(lam) && 1.0 + 2.0 * (double)lam < 16777216.0;
-            lam = n.lam;
             const int nrhs = n.use_conf ? 2 : 1;
-            for (int it = 0; it < n.num_iter; it++) {
-                fa.lam = lam;
-                fa.C = ca.Ch;
-                launch_fgs(nrhs, fast, true, dim3(hp / smk::FT, g), ctx->stream, fa);
-                fa.C = ca.Cv;
-                launch_fgs(nrhs, fast, false, dim3(wp / smk::FT, g), ctx->stream, fa);
-                HIP_TRY(ctx, hipGetLastError());
-                lam = lam * n.att;
+            float lam = n.lam;
+            if (pivots) {
+                // the right-hand-side sweeps over the precomputed pivots (sm_wls.hpp)
+                const size_t var = (size_t)g * roi_elems, dirv = (size_t)n.num_iter * var;
+                smk::FgsSolveArgs fa{};
+                fa.u[0] = ca.num;
+                fa.u[1] = ca.den;
+                fa.roi_pair = roi_elems;
+                fa.w = n.w;
+                fa.h = n.h;
+                fa.wp = wp;
+                for (int it = 0; it < n.num_iter; it++, lam = lam * n.att) {
+                    fa.lam = lam;
+                    for (int dir = 0; dir < 2; dir++) {
+                        fa.C = dir == 0 ? ca.Ch : ca.Cv;
+                        fa.R = (const float*)ctx->wls_R.p + dir * dirv + it * var;
+                        fa.IT = (const float*)ctx->wls_IT.p + dir * dirv + it * var;
+                        const dim3 grid((dir == 0 ? hp : wp) / smk::FT, g);
+                        if (nrhs == 2) launch_fgs_solve<2>(dir == 0, grid, ctx->stream, fa);
+                        else launch_fgs_solve<1>(dir == 0, grid, ctx->stream, fa);
+                        HIP_TRY(ctx, hipGetLastError());
+                    }
+                }
+            } else {  // more iterations than the pivot buffers hold: pivots inside each pass
+                smk::FgsArgs fa{};
+                fa.u[0] = ca.num;
+                fa.u[1] = ca.den;
+                fa.inter = (float*)ctx->wls_inter.p;
+                fa.roi_pair = roi_elems;
+                fa.w = n.w;
+                fa.h = n.h;
+                fa.wp = wp;
+                fa.dbg = ((ctx->dbg_flags & DBG_FGS_NO_SWEEP) ? 1 : 0) | ((ctx->dbg_flags & DBG_FGS_NO_MEM) ? 2 : 0);
+                const bool fast = wls_fast(n);
+                for (int it = 0; it < n.num_iter; it++, lam = lam * n.att) {
+                    fa.lam = lam;
+                    fa.C = ca.Ch;
+                    launch_fgs(nrhs, fast, true, dim3(hp / smk::FT, g), ctx->stream, fa);
+                    fa.C = ca.Cv;
+                    launch_fgs(nrhs, fast, false, dim3(wp / smk::FT, g), ctx->stream, fa);
+                    HIP_TRY(ctx, hipGetLastError());
+                }
             }
         }
         smk::WlsFinalArgs wa{};
@@ -1747,6 +1893,20 @@ int run_bm(sm_ctx* ctx, const uint8_t* dL, const uint8_t* dR, size_t pair_stride
     return SM_OK;
 }
 
+// the third stream of compute_disparity (WLS guide-only work), on the context's CU mask
+int ensure_wls_stream(sm_ctx* ctx)
+{
+    int rc;
+    if ((rc = ensure_event(ctx, ctx->ev_wls_fork)) != SM_OK) return rc;
+    if ((rc = ensure_event(ctx, ctx->ev_wls_ready)) != SM_OK) return rc;
+    if (ctx->wls_stream) return SM_OK;
+    if (!ctx->cu_mask.empty())
+        HIP_TRY(ctx, hipExtStreamCreateWithCUMask(&ctx->wls_stream, (uint32_t)ctx->cu_mask.size(), ctx->cu_mask.data()));
+    else
+        HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->wls_stream, hipStreamNonBlocking));
+    return SM_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1784,7 +1944,7 @@ void sm_destroy(sm_ctx* ctx)
                       &ctx->volbuf,  &ctx->wls_num, &ctx->wls_den,   &ctx->wls_inter,   &ctx->wls_disp[0], &ctx->wls_w,
                       &ctx->wls_disp[1], &ctx->wls_out, &ctx->sp_parent, &ctx->sp_count,
                       &ctx->rp_in,   &ctx->rp_out,  &ctx->rp_min,    &ctx->bm_pre[0],   &ctx->bm_pre[1],
-                      &ctx->bm_cost, &ctx->hop,     &ctx->sweep_err};
+                      &ctx->bm_cost, &ctx->hop,     &ctx->sweep_err, &ctx->wls_R,      &ctx->wls_IT};
     for (DevBuf* b : bufs)
         if (b->p) (void)hipFree(b->p);
     for (auto& bs : ctx->set) {
@@ -1804,6 +1964,9 @@ void sm_destroy(sm_ctx* ctx)
     if (ctx->ev_lr_join) (void)hipEventDestroy(ctx->ev_lr_join);
     sm_destroy(ctx->twin);
     if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
+    if (ctx->ev_wls_fork) (void)hipEventDestroy(ctx->ev_wls_fork);
+    if (ctx->ev_wls_ready) (void)hipEventDestroy(ctx->ev_wls_ready);
+    if (ctx->wls_stream) (void)hipStreamDestroy(ctx->wls_stream);
     if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
     if (ctx->side) (void)hipStreamDestroy(ctx->side);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
@@ -2085,8 +2248,23 @@ int sm_compute_disparity_batch_device(sm_ctx* ctx, const uint8_t* dL, const uint
     }
     if ((rc = ensure_event(ctx, ctx->ev_lr_fork)) != SM_OK) return rc;
     if ((rc = ensure_event(ctx, ctx->ev_lr_join)) != SM_OK) return rc;
+    if (stride < W) return fail(ctx, SM_E_ARG, "stride %d < width %d", stride, W);
+    WlsNorm wn;
+    if ((rc = normalize_wls(ctx, wls, H, W, wn)) != SM_OK) return rc;
     sm_ctx* tw = ctx->twin;
     StageTimer call(ctx, ctx->stream, SM_STAGE_CALL, npairs);
+    // the WLS filter's guide-only work (edge weights, the Thomas pivots of every pass) runs
+    // on a third stream beside the two matchers when the batch fits one WLS chunk
+    const WlsGeo wg = wls_geo(wn, npairs);
+    const bool prep = wg.roi && wg.G >= npairs;
+    if (prep) {
+        if ((rc = ensure_wls(ctx, wg, wn)) != SM_OK) return rc;
+        if ((rc = ensure_wls_stream(ctx)) != SM_OK) return rc;
+        HIP_TRY(ctx, hipEventRecord(ctx->ev_wls_fork, ctx->stream));
+        HIP_TRY(ctx, hipStreamWaitEvent(ctx->wls_stream, ctx->ev_wls_fork, 0));
+        if ((rc = wls_prepare(ctx, dL, pair_stride, stride, npairs, wn, wg, ctx->wls_stream)) != SM_OK) return rc;
+        HIP_TRY(ctx, hipEventRecord(ctx->ev_wls_ready, ctx->wls_stream));
+    }
     HIP_TRY(ctx, hipEventRecord(ctx->ev_lr_fork, ctx->stream));
     HIP_TRY(ctx, hipStreamWaitEvent(tw->stream, ctx->ev_lr_fork, 0));
     rc = sm_compute_batch_device(tw, dR, dL, npairs, pair_stride, H, W, stride, &rm, d_dispr);
@@ -2094,8 +2272,9 @@ int sm_compute_disparity_batch_device(sm_ctx* ctx, const uint8_t* dL, const uint
     HIP_TRY(ctx, hipEventRecord(ctx->ev_lr_join, tw->stream));
     rc = sm_compute_batch_device(ctx, dL, dR, npairs, pair_stride, H, W, stride, &lm, d_displ);
     HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_lr_join, 0));  // joined on every path
+    if (prep) HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_wls_ready, 0));
     if (rc != SM_OK) return rc;
-    return sm_wls_filter_batch_device(ctx, d_displ, d_dispr, dL, npairs, pair_stride, stride, H, W, wls, d_filtered);
+    return run_wls(ctx, d_displ, d_dispr, (size_t)H * W, dL, pair_stride, stride, npairs, H, W, wn, d_filtered, prep);
 }
 
 int sm_compute_disparity(sm_ctx* ctx, const uint8_t* L, const uint8_t* R, int H, int W, int stride,
@@ -2407,6 +2586,10 @@ int sm_set_cu_mask(sm_ctx* ctx, const uint32_t* mask, int nwords)
     }
     (void)hipStreamDestroy(ctx->own_stream);
     (void)hipStreamDestroy(ctx->side);
+    if (ctx->wls_stream) {  // recreated on the new mask when next needed
+        (void)hipStreamDestroy(ctx->wls_stream);
+        ctx->wls_stream = nullptr;
+    }
     ctx->own_stream = a;
     ctx->side = b;
     ctx->stream = a;
@@ -2433,6 +2616,10 @@ int sm_set_timing(sm_ctx* ctx, int enable)
 int sm_set_debug_flags(sm_ctx* ctx, int flags)
 {
     if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
+    if (!SM_ABLATIONS && (flags & kAblationFlags))
+        return fail(ctx, SM_E_UNSUPPORTED, "debug flags 0x%x need the ablation build (make -C stereo_match_amd/csrc "
+                    "ablation; STEREO_MATCH_AMD_LIB=.../libstereo_match_amd_ablate.so)",
+                    (unsigned)(flags & kAblationFlags));
     if (ctx->twin) sm_set_debug_flags(ctx->twin, flags);
     ctx->dbg_flags = flags;
     return SM_OK;

@@ -23,6 +23,9 @@ namespace smk {
 #ifndef SWEEP_STREAM_AUX
 #define SWEEP_STREAM_AUX 2  // cache policy of the E/W stores: nt (sm_sweep.hpp)
 #endif
+#ifndef EW_H16
+#define EW_H16 1  // census: f16 form of the packed recurrence
+#endif
 
 // NP packed u16 pairs -> LT bytes at byte offset off (u8: truncating pack; u16: as is)
 template <typename LT, int NP, int AUX = 0>
@@ -67,7 +70,11 @@ __global__ void __launch_bounds__(256) k_ew(EwArgs a)
     // volume stays below 2^32 bytes: the host's kMaxRecords guard)
     const uint32_t estep = dir ? (uint32_t)(-D) : (uint32_t)D;
     uint32_t e = ((uint32_t)y * (uint32_t)W1 + (uint32_t)(dir ? W1 - 1 : 0)) * (uint32_t)D + (uint32_t)(g * DPL);
-    const uint32_t P1p = (uint32_t)a.P1 * 0x10001u, P2 = (uint32_t)a.P2;
+    const uint32_t P1p = (uint32_t)a.P1 * 0x10001u, P2p = (uint32_t)a.P2 * 0x10001u;
+    // census (u8 costs): the f16 form of the recurrence (sm_pk.hpp sweep_step2)
+    constexpr bool H16 = sizeof(CT) == 1 && EW_H16;
+    constexpr uint32_t EDGE = H16 ? 0x7BFF7BFFu : (kBig | (kBig << 16));
+    const uint32_t eL = g == 0 ? EDGE : 0u, eR = g == VL - 1 ? EDGE : 0u;
 
     RawBytes<CB> ring[PF];
 #pragma unroll
@@ -94,7 +101,7 @@ __global__ void __launch_bounds__(256) k_ew(EwArgs a)
             for (int i = 0; i < NP; i++) asm volatile("" : "+v"(C[i])::"memory");
             ring[k].load(rc, s + PF < W1 ? (e + (uint32_t)PF * estep) * (uint32_t)sizeof(CT) : kOOB);
             uint32_t Ln[NP];
-            const uint32_t mn = sweep_step_pk<VL, NP>(Lp, minLp, C, P1p, P2, Ln);
+            const uint32_t mn = sweep_step2<VL, NP, H16>(Lp, minLp, C, P1p, P2p, eL, eR, Ln);  // minLp replicated
             store_pk<LT, NP, SWEEP_STREAM_AUX>(ro, (line_ok && s < W1) ? e * (uint32_t)sizeof(LT) : kOOB, Ln);
             e += estep;
 #pragma unroll

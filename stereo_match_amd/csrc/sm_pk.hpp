@@ -106,6 +106,107 @@ __device__ __forceinline__ uint32_t sweep_step_pk(const uint32_t (&Lp)[NP], uint
     return group_min<VL>(::min(mn & 0xFFFFu, mn >> 16));
 }
 
+// ---- census form: every census path value, partial and S sum is an integer below 2048
+// (L <= 62 + P2 <= 255, S <= 8 x 255), and for n < 2048 the u16 pattern n IS the f16 value
+// n * 2^-24 (a denormal below 1024, exponent 1 above; kernels keep f16 denormals,
+// .amdhsa_float_denorm_mode_16_64 3), so packed f16 add / sub / min are exact integer ops
+// on the unchanged u16 patterns (tools/ubench/f16_exact.hip checks every operand pair) and
+// gfx950's packed three-way minimum merges two steps of the recurrence.
+typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ h16x2 hv(uint32_t w) { return __builtin_bit_cast(h16x2, w); }
+__device__ __forceinline__ uint32_t hw(h16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+// IEEE-2019 minimum (no NaNs here): lowers to v_pk_minimum3_f16 without the operand
+// canonicalisation minNum needs, and adjacent minima fuse into one three-way instruction
+__device__ __forceinline__ uint32_t h2min(uint32_t a, uint32_t b) { return hw(__builtin_elementwise_minimum(hv(a), hv(b))); }
+__device__ __forceinline__ uint32_t h2min3(uint32_t a, uint32_t b, uint32_t c)
+{
+    return hw(__builtin_elementwise_minimum(__builtin_elementwise_minimum(hv(a), hv(b)), hv(c)));
+}
+__device__ __forceinline__ uint32_t h2add(uint32_t a, uint32_t b) { return hw(hv(a) + hv(b)); }
+__device__ __forceinline__ uint32_t h2sub(uint32_t a, uint32_t b) { return hw(hv(a) - hv(b)); }
+
+// sweep_step_pk on census values in the f16 form: per packed word alignbit, min, add P1,
+// minimum3 (Lp, minLp + P2), sub minLp, add C, and half a minimum3 for the row minimum
+template <int VL, int NP>
+__device__ __forceinline__ uint32_t sweep_step_h16(const uint32_t (&Lp)[NP], uint32_t minLp, const uint32_t (&C)[NP],
+                                                   uint32_t P1p, uint32_t P2, uint32_t (&Ln)[NP])
+{
+    constexpr uint32_t EDGE = 0x7BFF7BFFu;  // largest finite f16 (OpenCV's MAX_COST edge: above every L)
+    const uint32_t lm = Line<VL>::prev(EDGE, Lp[NP - 1]);
+    const uint32_t lq = Line<VL>::next(EDGE, Lp[0]);
+    const uint32_t mm = minLp * 0x10001u, dl = (minLp + P2) * 0x10001u;
+    uint32_t a1 = __builtin_amdgcn_alignbit(Lp[0], lm, 16);
+#pragma unroll
+    for (int k = 0; k < NP; k++) {
+        const uint32_t a2 = __builtin_amdgcn_alignbit(k + 1 < NP ? Lp[k + 1] : lq, Lp[k], 16);
+        const uint32_t v = h2min3(h2add(h2min(a1, a2), P1p), Lp[k], dl);
+        Ln[k] = h2add(h2sub(v, mm), C[k]);
+        a1 = a2;
+    }
+    uint32_t mn;
+    if constexpr (NP == 1) {
+        mn = Ln[0];
+    } else {
+        mn = h2min(Ln[0], Ln[1]);
+#pragma unroll
+        for (int k = 2; k < NP; k += 2) mn = k + 1 < NP ? h2min3(mn, Ln[k], Ln[k + 1]) : h2min(mn, Ln[k]);
+    }
+    return group_min<VL>(::min(mn & 0xFFFFu, mn >> 16));
+}
+
+// The fused sweeps' form of the step (u16 or, for census, the f16 form):
+//  * the row minimum travels replicated in both halves (m | m << 16): a lane's own
+//    minimum is min(w, swap(w)) and the cross-lane steps are plain u32 minima (on
+//    replicated words the u32 order is the order of m), so minLp + P2 is one packed add
+//    and minLp needs no repacking;
+//  * 16-lane lines take the d - 1 / d + 1 neighbours across lanes with zero-filling DPP
+//    moves OR'ed with the per-lane edge constants eL / eR (EDGE on the line's first /
+//    last lane, 0 elsewhere), which the compiler fuses into one v_or_b32_dpp each.
+template <int VL, int NP, bool H16>
+__device__ __forceinline__ uint32_t sweep_step2(const uint32_t (&Lp)[NP], uint32_t mmp, const uint32_t (&C)[NP],
+                                                uint32_t P1p, uint32_t P2p, uint32_t eL, uint32_t eR,
+                                                uint32_t (&Ln)[NP])
+{
+    constexpr uint32_t EDGE = H16 ? 0x7BFF7BFFu : (kBig | (kBig << 16));
+    uint32_t lm, lq;
+    if constexpr (VL == 16) {
+        lm = perm_dpp<DPP_ROW_SHR1>(Lp[NP - 1]) | eL;
+        lq = perm_dpp<DPP_ROW_SHL1>(Lp[0]) | eR;
+    } else if constexpr (VL == 8 || VL == 4) {  // lines inside a DPP row: the edge lanes select EDGE
+        lm = eL ? EDGE : perm_dpp<DPP_ROW_SHR1>(Lp[NP - 1]);
+        lq = eR ? EDGE : perm_dpp<DPP_ROW_SHL1>(Lp[0]);
+    } else {
+        lm = Line<VL>::prev(EDGE, Lp[NP - 1]);
+        lq = Line<VL>::next(EDGE, Lp[0]);
+    }
+    const uint32_t dl = H16 ? h2add(mmp, P2p) : pk_add(mmp, P2p);
+    uint32_t a1 = __builtin_amdgcn_alignbit(Lp[0], lm, 16);
+#pragma unroll
+    for (int k = 0; k < NP; k++) {
+        const uint32_t a2 = __builtin_amdgcn_alignbit(k + 1 < NP ? Lp[k + 1] : lq, Lp[k], 16);
+        if constexpr (H16) {
+            const uint32_t v = h2min3(h2add(h2min(a1, a2), P1p), Lp[k], dl);
+            Ln[k] = h2add(h2sub(v, mmp), C[k]);
+        } else {
+            uint32_t v = pk_min(pk_add(pk_min(a1, a2), P1p), Lp[k]);
+            v = pk_min(v, dl);
+            Ln[k] = pk_add(C[k], pk_sub(v, mmp));
+        }
+        a1 = a2;
+    }
+    uint32_t mn = Ln[0];
+    if constexpr (H16) {
+#pragma unroll
+        for (int k = 1; k < NP; k += 2) mn = k + 1 < NP ? h2min3(mn, Ln[k], Ln[k + 1]) : h2min(mn, Ln[k]);
+        mn = h2min(mn, __builtin_amdgcn_alignbit(mn, mn, 16));
+    } else {
+#pragma unroll
+        for (int k = 1; k < NP; k++) mn = pk_min(mn, Ln[k]);
+        mn = pk_min(mn, __builtin_amdgcn_alignbit(mn, mn, 16));
+    }
+    return group_min<VL>(mn);  // replicated halves: u32 minima are exact
+}
+
 // raw cost / E / W bytes of one lane -> NP packed pairs (u16 already pairs; u8 widened)
 template <typename CT, int DPL>
 __device__ __forceinline__ void unpack_ct_pk(const RawBytes<DPL * (int)sizeof(CT)>& r, uint32_t (&C)[DPL / 2])

@@ -1,13 +1,19 @@
 // sm_sweep.hip — translation unit of the fused-sweep kernels (sm_sweep.hpp):
 // instantiates k_sweep for every built (D, cost type, mode) and exposes a
 // plain host interface to sm_api.hip, so the units compile in parallel.  Built
-// once per (SWEEP_MODE, SWEEP_WIDE): the narrow strips (NCW 7, every D, plus the
-// k_sweep2 ablation and k_lr_rows) and the wide strips (wide_ncw, where built).
+// once per (SWEEP_MODE, SWEEP_WIDE): the narrow strips (NCW 7, every D, plus
+// k_lr_rows) and the wide strips (wide_ncw, where built).  The k_sweep2 ablation
+// (sm_sweep2.hpp) is compiled only into the ablation build (SM_ABLATIONS=1).
 #include <algorithm>
 
 #include "sm_sweep.hpp"
-#include "sm_sweep2.hpp"
 #include "sm_sweep_host.hpp"
+#ifndef SM_ABLATIONS
+#define SM_ABLATIONS 0
+#endif
+#if SM_ABLATIONS
+#include "sm_sweep2.hpp"
+#endif
 
 namespace smk {
 
@@ -110,7 +116,7 @@ struct LaunchF {
     }
 };
 
-#if !SWEEP_WIDE
+#if !SWEEP_WIDE && SM_ABLATIONS
 
 // column-per-lane sweeps (sm_sweep2.hpp, a measured ablation): built for u8 (census) costs
 // at D = 128; variant = compute waves per workgroup: 3 (16 columns per wave), 6 (8 columns)
@@ -159,7 +165,7 @@ hipError_t sweep2(int D, int ct_bytes, int variant, bool info, int device, Sweep
     }
 }
 
-#endif  // !SWEEP_WIDE
+#endif  // !SWEEP_WIDE && SM_ABLATIONS
 
 }  // namespace
 
@@ -182,8 +188,12 @@ hipError_t SW_CAT(sweep_launch_wide_m, SWEEP_MODE)(int D, int ct_bytes, const Sw
 #else
 hipError_t SW_CAT(sweep_info_m, SWEEP_MODE)(int D, int ct_bytes, int variant, int device, SweepInfo* out)
 {
+#if SM_ABLATIONS
     if (variant && sweep2(D, ct_bytes, variant, true, device, out, nullptr, 0, nullptr) == hipSuccess)
         return hipSuccess;
+#else
+    (void)variant;
+#endif
     InfoF f{device, out};
     return with_sweep(D, ct_bytes, f);
 }
@@ -191,10 +201,14 @@ hipError_t SW_CAT(sweep_info_m, SWEEP_MODE)(int D, int ct_bytes, int variant, in
 hipError_t SW_CAT(sweep_launch_m, SWEEP_MODE)(int D, int ct_bytes, int variant, const SweepArgs& a, int npairs,
                                               hipStream_t stream)
 {
+#if SM_ABLATIONS
     if (variant) {
         const hipError_t e = sweep2(D, ct_bytes, variant, false, 0, nullptr, &a, npairs, stream);
         if (e != hipErrorInvalidValue) return e;
     }
+#else
+    (void)variant;
+#endif
     LaunchF f{&a, dim3(a.nwg, npairs), stream};
     return with_sweep(D, ct_bytes, f);
 }

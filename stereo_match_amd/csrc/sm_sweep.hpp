@@ -44,6 +44,8 @@
 #include "sm_sweep_host.hpp"
 #include "sm_pk.hpp"
 
+#include <type_traits>
+
 namespace smk {
 
 typedef __attribute__((address_space(1))) unsigned long long gu64;
@@ -75,6 +77,10 @@ constexpr uint32_t SW_SPIN_LIMIT = 1u << 19;
 #ifndef SWEEP_U32
 #define SWEEP_U32 0
 #endif
+// census (u8 costs): the packed recurrence in the f16 form (sm_pk.hpp sweep_step_h16)
+#ifndef SWEEP_H16
+#define SWEEP_H16 1
+#endif
 
 // NCW: compute waves per workgroup (left halo, NCW-2 own, right halo).  Every strip
 // recomputes 2 halo waves' columns, so wider strips cost fewer instructions per own
@@ -95,18 +101,22 @@ struct SweepGeo {
     static constexpr int D = VL * DPL;
     static constexpr int NG = (DPL + 1) / 2;        // granules per lane (two u16 per granule)
     static constexpr int NGR = 64 * NG;             // granules per (strip, direction, block)
-    static constexpr int PF = 4;                    // rows of inputs in flight per lane
+    // rows of inputs in flight per lane (a divisor of HB: the ring slot is the row's index in
+    // its block); 2 where the wide strips' register budget needs it (12 waves, <= 168 VGPRs)
+    static constexpr int PF = (DPL >= 10 && NCW_ >= 11) ? 2 : 4;
+    static_assert(HB % PF == 0, "the input ring is indexed by the row within a block");
 };
 
 // wide strips where every mode's instance keeps its registers at the wide block size
-// (12 waves: <= 168 VGPRs, 14 waves: <= 128; round-2 builds): NCW 11 for u8 costs, 13 for
-// u16 costs where it fits, else 11; 0 = not built (the host also checks for scratch and
+// (12 waves: <= 168 VGPRs, 14 waves: <= 128): NCW 11 for u8 costs, 13 for u16 costs where
+// it fits (D = 128 needs up to 140 VGPRs in the per-role row loops of round 3: 11), else
+// 11; 0 = not built (the host also checks for scratch and
 // occupancy before it picks a wide instance, sm_sweep.hip)
 constexpr int wide_ncw(int D, int ct_bytes)
 {
     if (ct_bytes == 1) return (D <= 96 || D == 128 || D == 160 || D == 192) ? 11 : 0;
-    if (D == 16 || D == 32 || D == 96 || D == 128) return 13;
-    return (D == 48 || D == 80 || D == 160) ? 11 : 0;
+    if (D == 16 || D == 32 || D == 96) return 13;
+    return (D == 48 || D == 80 || D == 128 || D == 160) ? 11 : 0;
 }
 
 // NP packed words of one lane <-> LDS (widest aligned chunks)
@@ -262,6 +272,7 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
     // sgbm8 124.0 -> 120.8, census8 WTA sweep level (96.6 / 96.0); the 5-path WTA sweep is
     // slower with it (95.3 -> 97.9) and keeps the row barriers
     constexpr bool ROWSYNC = SWEEP_ROW_SYNC && MODE != 1;
+    constexpr bool PKMIN = DPL % 2 == 0 && !SWEEP_U32;  // packed loop: lmin words hold m | m << 16
     constexpr int LPW = G::LPW, NCW = G::NCW, HB = G::HB, NCOL = G::NCOL, COLS = G::COLS, CW = G::CW, D = G::D;
     constexpr int NG = G::NG, NGR = G::NGR, PF = G::PF;
     constexpr int CB = DPL * (int)sizeof(CT);  // cost / E / W bytes per lane and cell
@@ -328,6 +339,7 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
                         if (2 * tt + 1 < DPL) mn = min(mn, hi);
                     }
                     mn = group_min<VL / 2>(mn);  // over the VL/2 poller lanes of one column
+                    if (PKMIN) mn *= 0x10001u;   // the packed steps keep minLp replicated in both halves
                     if (need && (lane % (VL / 2)) == 0) lmin[wb][dir][col] = mn;
                 }
                 lds_barrier();
@@ -358,11 +370,15 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
     auto wait_row = [&](int s) {
         if (sync_dead) return;
         for (uint32_t spins = 0;; spins++) {
+            // both counters in flight at once (relaxed), one acquire for the pair
             const uint32_t nl = __builtin_amdgcn_readfirstlane(
-                __hip_atomic_load(&rowcnt[wl], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+                __hip_atomic_load(&rowcnt[wl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
             const uint32_t nr = __builtin_amdgcn_readfirstlane(
-                __hip_atomic_load(&rowcnt[wr], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
-            if (min(nl, nr) >= (uint32_t)s) return;
+                __hip_atomic_load(&rowcnt[wr], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+            if (min(nl, nr) >= (uint32_t)s) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+                return;
+            }
             if (spins >= SW_SPIN_LIMIT) {  // never expected: report, let the guarded fallback recompute
                 if (lane == 0) atomicOr(a.err, 1u);
                 sync_dead = true;
@@ -420,172 +436,191 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
         }
         if constexpr (MODE == 2) rp_[k].template load<SWEEP_STREAM_AUX>(rp, boff(eo, 2));
     };
-#pragma unroll
-    for (int k = 0; k < PF; k++) issue(k, k);
-
     if constexpr (DPL % 2 == 0 && !SWEEP_U32) {
-        // ---- packed u16-pair form (same steps as the u32 loop below)
+        // ---- packed u16-pair form (same steps as the u32 loop below), one straight-line
+        // row loop per wave role so the three directions of an own wave interleave:
+        //   wait for the neighbours' row s-1 -> LDS reads of the diagonal predecessors ->
+        //   V (no LDS input) while they land -> A, B -> LDS writes -> publish row s ->
+        //   the partial sum (down sweep) or S + WTA + uniqueness (WTA sweeps), which no
+        //   other wave waits for.
+        // Columns outside [0, W1) need no masking: their costs load as 0 (out-of-range
+        // buffer offsets), so a direction entering from outside the domain stays at the
+        // entering state (L = 0 + min(0, P1, P2) - 0 = 0), and the garbage a direction
+        // leaving the domain produces only flows further outward (A: rightward, B:
+        // leftward), never into a domain column or a published halo snapshot.
         constexpr int NP = DPL / 2;
-        const uint32_t P1p = P1 * 0x10001u;
-        uint32_t LVp[NP];
-#pragma unroll
-        for (int i = 0; i < NP; i++) LVp[i] = 0;
-        for (int b = 0; b < nblk; b++) {
-#pragma unroll
-            for (int j = 0; j < HB; j++) {
-                const int k = j % PF;
-                const int s = b * HB + j;
-                const bool live = s < H;
-                const int y = UP ? H - 1 - s : s;
-                const int rb = (s + 1) & 1, wb = s & 1;
-                const uint32_t e = live ? cell(y) : NONE;
-                uint32_t C[NP], Ein[NP], Win[NP], Pin[NP];
-                unpack_ct_pk<CT, DPL>(rc_[k], C);
-                if constexpr (WTA) {
-                    unpack_ct_pk<CT, DPL>(re_[k], Ein);
-                    unpack_ct_pk<CT, DPL>(rw_[k], Win);
+        const uint32_t P1p = P1 * 0x10001u, P2p = P2 * 0x10001u;
+        // line-edge constants of sweep_step2 (16-lane lines): EDGE on the first / last lane
+        constexpr uint32_t EDGE2 = (sizeof(CT) == 1 && SWEEP_H16) ? 0x7BFF7BFFu : (kBig | (kBig << 16));
+        const uint32_t eL = g == 0 ? EDGE2 : 0u, eR = g == VL - 1 ? EDGE2 : 0u;
+        // census sums stay below 2^11 (8 paths x (62 + P2 <= 193)): plain packed adds; u16
+        // costs saturate in OpenCV's order (normalize's domain keeps L <= 16383)
+        constexpr bool SAT = sizeof(CT) == 2;
+        constexpr bool H16 = !SAT && SWEEP_H16;  // census: f16 form of the recurrence and the sums
+        auto run = [&](auto role_c) {
+            constexpr int ROLE = decltype(role_c)::value;  // 0 left halo (A), 1 own (A, B, V), 2 right halo (B)
+            constexpr bool HAS_A = ROLE != 2, HAS_B = ROLE != 0, OWN = ROLE == 1;
+            auto issue_r = [&](int k, int s) {
+                const uint32_t en = s < H ? cell(UP ? H - 1 - s : s) : NONE;
+                rc_[k].template load<WTA ? SWEEP_COST_AUX : 0>(rc, boff(en, sizeof(CT)));
+                if constexpr (OWN && WTA) {
+                    re_[k].template load<SWEEP_STREAM_AUX>(re, boff(en, sizeof(CT)));
+                    rw_[k].template load<SWEEP_STREAM_AUX>(rw, boff(en, sizeof(CT)));
                 }
-                if constexpr (MODE == 2) unpack_ct_pk<uint16_t, DPL>(rp_[k], Pin);
+                if constexpr (OWN && MODE == 2) rp_[k].template load<SWEEP_STREAM_AUX>(rp, boff(en, 2));
+            };
 #pragma unroll
-                for (int i = 0; i < NP; i++) {  // before the refill (see the u32 loop)
-                    asm volatile("" : "+v"(C[i])::"memory");
-                    if constexpr (WTA) asm volatile("" : "+v"(Ein[i]), "+v"(Win[i])::"memory");
-                    if constexpr (MODE == 2) asm volatile("" : "+v"(Pin[i])::"memory");
-                }
-                issue(k, s + PF);
-                // E + W (+ the down partial): off the recurrences' dependency chain (saturating
-                // adds of non-negative values are associative, so the sum below is unchanged)
-                uint32_t EWP[NP];
-                if constexpr (WTA) {
+            for (int k = 0; k < PF; k++) issue_r(k, k);
+            uint32_t LVp[NP];
 #pragma unroll
-                    for (int i = 0; i < NP; i++) {
-                        EWP[i] = pk_adds(Ein[i], Win[i]);
-                        if constexpr (MODE == 2) EWP[i] = pk_adds(EWP[i], Pin[i]);
+            for (int i = 0; i < NP; i++) LVp[i] = 0;
+            uint32_t mVl = 0;
+            // d + 1 of each packed half of this lane (uniqueness window test)
+            uint32_t dpk[NP];
+#pragma unroll
+            for (int i = 0; i < NP; i++) dpk[i] = (uint32_t)(g * DPL + 2 * i + 1) * 0x10001u + 0x10000u;
+            for (int b = 0; b < nblk; b++) {
+#pragma unroll
+                for (int j = 0; j < HB; j++) {
+                    const int k = j % PF;
+                    const int s = b * HB + j;
+                    const bool live = s < H;
+                    const int y = UP ? H - 1 - s : s;
+                    const int rb = (s + 1) & 1, wb = s & 1;
+                    const uint32_t e = live ? cell(y) : NONE;
+                    uint32_t C[NP], Ein[NP], Win[NP], Pin[NP];
+                    unpack_ct_pk<CT, DPL>(rc_[k], C);
+                    if constexpr (OWN && WTA) {
+                        unpack_ct_pk<CT, DPL>(re_[k], Ein);
+                        unpack_ct_pk<CT, DPL>(rw_[k], Win);
                     }
-                }
-
-                if (ROWSYNC && j > 0) wait_row(s);
-                uint32_t nA[NP], nB[NP];
-                uint32_t mnA = 0, mnB = 0;
-                if (!halo_r) {
-                    uint32_t LA[NP];
-                    lds_get_pk<NP>(&lv[rb][0][c][g * DPL], LA);
-                    mnA = sweep_step_pk<VL, NP>(LA, lmin[rb][0][c], C, P1p, P2, nA);
-                    if (wave_ragged) {
+                    if constexpr (OWN && MODE == 2) unpack_ct_pk<uint16_t, DPL>(rp_[k], Pin);
 #pragma unroll
-                        for (int i = 0; i < NP; i++) nA[i] = active ? nA[i] : 0u;
-                        mnA = active ? mnA : 0u;
+                    for (int i = 0; i < NP; i++) {  // before the refill (see the u32 loop)
+                        asm volatile("" : "+v"(C[i])::"memory");
+                        if constexpr (OWN && WTA) asm volatile("" : "+v"(Ein[i]), "+v"(Win[i])::"memory");
+                        if constexpr (OWN && MODE == 2) asm volatile("" : "+v"(Pin[i])::"memory");
                     }
-                    lds_put_pk<NP>(&lv[wb][0][c + 1][g * DPL], nA);
-                    if (g == 0) lmin[wb][0][c + 1] = mnA;
-                }
-                if (!halo_l) {
-                    uint32_t LB[NP];
-                    lds_get_pk<NP>(&lv[rb][1][c + 2][g * DPL], LB);
-                    mnB = sweep_step_pk<VL, NP>(LB, lmin[rb][1][c + 2], C, P1p, P2, nB);
-                    if (wave_ragged) {
-#pragma unroll
-                        for (int i = 0; i < NP; i++) nB[i] = active ? nB[i] : 0u;
-                        mnB = active ? mnB : 0u;
+                    issue_r(k, s + PF);
+                    if (ROWSYNC && j > 0) wait_row(s);
+                    // diagonal predecessors: column c-1 (A) and c+1 (B) of the previous row
+                    uint32_t LA[NP], LB[NP], mA = 0, mB = 0;
+                    if constexpr (HAS_A) {
+                        lds_get_pk<NP>(&lv[rb][0][c][g * DPL], LA);
+                        mA = lmin[rb][0][c];
                     }
-                    lds_put_pk<NP>(&lv[wb][1][c + 1][g * DPL], nB);
-                    if (g == 0) lmin[wb][1][c + 1] = mnB;
-                }
-                if (j == HB - 1 && b + 1 < nblk) {
-                    const bool pa = wave == NCW - 2 && has_right, pb = wave == 1 && has_left;
-                    if (pa || pb) {
-                        const uint32_t tag = tag0 | (uint32_t)(b + 1);
-                        const uint32_t o = (uint32_t)((gbase(wg, pa ? 0 : 1, b) + (size_t)(kl * VL + g) * NG) * 8);
-#pragma unroll
-                        for (int q = 0; q < NG; q++)
-                            __builtin_amdgcn_raw_buffer_store_b64(u32x2{pa ? nA[q] : nB[q], tag}, rhop, o + 8 * q, 0, 16);
+                    if constexpr (HAS_B) {
+                        lds_get_pk<NP>(&lv[rb][1][c + 2][g * DPL], LB);
+                        mB = lmin[rb][1][c + 2];
                     }
-                }
-
-                uint32_t out[NP];
-#pragma unroll
-                for (int i = 0; i < NP; i++) out[i] = 0;
-                uint32_t recw = 0, nbw = 0;
-                bool wpx = false;
-                if (own) {
-                    uint32_t nV[NP];
-                    const uint32_t mnV = sweep_step_pk<VL, NP>(LVp, mV, C, P1p, P2, nV);
-#pragma unroll
-                    for (int i = 0; i < NP; i++) LVp[i] = nV[i];
-                    mV = mnV;
-                    if constexpr (MODE == 0) {
-#pragma unroll
-                        for (int i = 0; i < NP; i++) out[i] = pk_add(pk_add(nV[i], nA[i]), nB[i]);
+                    uint32_t nV[NP], nA[NP], nB[NP], mnV = 0, mnA = 0, mnB = 0;
+                    auto step = [&](const uint32_t(&Lp)[NP], uint32_t m, uint32_t(&Ln)[NP]) {
+                        return sweep_step2<VL, NP, H16>(Lp, m, C, P1p, P2p, eL, eR, Ln);
+                    };
+                    if constexpr (OWN) mnV = step(LVp, mVl, nV);
+                    if constexpr (HAS_A) mnA = step(LA, mA, nA);
+                    if constexpr (HAS_B) mnB = step(LB, mB, nB);
+                    if constexpr (HAS_A) {
+                        lds_put_pk<NP>(&lv[wb][0][c + 1][g * DPL], nA);
+                        if (g == 0) lmin[wb][0][c + 1] = mnA;
+                    }
+                    if constexpr (HAS_B) {
+                        lds_put_pk<NP>(&lv[wb][1][c + 1][g * DPL], nB);
+                        if (g == 0) lmin[wb][1][c + 1] = mnB;
+                    }
+                    // the row is published (neighbour counters) or, at a block end and
+                    // without row sync, closed by a barrier; the poller writes the halo
+                    // snapshot after the block-end barrier, while the waves run their WTA
+                    if (!ROWSYNC || j == HB - 1) {
+                        if (!(a.dbg & 4)) lds_barrier();
                     } else {
-                        uint32_t Sp[NP], S[DPL];
-                        uint32_t key = 0xFFFFFFFFu;
+                        publish_row(s);
+                    }
+                    if constexpr (OWN) {
 #pragma unroll
-                        for (int i = 0; i < NP; i++) {
-                            uint32_t t = pk_adds(pk_adds(nV[i], nA[i]), pk_adds(nB[i], EWP[i]));
-                            t = pk_min(t, 0x7FFF7FFFu);  // min(sum, 32767) (census sums stay below 2^11)
-                            Sp[i] = t;
-                            S[2 * i] = t & 0xFFFFu;
-                            S[2 * i + 1] = t >> 16;
-                            key = min(key, min((t << 16) | wta_rank(g * DPL + 2 * i, MODE == 1),
-                                               (t & 0xFFFF0000u) | wta_rank(g * DPL + 2 * i + 1, MODE == 1)));
-                        }
-                        lds_put_pk<NP>(&srow[(wave - 1) % (NCW - 2)][kl][g * DPL], Sp);
-                        key = group_min<VL>(key);
-                        const uint32_t minS = key >> 16;
-                        const int best = wta_unrank(key & 0xFFFF, MODE == 1);  // MODE 1 = 5 paths
-                        const int bm = max(best - 1, 0), bq = min(best + 1, D - 1);
-                        const uint32_t Sm = srow[(wave - 1) % (NCW - 2)][kl][bm];
-                        const uint32_t Sq = srow[(wave - 1) % (NCW - 2)][kl][bq];
-                        bool ok;
-                        if (ku > 0) {
-                            // uniqueness: S*ku < 100*minS  <=>  S < T = ceil(100*minS / ku); the
-                            // pixel passes iff only best-1, best, best+1 are below T, so count
-                            // the entries below T (packed) and compare with that window's count
-                            const uint32_t lim = minS * 100u;
-                            uint32_t T = 0xFFFFu;
-                            if (lim <= 0xFFFFu * (uint32_t)ku) {  // T < 2^16: float quotient, exact fix-up
-                                T = (uint32_t)((float)lim * a.inv_ku);
-                                T += __umul24(T, (uint32_t)ku) < lim ? 1u : 0u;
-                                T -= (T > 0 && __umul24(T - 1, (uint32_t)ku) >= lim) ? 1u : 0u;
+                        for (int i = 0; i < NP; i++) LVp[i] = nV[i];
+                        mVl = mnV;
+                        // snapshot of the block's last row for the neighbouring strips' halos
+                        if (j == HB - 1 && b + 1 < nblk) {
+                            const bool pa = wave == NCW - 2 && has_right, pb = wave == 1 && has_left;
+                            if (pa || pb) {
+                                const uint32_t tag = tag0 | (uint32_t)(b + 1);
+                                const uint32_t o = (uint32_t)((gbase(wg, pa ? 0 : 1, b) + (size_t)(kl * VL + g) * NG) * 8);
+#pragma unroll
+                                for (int q = 0; q < NG; q++)
+                                    __builtin_amdgcn_raw_buffer_store_b64(u32x2{pa ? nA[q] : nB[q], tag}, rhop, o + 8 * q,
+                                                                          0, 16);
                             }
-                            const uint32_t Tp = T * 0x10001u;
-                            uint32_t cp = 0;
-#pragma unroll
-                            for (int i = 0; i < NP; i++)
-                                cp = pk_add(cp, pk_min(pkw(__builtin_elementwise_sub_sat(pkv(Tp), pkv(Sp[i]))), 0x10001u));
-                            const uint32_t cnt = group_sum<VL>((cp & 0xFFFFu) + (cp >> 16));
-                            const uint32_t win = (minS < T ? 1u : 0u) + (best > 0 && Sm < T ? 1u : 0u) +
-                                                 (best < D - 1 && Sq < T ? 1u : 0u);
-                            ok = cnt == win;
-                        } else {
-                            uint32_t far = 0;
-                            const int gb = g * DPL - best + 1;
-#pragma unroll
-                            for (int i = 0; i < DPL; i++)
-                                far = max(far, (int)S[i] * ku < (int)minS * 100 ? (uint32_t)(gb + i) : 0u);
-                            far = group_max<VL>(far);
-                            ok = far <= 2u;
                         }
-                        ok = ok && minS < 32767u;
-                        recw = ok ? ((minS << 16) | (uint32_t)best) : 0xFFFFFFFFu;
-                        nbw = Sm | (Sq << 16);
-                        wpx = g == 0 && active && live;
+                        if constexpr (MODE == 0) {
+                            uint32_t out[NP];
+#pragma unroll
+                            for (int i = 0; i < NP; i++) out[i] = pk_add(pk_add(nV[i], nA[i]), nB[i]);
+                            bstore_n<uint32_t, NP, SWEEP_STREAM_AUX>(rp, boff(e, 2), out);
+                        } else {
+                            uint32_t Sp[NP];
+                            uint32_t key = 0xFFFFFFFFu;
+#pragma unroll
+                            for (int i = 0; i < NP; i++) {
+                                uint32_t t;
+                                if constexpr (SAT) {
+                                    uint32_t ew = pk_adds(Ein[i], Win[i]);
+                                    if constexpr (MODE == 2) ew = pk_adds(ew, Pin[i]);
+                                    t = pk_adds(pk_adds(nV[i], nA[i]), pk_adds(nB[i], ew));
+                                    t = pk_min(t, 0x7FFF7FFFu);  // min(sum, 32767)
+                                } else {
+                                    uint32_t ew = pk_add(Ein[i], Win[i]);
+                                    if constexpr (MODE == 2) ew = pk_add(ew, Pin[i]);
+                                    t = pk_add(pk_add(nV[i], nA[i]), pk_add(nB[i], ew));
+                                }
+                                Sp[i] = t;
+                                key = min(key, min((t << 16) | wta_rank(g * DPL + 2 * i, MODE == 1),
+                                                   (t & 0xFFFF0000u) | wta_rank(g * DPL + 2 * i + 1, MODE == 1)));
+                            }
+                            lds_put_pk<NP>(&srow[(wave - 1) % (NCW - 2)][kl][g * DPL], Sp);
+                            key = group_min<VL>(key);
+                            const uint32_t minS = key >> 16;
+                            const int best = wta_unrank(key & 0xFFFF, MODE == 1);  // MODE 1 = 5 paths
+                            const int bm = max(best - 1, 0), bq = min(best + 1, D - 1);
+                            const uint32_t Sm = srow[(wave - 1) % (NCW - 2)][kl][bm];
+                            const uint32_t Sq = srow[(wave - 1) % (NCW - 2)][kl][bq];
+                            // uniqueness: the pixel is rejected iff some d with |d - best| > 1 has
+                            // S[d]*(100-u) < 100*minS, i.e. iff m2 * ku < 100 * minS for m2 = the
+                            // minimum of S outside best-1..best+1.  The window's entries are pushed
+                            // to >= 0xFFFD (above every S <= 32767) before the minimum: t = d -
+                            // (best-1) in {0, 1, 2} exactly inside it, 3 - t (saturating) > 0 there,
+                            // times 0xFFFF = -(3 - t) mod 2^16.
+                            const uint32_t bm1p = (uint32_t)best * 0x10001u;  // t = (d + 1) - best = d - (best - 1)
+                            uint32_t m2p = 0xFFFFFFFFu;
+#pragma unroll
+                            for (int i = 0; i < NP; i++) {
+                                const uint32_t t = pk_sub(dpk[i], bm1p);
+                                const uint32_t w = pkw(__builtin_elementwise_sub_sat(pkv(0x00030003u), pkv(t)));
+                                const uint32_t mask = pkw(pkv(w) * pkv(0xFFFFFFFFu));
+                                m2p = pk_min(m2p, pk_adds(Sp[i], mask));
+                            }
+                            const uint32_t m2 = group_min<VL>(min(m2p & 0xFFFFu, m2p >> 16));
+                            const bool ok = !(__mul24((int)m2, ku) < __mul24((int)minS, 100)) && minS < 32767u;
+                            const uint32_t recw = ok ? ((minS << 16) | (uint32_t)best) : 0xFFFFFFFFu;
+                            const uint32_t nbw = Sm | (Sq << 16);
+                            const bool wpx = g == 0 && active && live;
+                            const uint32_t px = (uint32_t)y * (uint32_t)a.W + (uint32_t)(x1 + a.minX1);
+                            __builtin_amdgcn_raw_buffer_store_b32(recw, rrec, wpx ? px * 4 : kOOB, 0, 0);
+                            __builtin_amdgcn_raw_buffer_store_b32(nbw, rnb, wpx ? px * 4 : kOOB, 0, 0);
+                        }
                     }
                 }
-                if constexpr (MODE == 0) {
-                    bstore_n<uint32_t, NP, SWEEP_STREAM_AUX>(rp, own ? boff(e, 2) : kOOB, out);
-                } else {
-                    const uint32_t px = (uint32_t)y * (uint32_t)a.W + (uint32_t)(x1 + a.minX1);
-                    __builtin_amdgcn_raw_buffer_store_b32(recw, rrec, wpx ? px * 4 : kOOB, 0, 0);
-                    __builtin_amdgcn_raw_buffer_store_b32(nbw, rnb, wpx ? px * 4 : kOOB, 0, 0);
-                }
-                end_row(j, s);
+                if (b + 1 < nblk) lds_barrier();  // the poller has written the halo snapshot
             }
-            if (b + 1 < nblk) lds_barrier();
-        }
+        };
+        if (halo_l) run(std::integral_constant<int, 0>{});
+        else if (halo_r) run(std::integral_constant<int, 2>{});
+        else run(std::integral_constant<int, 1>{});
         return;
     }
 
+#pragma unroll
+    for (int k = 0; k < PF; k++) issue(k, k);
     for (int b = 0; b < nblk; b++) {
 #pragma unroll
         for (int j = 0; j < HB; j++) {

@@ -49,8 +49,41 @@ struct WlsConfArgs {
     int radius, lrc_thresh;
     float roll_off;
     int use_confidence;
+    int weights;     // 1: also write Ch / Cv (0: k_wls_weights wrote them)
     float tab[256];  // -exp(-k / sigma), k = |delta guide|
 };
+
+// The smoother's edge weights from the guide alone (the part of k_wls_conf that does not
+// need the disparity maps, so compute_disparity can run it, and the pivots, beside the
+// matchers).  One workgroup per padded ROI row and pair.
+__global__ void __launch_bounds__(256) k_wls_weights(WlsConfArgs a)
+{
+#pragma clang fp contract(off)
+    __shared__ float tab[256];
+    tab[threadIdx.x] = a.tab[threadIdx.x];
+    __syncthreads();
+    const int yr = blockIdx.x, pair = blockIdx.y;
+    const size_t ro = pair * a.roi_pair + (size_t)yr * a.wp;
+    float* Ch = a.Ch + ro;
+    float* Cv = a.Cv + ro;
+    const uint8_t* g = a.guide + pair * a.guide_pair + (size_t)(a.y0 + yr) * a.guide_stride + a.x0;
+    for (int j = threadIdx.x; j < a.wp; j += 256) {
+        float ch = 0.f, cv = 0.f;
+        if (yr < a.h && j < a.w) {
+            const int g0 = g[j];
+            if (j < a.w - 1) {
+                const int d = (int)g[j + 1] - g0;
+                ch = tab[d < 0 ? -d : d];
+            }
+            if (yr < a.h - 1) {
+                const int d = (int)g[j + a.guide_stride] - g0;
+                cv = tab[d < 0 ? -d : d];
+            }
+        }
+        Ch[j] = ch;
+        Cv[j] = cv;
+    }
+}
 
 // cv::borderInterpolate(BORDER_REFLECT_101): reflect until inside (a window
 // wider than the image reflects more than once)
@@ -97,7 +130,10 @@ __global__ void __launch_bounds__(256) k_wls_conf(WlsConfArgs a)
     float* Ch = a.Ch + ro;
     float* Cv = a.Cv + ro;
     if (yr >= a.h) {  // padding row
-        for (int j = threadIdx.x; j < a.wp; j += 256) num[j] = den[j] = Ch[j] = Cv[j] = 0.f;
+        for (int j = threadIdx.x; j < a.wp; j += 256) {
+            num[j] = den[j] = 0.f;
+            if (a.weights) Ch[j] = Cv[j] = 0.f;
+        }
         return;
     }
     const int y = a.y0 + yr;
@@ -106,21 +142,23 @@ __global__ void __launch_bounds__(256) k_wls_conf(WlsConfArgs a)
     const uint8_t* g = a.guide + pair * a.guide_pair + (size_t)y * a.guide_stride + a.x0;
     const int16_t* dlrow = dl + (size_t)y * a.W;
     __syncthreads();
-    for (int j = threadIdx.x; j < a.wp; j += 256) {  // smoother weights
-        float ch = 0.f, cv = 0.f;
-        if (j < a.w) {
-            const int g0 = g[j];
-            if (j < a.w - 1) {
-                const int d = (int)g[j + 1] - g0;
-                ch = tab[d < 0 ? -d : d];
+    if (a.weights) {  // smoother weights (skipped when k_wls_weights computed them ahead)
+        for (int j = threadIdx.x; j < a.wp; j += 256) {
+            float ch = 0.f, cv = 0.f;
+            if (j < a.w) {
+                const int g0 = g[j];
+                if (j < a.w - 1) {
+                    const int d = (int)g[j + 1] - g0;
+                    ch = tab[d < 0 ? -d : d];
+                }
+                if (yr < a.h - 1) {
+                    const int d = (int)g[j + a.guide_stride] - g0;
+                    cv = tab[d < 0 ? -d : d];
+                }
             }
-            if (yr < a.h - 1) {
-                const int d = (int)g[j + a.guide_stride] - g0;
-                cv = tab[d < 0 ? -d : d];
-            }
+            Ch[j] = ch;
+            Cv[j] = cv;
         }
-        Ch[j] = ch;
-        Cv[j] = cv;
     }
     if (!a.use_confidence) {
         for (int j = threadIdx.x; j < a.wp; j += 256) num[j] = j < a.w ? (float)dlrow[a.x0 + j] : 0.f;
@@ -373,6 +411,196 @@ __global__ void __launch_bounds__(64) k_fgs(FgsArgs a)
                 tile_to_lds<ROWS>(r0, U0, lane);
                 if (NRHS == 2) tile_to_lds<ROWS>(r1, U1, lane);
             }
+        }
+    }
+}
+
+// ---- the Thomas pivots on their own (round 3).  The elimination factors of
+// (I + lam L_w) depend only on the weights C and lam, not on the right-hand sides:
+//   r[j] = 1/(1 - lam(C[j-1]+C[j]) - lam C[j-1] c'[j-1]),  c'[j] = (lam C[j]) r[j]
+// k_fgs_pivots runs that chain (6 dependent operations per element) for every
+// iteration's lam at once and stores r and c'; k_fgs_solve then carries only the
+// right-hand sides (forward (f - lam C[j-1] d') r: 3 dependent operations; backward
+// d' - c' x: 2).  Same float32 operations in the same order as k_fgs / oracle/wls_np.py.
+struct FgsPivotArgs {
+    const float* C;     // Ch (ROWS) or Cv, [pair][hp][wp]
+    float* R;           // [it][pair][hp][wp] pivot reciprocals
+    float* IT;          // [it][pair][hp][wp] elimination factors c'
+    size_t roi_pair, var_stride;  // elements per pair, per iteration (= npairs * roi_pair)
+    int w, h, wp;
+    float lam[8];       // lam of each iteration (lam0 * att^it, float32 as the host iterates)
+};
+
+template <bool ROWS, bool FAST>
+__global__ void __launch_bounds__(64) k_fgs_pivots(FgsPivotArgs a)
+{
+#pragma clang fp contract(off)
+    __shared__ float Ct[FT * FP], RT[FT * FP], IT[FT * FP];
+    const int lane = threadIdx.x, it = blockIdx.y, pair = blockIdx.z;
+    const int n = ROWS ? a.w : a.h;
+    const int l0 = blockIdx.x * FT, wp = a.wp;
+    const uint64_t bytes = a.roi_pair * 4;
+    const rsrc_t C = make_rsrc(a.C + pair * a.roi_pair, bytes);
+    const size_t vo = (size_t)it * a.var_stride + pair * a.roi_pair;
+    const rsrc_t R = make_rsrc(a.R + vo, bytes);
+    const rsrc_t I = make_rsrc(a.IT + vo, bytes);
+    const uint32_t voff0 = tile_voff<ROWS>(l0, 0, wp, lane);
+    const uint32_t cstep = ROWS ? FT * 4 : (uint32_t)FT * wp * 4;
+    const float lam = a.lam[it];
+    const int nchunks = (n + FT - 1) / FT;
+    float4 rc[16];
+    tile_load<ROWS>(rc, C, voff0, wp);
+    tile_to_lds<ROWS>(rc, Ct, lane);
+    float ip = 0.f, cp = 0.f;
+    for (int c = 0; c < nchunks; c++) {
+        const int j0 = c * FT;
+        const bool next = c + 1 < nchunks;
+        __syncthreads();
+        if (next) tile_load<ROWS>(rc, C, voff0 + (c + 1) * cstep, wp);
+        const int m = min(FT, n - j0);
+#pragma unroll 4
+        for (int jj = 0; jj < m; jj++) {
+            const int t = TileMap<ROWS>::tix(lane, jj);
+            const float cj = Ct[t];
+            const float tt = 1.0f - lam * (cp + cj);
+            const float lcp = lam * cp;
+            const float r = pivot_rcp<FAST>(tt - lcp * ip);
+            ip = (lam * cj) * r;
+            RT[t] = r;
+            IT[t] = ip;
+            cp = cj;
+        }
+        __syncthreads();
+        const uint32_t vc = voff0 + c * cstep;
+        tile_store<ROWS>(R, vc, RT, wp, lane);
+        tile_store<ROWS>(I, vc, IT, wp, lane);
+        if (next) {
+            __syncthreads();
+            tile_to_lds<ROWS>(rc, Ct, lane);
+        }
+    }
+}
+
+struct FgsSolveArgs {
+    float* u[2];        // right-hand sides, [pair][hp][wp], solved in place
+    const float* C;     // edge weights along the solve direction (Ch or Cv)
+    const float* R;     // this iteration's pivot reciprocals [pair][hp][wp]
+    const float* IT;    // this iteration's elimination factors
+    size_t roi_pair;
+    int w, h, wp;
+    float lam;
+};
+
+// the right-hand-side sweeps of one pass given the pivots (64 lines per one-wave workgroup)
+template <int NRHS, bool ROWS>
+__global__ void __launch_bounds__(64) k_fgs_solve(FgsSolveArgs a)
+{
+#pragma clang fp contract(off)
+    __shared__ float Ct[FT * FP], RT[FT * FP], U0[FT * FP], U1[NRHS == 2 ? FT * FP : 1];
+    const int lane = threadIdx.x, pair = blockIdx.y;
+    const int n = ROWS ? a.w : a.h;
+    const int l0 = blockIdx.x * FT, wp = a.wp;
+    const uint64_t bytes = a.roi_pair * 4;
+    const rsrc_t u0 = make_rsrc(a.u[0] + pair * a.roi_pair, bytes);
+    const rsrc_t u1 = make_rsrc(a.u[NRHS == 2 ? 1 : 0] + pair * a.roi_pair, bytes);
+    const rsrc_t C = make_rsrc(a.C + pair * a.roi_pair, bytes);
+    const rsrc_t R = make_rsrc(a.R + pair * a.roi_pair, bytes);
+    const rsrc_t I = make_rsrc(a.IT + pair * a.roi_pair, bytes);
+    const uint32_t voff0 = tile_voff<ROWS>(l0, 0, wp, lane);
+    const uint32_t cstep = ROWS ? FT * 4 : (uint32_t)FT * wp * 4;
+    const float lam = a.lam;
+    const int nchunks = (n + FT - 1) / FT;
+    float4 rc[16], rr[16], r0[16], r1[16];
+    tile_load<ROWS>(rc, C, voff0, wp);
+    tile_load<ROWS>(rr, R, voff0, wp);
+    tile_load<ROWS>(r0, u0, voff0, wp);
+    if (NRHS == 2) tile_load<ROWS>(r1, u1, voff0, wp);
+    tile_to_lds<ROWS>(rc, Ct, lane);
+    tile_to_lds<ROWS>(rr, RT, lane);
+    tile_to_lds<ROWS>(r0, U0, lane);
+    if (NRHS == 2) tile_to_lds<ROWS>(r1, U1, lane);
+    float p0 = 0.f, p1 = 0.f, cp = 0.f;
+    for (int c = 0; c < nchunks; c++) {
+        const int j0 = c * FT;
+        const bool next = c + 1 < nchunks;
+        __syncthreads();
+        if (next) {  // prefetch chunk c+1 (consumed after the sweep)
+            const uint32_t vn = voff0 + (c + 1) * cstep;
+            tile_load<ROWS>(rc, C, vn, wp);
+            tile_load<ROWS>(rr, R, vn, wp);
+            tile_load<ROWS>(r0, u0, vn, wp);
+            if (NRHS == 2) tile_load<ROWS>(r1, u1, vn, wp);
+        }
+        const int m = min(FT, n - j0);
+#pragma unroll 8
+        for (int jj = 0; jj < m; jj++) {
+            const int t = TileMap<ROWS>::tix(lane, jj);
+            const float r = RT[t];
+            const float lcp = lam * cp;
+            p0 = (U0[t] - lcp * p0) * r;
+            U0[t] = p0;
+            if (NRHS == 2) {
+                p1 = (U1[t] - lcp * p1) * r;
+                U1[t] = p1;
+            }
+            cp = Ct[t];
+        }
+        __syncthreads();
+        const uint32_t vc = voff0 + c * cstep;
+        tile_store<ROWS>(u0, vc, U0, wp, lane);
+        if (NRHS == 2) tile_store<ROWS>(u1, vc, U1, wp, lane);
+        if (next) {
+            __syncthreads();
+            tile_to_lds<ROWS>(rc, Ct, lane);
+            tile_to_lds<ROWS>(rr, RT, lane);
+            tile_to_lds<ROWS>(r0, U0, lane);
+            if (NRHS == 2) tile_to_lds<ROWS>(r1, U1, lane);
+        }
+    }
+    // backward substitution; the last chunk's d' is still in LDS (RT takes c')
+    {
+        __syncthreads();
+        tile_load<ROWS>(rr, I, voff0 + (nchunks - 1) * cstep, wp);
+        tile_to_lds<ROWS>(rr, RT, lane);
+    }
+    for (int c = nchunks - 1; c >= 0; c--) {
+        const int j0 = c * FT;
+        const bool prev = c > 0;
+        __syncthreads();
+        if (prev) {
+            const uint32_t vp = voff0 + (c - 1) * cstep;
+            tile_load<ROWS>(rr, I, vp, wp);
+            tile_load<ROWS>(r0, u0, vp, wp);
+            if (NRHS == 2) tile_load<ROWS>(r1, u1, vp, wp);
+        }
+        const int m = min(FT, n - j0);
+        int jj = m - 1;
+        if (c == nchunks - 1) {  // x[n-1] = d'[n-1]
+            const int t = TileMap<ROWS>::tix(lane, jj);
+            p0 = U0[t];
+            if (NRHS == 2) p1 = U1[t];
+            jj--;
+        }
+#pragma unroll 8
+        for (; jj >= 0; jj--) {
+            const int t = TileMap<ROWS>::tix(lane, jj);
+            const float f = RT[t];
+            p0 = U0[t] - f * p0;
+            U0[t] = p0;
+            if (NRHS == 2) {
+                p1 = U1[t] - f * p1;
+                U1[t] = p1;
+            }
+        }
+        __syncthreads();
+        const uint32_t vc = voff0 + c * cstep;
+        tile_store<ROWS>(u0, vc, U0, wp, lane);
+        if (NRHS == 2) tile_store<ROWS>(u1, vc, U1, wp, lane);
+        if (prev) {
+            __syncthreads();
+            tile_to_lds<ROWS>(rr, RT, lane);
+            tile_to_lds<ROWS>(r0, U0, lane);
+            if (NRHS == 2) tile_to_lds<ROWS>(r1, U1, lane);
         }
     }
 }

@@ -9,6 +9,23 @@ if ROOT not in sys.path:
 
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
+# sm_set_debug_flags bits only the ablation build accepts (sm_api.hip kAblationFlags)
+ABLATION_FLAGS = 1 | 2 | 4 | 16 | 32 | 128 | (1 << 27) | 32768 | (7 << 24) | (1 << 28) | (1 << 29) | (1 << 31)
+
+
+def ablation_build() -> bool:
+    """True when the loaded library is the ablation build (make ablation)."""
+    from stereo_match_amd import _lib
+
+    return b"ablation" in (_lib.load().sm_version() or b"")
+
+
+def skip_unless_ablation(flags: int):
+    """Tests of measured ablations run only against libstereo_match_amd_ablate.so
+    (STEREO_MATCH_AMD_LIB); the product library rejects their flags."""
+    if flags & ABLATION_FLAGS and not ablation_build():
+        pytest.skip("ablation build only (make -C stereo_match_amd/csrc ablation)")
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (run with -m gpu on the GPU box)")

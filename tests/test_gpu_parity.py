@@ -9,6 +9,7 @@ import numpy as np
 import pytest
 
 from oracle import ref_c, sgm_np
+from conftest import skip_unless_ablation
 from stereo_match_amd import _lib, synthetic
 
 pytestmark = pytest.mark.gpu
@@ -56,6 +57,7 @@ def test_census_images_match_oracle(eng):
                                                 (0, 5, 64, 0), (1, 5, 128, 0), (1, 8, 64, 48), (0, 5, 128, 48),
                                                 (1, 8, 128, 1024), (1, 8, 128, 2048), (1, 8, 48, 1024)])
 def test_path_volumes_match_oracle(eng, cost, mode, D, flags):
+    skip_unless_ablation(flags)
     left, right, _ = synthetic.random_dot_pair(33, 101 + D, D, seed=8)
     p = dict(synthetic.headline_params(D) if cost else synthetic.parity_params(D), mode=mode)
     # flags 48 = fused row kernel (32) + keep its W volume (16), which it normally never writes;
@@ -97,7 +99,8 @@ def test_random_shapes_vs_c_oracle(eng, c, flags):
     default they need >= 3 pairs per launch group; one pair picks narrow strips
     where the strip-width model prefers them), on narrow strips everywhere
     (1 << 19) and on wide strips wherever built (1 << 21), and the hybrid engine
-    (32768, 5 and 8 paths)."""
+    (32768, 5 and 8 paths; ablation build)."""
+    skip_unless_ablation(flags)
     eng.set_debug_flags(flags)
     try:
         _random_case(eng, c)
@@ -150,6 +153,7 @@ def test_sgbm_cost_block_sizes(eng, bs, D, minD):
                                                   ("kitti", 1, 8, 16384 | (1 << 21)), ("kitti", 0, 5, 16384 | (1 << 21)),
                                                   ("kitti", 0, 8, 16384 | (1 << 21)), ("mccnn", 1, 8, 16384 | (1 << 21))])
 def test_full_size_bit_exact(eng, name, cost, mode, flags):
+    skip_unless_ablation(flags)
     H, W, D = synthetic.CONFIGS[name]
     left, right, gt = synthetic.random_dot_pair(H, W, D, seed=42)
     p = dict(synthetic.headline_params(D) if cost else synthetic.parity_params(D), mode=mode)
@@ -219,6 +223,7 @@ def test_batch_pipeline_groups(eng, flags):
     the sets."""
     import torch
 
+    skip_unless_ablation(flags)
     eng.set_debug_flags(flags)
     try:
         for (H, W, D, n) in [(70, 260, 64, 7), (90, 330, 128, 5)]:

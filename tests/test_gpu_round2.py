@@ -9,6 +9,7 @@ import numpy as np
 import pytest
 
 from oracle import ref_c, sgm_np, wls_np
+from conftest import ABLATION_FLAGS, ablation_build
 from stereo_match_amd import _lib, synthetic
 
 pytestmark = pytest.mark.gpu
@@ -228,9 +229,21 @@ def test_valid_result_flags_leave_compute_disparity_unchanged(eng, D):
     ref = eng.compute_disparity(gl, gr, prm, wp)
     for f in (8, 64, 128, 256, 1 << 12, 1 << 13, 1 << 14, (1 << 14) | 128, (1 << 14) | 256, (1 << 14) | (1 << 19), 1 << 15,
               1 << 19, 1 << 21, 1 << 22, 1 << 23, 1 << 27, 1 << 30, 2 << 16):
+        if f & ABLATION_FLAGS and not ablation_build():
+            continue
         eng.set_debug_flags(f)
         try:
             got = eng.compute_disparity(gl, gr, prm, wp)
         finally:
             eng.set_debug_flags(0)
         assert np.array_equal(got[0], ref[0]) and np.array_equal(got[1], ref[1]), f
+
+
+def test_product_library_rejects_ablation_flags(eng):
+    """The product library leaves the measured ablations out (SM_ABLATIONS=0)."""
+    if ablation_build():
+        pytest.skip("ablation build accepts them")
+    for f in (32768, 128, 1 << 27, 32, 1 << 24, 1 << 31):
+        with pytest.raises(_lib.SmError):
+            eng.set_debug_flags(f)
+    eng.set_debug_flags(0)

@@ -29,6 +29,9 @@ __global__ void k(uint32_t* out, uint32_t seed)
                 asm volatile("s_nop 1\n\tv_min_u32_dpp %0, %1, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1"
                              : "=v"(t) : "v"(v));
             else if constexpr (OP == 4) asm volatile("v_alignbit_b32 %0, %1, %2, 16" : "=v"(t) : "v"(v), "s"(s));
+            else if constexpr (OP == 6) asm volatile("v_pk_min_f16 %0, %1, %2" : "=v"(t) : "v"(v), "s"(s));
+            else if constexpr (OP == 7) asm volatile("v_pk_add_f16 %0, %1, %2" : "=v"(t) : "v"(v), "s"(s));
+            else if constexpr (OP == 8) asm volatile("v_pk_minimum3_f16 %0, %1, %2, %1" : "=v"(t) : "v"(v), "s"(s));
             else t = __builtin_amdgcn_perm(v, s, 0x05040100u);
             a[i] = t;
         }
@@ -85,6 +88,11 @@ int main()
     row<3, 8>("s_nop1+v_min_u32_dpp", d);
     row<4, 8>("v_alignbit_b32", d);
     row<5, 8>("v_perm_b32", d);
+    row<6, 1>("v_pk_min_f16", d);
+    row<6, 8>("v_pk_min_f16", d);
+    row<7, 8>("v_pk_add_f16", d);
+    row<8, 1>("v_pk_minimum3_f16", d);
+    row<8, 8>("v_pk_minimum3_f16", d);
     (void)hipFree(d);
     return 0;
 }
