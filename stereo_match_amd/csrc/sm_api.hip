@@ -1681,7 +1681,9 @@ int run_wls(sm_ctx* ctx, const int16_t* dl, const int16_t* dr, size_t disp_pair,
             ca.use_confidence = n.use_conf;
             ca.weights = 0;  // wls_prepare wrote Ch / Cv
             std::memcpy(ca.tab, n.tab, sizeof ca.tab);
-            hipLaunchKernelGGL(smk::k_wls_conf, dim3(hp, g), dim3(256), (size_t)(256 + n.w) * 4, ctx->stream, ca);
+            ca.separable = smk::wls_conf_lds(n.w, n.radius) <= 65536 ? 1 : 0;
+            hipLaunchKernelGGL(smk::k_wls_conf, dim3(hp, g), dim3(256),
+                               ca.separable ? smk::wls_conf_lds(n.w, n.radius) : (size_t)(256 + n.w) * 4, ctx->stream, ca);
             HIP_TRY(ctx, hipGetLastError());
             const int nrhs = n.use_conf ? 2 : 1;
             float lam = n.lam;

@@ -173,8 +173,11 @@ __device__ __forceinline__ uint32_t sweep_step2(const uint32_t (&Lp)[NP], uint32
         lm = perm_dpp<DPP_ROW_SHR1>(Lp[NP - 1]) | eL;
         lq = perm_dpp<DPP_ROW_SHL1>(Lp[0]) | eR;
     } else if constexpr (VL == 8 || VL == 4) {  // lines inside a DPP row: the edge lanes select EDGE
-        lm = eL ? EDGE : perm_dpp<DPP_ROW_SHR1>(Lp[NP - 1]);
-        lq = eR ? EDGE : perm_dpp<DPP_ROW_SHL1>(Lp[0]);
+        // the moves run in every lane BEFORE the select (inside a lane-divergent arm the
+        // edge lanes would be inactive sources and read as 0)
+        const uint32_t pm = perm_dpp<DPP_ROW_SHR1>(Lp[NP - 1]), pq = perm_dpp<DPP_ROW_SHL1>(Lp[0]);
+        lm = eL ? EDGE : pm;
+        lq = eR ? EDGE : pq;
     } else {
         lm = Line<VL>::prev(EDGE, Lp[NP - 1]);
         lq = Line<VL>::next(EDGE, Lp[0]);

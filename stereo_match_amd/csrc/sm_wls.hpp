@@ -50,6 +50,7 @@ struct WlsConfArgs {
     float roll_off;
     int use_confidence;
     int weights;     // 1: also write Ch / Cv (0: k_wls_weights wrote them)
+    int separable;   // 1: box sums through LDS column sums (wls_conf_lds bytes of dynamic LDS)
     float tab[256];  // -exp(-k / sigma), k = |delta guide|
 };
 
@@ -116,12 +117,60 @@ __device__ inline float discontinuity_conf(const int16_t* __restrict__ d, int H,
     return c > 0.0f ? c : 0.0f;
 }
 
+// discontinuity_conf for n consecutive columns xs.. of row y, separably: the column
+// sums of the window's 2r+1 rows (reflect-101) for the n + 2r columns the windows
+// touch, then 2r+1-wide horizontal sums of those (integer sums: the same values as
+// discontinuity_conf's loop in any order).  Writes out[0..n) (LDS); cs / cs2 hold
+// n + 2r column sums.  All threads of the workgroup take part (barriers inside).
+__device__ inline void conf_row(const int16_t* __restrict__ d, int H, int W, int y, int xs, int n, int r, double scale,
+                                float roll_off, float* out, int* cs, long long* cs2)
+{
+#pragma clang fp contract(off)
+    const int m = n + 2 * r;
+    for (int i = threadIdx.x; i < m; i += blockDim.x) {
+        const int x = reflect101(xs - r + i, W);
+        int s = 0;
+        long long s2 = 0;
+        for (int dy = -r; dy <= r; dy++) {
+            const int v = d[(size_t)reflect101(y + dy, H) * W + x];
+            s += v;
+            s2 += (long long)v * v;
+        }
+        cs[i] = s;
+        cs2[i] = s2;
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < n; j += blockDim.x) {
+        int s = 0;
+        long long s2 = 0;
+        for (int k = 0; k <= 2 * r; k++) {
+            s += cs[j + k];
+            s2 += cs2[j + k];
+        }
+        const float mm = (float)((double)s * scale);
+        const float m2 = (float)((double)s2 * scale);
+        const float var = m2 - mm * mm;
+        const float c = 1.0f - roll_off * var;
+        out[j] = c > 0.0f ? c : 0.0f;
+    }
+    __syncthreads();
+}
+
+// dynamic LDS: tab[256], confr[w], confl[w], column sums cs[w + 2r] (int), cs2 (int64)
+__host__ __device__ inline size_t wls_conf_lds(int w, int r)
+{
+    return ((size_t)(256 + 2 * w) * 4 + 7) / 8 * 8 + (size_t)(w + 2 * r) * 12 + 16;
+}
+
 __global__ void __launch_bounds__(256) k_wls_conf(WlsConfArgs a)
 {
 #pragma clang fp contract(off)
-    extern __shared__ uint32_t smem[];  // tab[256], right-view confidence of this row [w]
+    extern __shared__ uint32_t smem[];  // tab[256], right / left confidence of this row [w], column sums
     float* tab = reinterpret_cast<float*>(smem);
     float* confr = tab + 256;
+    float* confl = confr + a.w;
+    long long* cs2 = reinterpret_cast<long long*>(smem + ((256 + 2 * a.w) + 1) / 2 * 2);
+    int* cs = reinterpret_cast<int*>(cs2 + (a.w + 2 * a.radius));
     for (int i = threadIdx.x; i < 256; i += 256) tab[i] = a.tab[i];
     const int yr = blockIdx.x, pair = blockIdx.y;
     const size_t ro = pair * a.roi_pair + (size_t)yr * a.wp;
@@ -165,9 +214,14 @@ __global__ void __launch_bounds__(256) k_wls_conf(WlsConfArgs a)
         return;
     }
     const double scale = 1.0 / (double)((2 * a.radius + 1) * (2 * a.radius + 1));
-    for (int j = threadIdx.x; j < a.w; j += 256)
-        confr[j] = discontinuity_conf(dr, a.H, a.W, y, a.rx0 + j, a.radius, scale, a.roll_off);
-    __syncthreads();
+    if (a.separable) {
+        conf_row(dr, a.H, a.W, y, a.rx0, a.w, a.radius, scale, a.roll_off, confr, cs, cs2);
+        conf_row(dl, a.H, a.W, y, a.x0, a.w, a.radius, scale, a.roll_off, confl, cs, cs2);
+    } else {  // rows too wide for the column sums in LDS: per pixel (tab + confr only)
+        for (int j = threadIdx.x; j < a.w; j += 256)
+            confr[j] = discontinuity_conf(dr, a.H, a.W, y, a.rx0 + j, a.radius, scale, a.roll_off);
+        __syncthreads();
+    }
     const int16_t* drrow = dr + (size_t)y * a.W;
     for (int j = threadIdx.x; j < a.wp; j += 256) {
         if (j >= a.w) {
@@ -175,7 +229,7 @@ __global__ void __launch_bounds__(256) k_wls_conf(WlsConfArgs a)
             continue;
         }
         const int X = a.x0 + j;
-        float c = discontinuity_conf(dl, a.H, a.W, y, X, a.radius, scale, a.roll_off);
+        float c = a.separable ? confl[j] : discontinuity_conf(dl, a.H, a.W, y, X, a.radius, scale, a.roll_off);
         const int d = dlrow[X];
         const int ri = X - (d >> 4);
         if (ri >= a.rx0 && ri < a.rx0 + a.w) {
@@ -298,7 +352,11 @@ __device__ inline void tile_store(rsrc_t rs, uint32_t voff, const float* T, int 
         v[1] = __float_as_uint(T[TileMap<ROWS>::tix_e(ll, pl, 1)]);
         v[2] = __float_as_uint(T[TileMap<ROWS>::tix_e(ll, pl, 2)]);
         v[3] = __float_as_uint(T[TileMap<ROWS>::tix_e(ll, pl, 3)]);
-        __builtin_amdgcn_raw_buffer_store_b128(v, rs, voff, k * 16 * wp, 0);
+        // the offset goes into the VGPR, soffset stays the literal 0: the compiler's hazard
+        // recognizer treats a >64-bit MUBUF store with an SGPR soffset as free of the
+        // store-data hazard and lets the next VALU overwrite the data VGPRs at once, which on
+        // gfx950 under load stored those new values (addresses) instead of the tile
+        __builtin_amdgcn_raw_buffer_store_b128(v, rs, voff + (uint32_t)(k * 16 * wp), 0, 0);
     }
 }
 

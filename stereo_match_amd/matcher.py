@@ -152,12 +152,12 @@ def _check_pair(left, right, colour=False):
         raise ValueError("left and right images must have the same size and type")
     if left.dtype != np.uint8:
         raise ValueError("images must be CV_8U (uint8)")
+    if left.ndim not in (2, 3) or left.size == 0:
+        raise ValueError("images must be non-empty 2-D arrays")
     if left.ndim == 3 and colour and left.shape[2] == 1:
         return
     if left.ndim == 3 and not (colour and left.shape[2] == 3):
         raise ValueError("images must be gray (H, W)" + (" or BGR (H, W, 3)" if colour else ""))
-    if left.ndim not in (2, 3) or left.size == 0:
-        raise ValueError("images must be non-empty 2-D arrays")
 
 
 def _compute_torch(left, right, prm: SmParams):

@@ -194,3 +194,43 @@ def test_hypothesis_wls_vs_oracle(eng, H, W, lo, ro, to, bo, r, lam, sigma, lrc,
              min_disp=int(rng.integers(-3, 3)))
     out = eng.wls_filter(displ, guide, dispr if conf else None, wls_params(p, H, W))
     assert np.array_equal(out, wls_np.wls_filter(displ, guide, dispr if conf else None, p))
+
+
+def test_compute_disparity_repeatable_with_side_stream_prepare():
+    """The WLS guide-only work (weights, pivots) runs on its own stream beside the two
+    matchers; every call must give the filter-alone result.  This caught a store-data
+    hazard (sm_wls.hpp tile_store) that only showed with kernels running side by side."""
+    import torch
+
+    import stereo_match_amd as sm
+    from stereo_match_amd import wls
+    from stereo_match_amd.stereo_vision import matcher_from_settings
+
+    for D in (64, 128):
+        s = dict(sm.DEFAULT_SETTINGS, window_size=5, num_disparities=D)
+        H, W = 120, 420
+        gl, gr, _ = synthetic.random_dot_pair(H, W, D, seed=D + 3)
+        lm = matcher_from_settings(s)
+        prm = lm.params()
+        wf = wls.createDisparityWLSFilter(lm)
+        wf.setLambda(s["lmbda"])
+        wf.setSigmaColor(s["sigma"])
+        wp = wf.params(H, W)
+        eng = _lib.Engine(0)
+        try:
+            L = torch.tensor(gl, device="cuda")
+            R = torch.tensor(gr, device="cuda")
+            dl = torch.empty((H, W), dtype=torch.int16, device="cuda")
+            dr = torch.empty_like(dl)
+            fo = torch.empty_like(dl)
+            first = None
+            for i in range(12):
+                eng.compute_disparity_batch_device(L.data_ptr(), R.data_ptr(), 1, H * W, H, W, W, prm, wp,
+                                                   dl.data_ptr(), dr.data_ptr(), fo.data_ptr())
+                eng.synchronize()
+                if first is None:
+                    first = (dl.cpu().numpy(), dr.cpu().numpy())
+                    alone = eng.wls_filter(first[0], gl, first[1], wp)
+                assert np.array_equal(fo.cpu().numpy(), alone), (D, i)
+        finally:
+            eng.close()

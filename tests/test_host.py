@@ -102,6 +102,8 @@ def test_wls_factory_mutates_left_matcher_like_ximgproc():
     (np.zeros((4, 40), np.uint16), np.zeros((4, 40), np.uint16), ValueError),
     (np.zeros((0, 40), np.uint8), np.zeros((0, 40), np.uint8), ValueError),
     (np.zeros((4, 40, 2), np.uint8), np.zeros((4, 40, 2), np.uint8), ValueError),  # gray or BGR only
+    (np.zeros((0, 40, 1), np.uint8), np.zeros((0, 40, 1), np.uint8), ValueError),  # empty single-channel 3-D
+    (np.zeros((4, 40, 3, 1), np.uint8), np.zeros((4, 40, 3, 1), np.uint8), ValueError),
 ])
 def test_bad_inputs_raise_before_gpu(left, right, exc):
     with pytest.raises(exc):
