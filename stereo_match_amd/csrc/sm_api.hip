@@ -678,9 +678,9 @@ int stream_cus(hipStream_t st, int ncu)
 int ensure_sweep_err(sm_ctx* ctx)
 {
     if (ctx->sweep_err.p) return SM_OK;
-    int rc = ensure(ctx, ctx->sweep_err, 256);
+    int rc = ensure(ctx, ctx->sweep_err, SWEEP_STATS ? (size_t(8) << 20) : 256);
     if (rc != SM_OK) return rc;
-    HIP_TRY(ctx, hipMemsetAsync(ctx->sweep_err.p, 0, 256, ctx->stream));
+    HIP_TRY(ctx, hipMemsetAsync(ctx->sweep_err.p, 0, SWEEP_STATS ? (size_t(8) << 20) : 256, ctx->stream));
     return SM_OK;
 }
 
@@ -814,6 +814,9 @@ int sweep_pass(sm_ctx* ctx, const Norm& n, const Geo& g, const SweepJob& j, int 
         a.inv_ku = n.uniq < 100 ? 1.0f / (float)(100 - n.uniq) : 0.f;
         a.nwg = nwg;
         a.epoch = ctx->hop_epoch;
+#if SWEEP_STATS
+        a.stats = (unsigned long long*)((char*)ctx->sweep_err.p + 1024);
+#endif
         a.dbg = (ctx->dbg_flags >> 24) & 7;  // timing ablations (results wrong): 1 no polls
         HIP_TRY(ctx, smk::sweep_launch(n.D, (int)elem_bytes(n), mode, si.impl, a, np, ctx->stream));
     }
@@ -1040,9 +1043,10 @@ int launch_sgbm_cost2(sm_ctx* ctx, const Norm& n, const Geo& g, const smk::SgbmC
 int group_size(const sm_ctx* ctx, const Norm& n, int H, int npairs, bool sweep, bool hybrid)
 {
     const size_t cells = (size_t)H * std::max(n.width1, 1) * n.D;
-    // sweep engine: E + W volumes (+ the u16 partial at 8 paths); hybrid: 5 volumes + the
-    // partial; else one volume per direction
-    const size_t per = sweep    ? cells * (2 * elem_bytes(n) + (n.ndirs == 8 ? 2 : 0))
+    // sweep engine: a slot per direction (E and W, and every other direction's volume the
+    // guarded fallback writes: run_pairs' L_pair) + the u16 partial at 8 paths; hybrid: 5
+    // volumes + the partial; else one volume per direction
+    const size_t per = sweep    ? cells * (n.ndirs * elem_bytes(n) + (n.ndirs == 8 ? 2 : 0))
                        : hybrid ? cells * (hybrid_slots(n) * elem_bytes(n) + 2)
                                 : cells * elem_bytes(n) * n.ndirs;
     size_t g = std::max<size_t>(1, kSetBudget / std::max<size_t>(per, 1));
@@ -1219,8 +1223,12 @@ int run_wide(sm_ctx* ctx, const Src& src, const Geo& g, const Norm& n, BufSet& b
         wa.P2 = n.P2;
         wa.hh = n.mode == SM_MODE_HH;
         constexpr int TX = 64;
-        hipLaunchKernelGGL((smk::k_wide_hsum<TX>), dim3((n.width1 + TX - 1) / TX, H, G), dim3(256),
-                           (size_t)(TX + 2 * wa.SW2) * n.D * 2, ctx->stream, wa);
+        // a window sum past 32767 makes OpenCV's saturating running sums differ from the window sums
+        if ((long long)(2 * wa.SW2 + 1) * n.cn * (2 * n.ftzero + 63) > 32767)
+            hipLaunchKernelGGL(smk::k_wide_hsum_scan, dim3(H, G), dim3(256), 0, ctx->stream, wa);
+        else
+            hipLaunchKernelGGL((smk::k_wide_hsum<TX>), dim3((n.width1 + TX - 1) / TX, H, G), dim3(256),
+                               (size_t)(TX + 2 * wa.SW2) * n.D * 2, ctx->stream, wa);
         HIP_TRY(ctx, hipGetLastError());
         hipLaunchKernelGGL(smk::k_wide_vscan, dim3((unsigned)((g.vol / H + 255) / 256), G), dim3(256), 0,
                            ctx->stream, wa);
@@ -1975,6 +1983,8 @@ void sm_destroy(sm_ctx* ctx)
     delete ctx;
 }
 
+// The twin context (compute_disparity's right matcher) keeps its own stream on purpose:
+// it forks from and joins back into this ctx->stream by events, whichever stream that is.
 int sm_set_stream(sm_ctx* ctx, void* hip_stream)
 {
     if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
@@ -2569,7 +2579,12 @@ int sm_set_cu_mask(sm_ctx* ctx, const uint32_t* mask, int nwords)
     if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
     if (nwords < 0 || (nwords > 0 && !mask)) return fail(ctx, SM_E_ARG, "bad CU mask");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    HIP_TRY(ctx, hipDeviceSynchronize());
+    // the streams about to be replaced drain first (this context's only: other contexts'
+    // and the caller's unrelated work keep running; the twin drains its own below)
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->own_stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->side));
+    if (ctx->wls_stream) HIP_TRY(ctx, hipStreamSynchronize(ctx->wls_stream));
     hipStream_t a = nullptr, b = nullptr;
     if (nwords > 0) {
         HIP_TRY(ctx, hipExtStreamCreateWithCUMask(&a, (uint32_t)nwords, mask));
@@ -2676,8 +2691,34 @@ long long sm_debug_fetch(sm_ctx* ctx, int what, void* host, size_t bytes)
     case 1: need = vol * et * ctx->last_ndirs; break;
     case 2: need = img * 2; break;
     case 3: need = img * 16; break;
+#if SWEEP_STATS
+    case 20: need = 24 * 8; break;  // sm_sweep.hpp SWEEP_STATS counters (read and cleared)
+    case 21: need = 2048; break;    // the down sweep's workgroups' XCC ids (| 0x80), by linear id
+    case 22: need = 6 * 65536 * 8; break;  // snapshot publish / observe times (s_memrealtime)
+#endif
     default: return fail(ctx, SM_E_ARG, "debug item %d unknown", what);
     }
+#if SWEEP_STATS
+    if (what == 22 && host) {
+        HIP_TRY(ctx, hipDeviceSynchronize());
+        if (!ctx->sweep_err.p) return 0;
+        HIP_TRY(ctx, hipMemcpy(host, (char*)ctx->sweep_err.p + 1024 + 1024 * 8, need, hipMemcpyDeviceToHost));
+        return (long long)need;
+    }
+    if (what == 21 && host) {
+        HIP_TRY(ctx, hipDeviceSynchronize());
+        if (!ctx->sweep_err.p) return 0;
+        HIP_TRY(ctx, hipMemcpy(host, (char*)ctx->sweep_err.p + 1024 + 1024, need, hipMemcpyDeviceToHost));
+        return (long long)need;
+    }
+    if (what == 20 && host) {
+        HIP_TRY(ctx, hipDeviceSynchronize());
+        if (!ctx->sweep_err.p) return 0;
+        HIP_TRY(ctx, hipMemcpy(host, (char*)ctx->sweep_err.p + 1024, need, hipMemcpyDeviceToHost));
+        HIP_TRY(ctx, hipMemset((char*)ctx->sweep_err.p + 1024, 0, need));
+        return (long long)need;
+    }
+#endif
     if (!host) return (long long)need;
     if (bytes < need) return fail(ctx, SM_E_ARG, "host buffer too small (%zu < %zu)", bytes, need);
     if (need == 0) return 0;

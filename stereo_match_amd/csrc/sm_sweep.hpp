@@ -52,6 +52,18 @@ typedef __attribute__((address_space(1))) unsigned long long gu64;
 
 constexpr uint32_t SW_SPIN_LIMIT = 1u << 19;
 
+// SWEEP_STATS builds (tools/build_variant.sh): shader-clock cycles each wave spends in
+// the row / block synchronisation, summed per mode into SweepArgs::stats[8 * MODE + k]:
+// 0 poller in polls, 1 poller in barriers, 2 compute waves in wait_row, 3 compute waves
+// in block barriers, 4 compute waves' lifetime, 5 compute waves, 6 poller lifetime
+#if SWEEP_STATS
+#define SW_T0(v) const uint64_t v = __builtin_readcyclecounter()
+#define SW_ACC(acc, v) acc += __builtin_readcyclecounter() - v
+#else
+#define SW_T0(v) (void)0
+#define SW_ACC(acc, v) (void)0
+#endif
+
 // cache policy of the sweeps' read-once streams (E/W and partial loads, partial and E/W
 // stores): nt (2) keeps them from evicting the cost volume the other passes re-read (census8
 // sweeps 259.5 -> 256.1, sgbm5 259.8 -> 257.9, sgbm8 328.7 -> 323.9 us per pair); 0 = default
@@ -236,20 +248,83 @@ __device__ __forceinline__ void lds_barrier()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
+// Strip placement: workgroups are dispatched to the 8 XCDs round-robin by linear id
+// (from an offset that carries over between launches), so the (strip, pair) of a
+// workgroup is taken from its linear id such that one pair's strips share a residue
+// mod 8, i.e. one XCD and its L2: the halo hand-offs then stay inside that L2
+// (SWEEP_XCD_MAP; the protocol stays correct for any placement, see poll_granules).
+#ifndef SWEEP_XCD_MAP
+#define SWEEP_XCD_MAP 0  // measured: census8 3475 vs 4713 pairs per second (one pair per XCD is slower)
+#endif
+// first-phase poll loads (same-XCD source strips): cache policy bits of the
+// buffer load (1 = sc0: past the CU's L1, served by the shared L2); 0 = no first phase
+#ifndef SWEEP_POLL_FAST_AUX
+#define SWEEP_POLL_FAST_AUX 0  // sc0 polls never saw the sc1 snapshot stores (516 pairs per second)
+#endif
+#ifndef SWEEP_POLL_FAST_SPINS
+#define SWEEP_POLL_FAST_SPINS 256
+#endif
+// the strip's boundary waves publish their snapshot before the block-end barrier (1; 0:
+// after it), and with 2 the poller also polls the neighbours' before that barrier
+#ifndef SWEEP_EARLY_XCHG
+#define SWEEP_EARLY_XCHG 1
+#endif
+
+__device__ __forceinline__ void sweep_place(int nwg, int& strip, int& pair)
+{
+    if (!SWEEP_XCD_MAP) {
+        strip = blockIdx.x;
+        pair = blockIdx.y;
+        return;
+    }
+    const uint32_t n = (uint32_t)nwg * gridDim.y;
+    const uint32_t lin = blockIdx.x + blockIdx.y * (uint32_t)nwg;
+    const uint32_t r = lin % 8u, q = lin / 8u, base = n / 8u, extra = n % 8u;
+    const uint32_t w = r * base + min(r, extra) + q;  // pair-major item of residue class r
+    strip = (int)(w % (uint32_t)nwg);
+    pair = (int)(w / (uint32_t)nwg);
+}
+
+// the linear id sweep_place gives item (strip, pair) (same-XCD test of two strips)
+__device__ __forceinline__ uint32_t sweep_lin(int nwg, int strip, int pair)
+{
+    const uint32_t n = (uint32_t)nwg * gridDim.y, base = n / 8u, extra = n % 8u;
+    const uint32_t w = (uint32_t)pair * (uint32_t)nwg + (uint32_t)strip;
+    // residue class r holds items [r*base + min(r, extra), ... + base + (r < extra))
+    const uint32_t big = extra * (base + 1);
+    const uint32_t r = w < big ? w / (base + 1) : extra + (w - big) / max(base, 1u);
+    const uint32_t q = w - (r * base + min(r, extra));
+    return q * 8u + r;
+}
+
 // Poll N granules of one lane until every tag equals `tag` (lanes with !need
-// do not load).  Wave-uniform exit; gives up after SW_SPIN_LIMIT passes.
+// do not load).  Wave-uniform exit; gives up after SW_SPIN_LIMIT passes.  With
+// fast (the source strip runs on this XCD), the first SWEEP_POLL_FAST_SPINS passes
+// load through the XCD's L2 (the producer's sc1 store writes it through); a stale
+// line there (the source on another XCD after all) cannot carry the awaited tag,
+// so correctness never depends on the placement: the later passes load sc1.
+// (rs, off: the same granules as a wave-uniform buffer resource + this lane's byte offset)
 template <int N>
 __device__ __forceinline__ void poll_granules(const gu64* src, bool need, uint32_t tag, uint32_t (&v)[N], bool& dead,
-                                              uint32_t* err)
+                                              uint32_t* err, bool fast, rsrc_t rs, uint32_t off)
 {
     for (uint32_t spins = 0;; spins++) {
         bool ok = true;
         if (need) {
+            if (SWEEP_POLL_FAST_AUX && fast && spins < SWEEP_POLL_FAST_SPINS) {
 #pragma unroll
-            for (int k = 0; k < N; k++) {
-                const unsigned long long x = __hip_atomic_load(src + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                v[k] = (uint32_t)x;
-                ok &= (uint32_t)(x >> 32) == tag;
+                for (int k = 0; k < N; k++) {
+                    const u32x2 x = __builtin_amdgcn_raw_buffer_load_b64(rs, off + k * 8, 0, SWEEP_POLL_FAST_AUX);
+                    v[k] = x[0];
+                    ok &= x[1] == tag;
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < N; k++) {
+                    const unsigned long long x = __hip_atomic_load(src + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    v[k] = (uint32_t)x;
+                    ok &= (uint32_t)(x >> 32) == tag;
+                }
             }
         }
         if (__all(ok) || dead) return;
@@ -292,7 +367,8 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
     __syncthreads();
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int wg = blockIdx.x, pair = blockIdx.y;
+    int wg, pair;
+    sweep_place(a.nwg, wg, pair);
     const int H = a.H, W1 = a.W1;
     const int nblk = (H + HB - 1) / HB;
     const bool has_left = wg > 0, has_right = wg + 1 < a.nwg;
@@ -312,18 +388,45 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
         const int src_strip = need ? (dir == 0 ? wg - 1 : wg + 1) : wg;
         const int col = (dir == 0 ? pkl : NCOL - LPW + pkl) + 1;  // LDS column slot
         bool dead = (a.dbg & 1) != 0;
+        [[maybe_unused]] uint64_t st_poll = 0, st_bar = 0;
+        SW_T0(st_life);
+        // the source strip on this XCD (sweep_place): poll through the shared L2 first
+        const bool fast = SWEEP_XCD_MAP && (sweep_lin(a.nwg, src_strip, pair) & 7u) == ((blockIdx.x + blockIdx.y * (uint32_t)a.nwg) & 7u);
+        const bool xchg = (has_left || has_right) && !(a.dbg & 2);  // wave-uniform
+        const rsrc_t rhop_p = make_rsrc(hopp, (uint64_t)a.hop_pair * 8);
         for (int b = 0; b < nblk; b++) {
+            // the neighbours' snapshot of block b (published before their block-end barrier),
+            // fetched before ours (SWEEP_EARLY_XCHG) or after it
+            uint32_t v[GPL];
+            auto poll = [&]() {
+                if (b + 1 < nblk && xchg) {
+                    const gu64* src = (const gu64*)(hopp + gbase(src_strip, dir, b) + r0);
+                    SW_T0(tp);
+                    poll_granules<GPL>(src, need, tag0 | (uint32_t)(b + 1), v, dead, a.err, fast, rhop_p,
+                                       (uint32_t)((gbase(src_strip, dir, b) + r0) * 8));
+                    SW_ACC(st_poll, tp);
+#if SWEEP_STATS
+                    if (a.stats && (lane == 0 || lane == 32) && need)  // observed time of (source strip, dir, block)
+                        a.stats[1024 + 3 * 65536 + (size_t)MODE * 65536 +
+                                ((size_t)(pair * a.nwg + src_strip) * 2 + dir) * nblk + b] = __builtin_amdgcn_s_memrealtime();
+#endif
+                }
+            };
             if (ROWSYNC) {
+                if (SWEEP_EARLY_XCHG == 2) poll();
+                SW_T0(tb);
                 if (!(a.dbg & 4)) lds_barrier();  // the compute waves' end-of-block barrier
+                SW_ACC(st_bar, tb);
             } else {
 #pragma unroll 1
-                for (int j = 0; j < HB; j++) if (!(a.dbg & 4)) lds_barrier();  // 4: timing only, no row barriers
+                for (int j = 0; j < HB; j++) {
+                    if (SWEEP_EARLY_XCHG == 2 && j == HB - 1) poll();  // after the rows the snapshot needs
+                    if (!(a.dbg & 4)) lds_barrier();  // 4: timing only, no row barriers
+                }
             }
+            if (SWEEP_EARLY_XCHG != 2) poll();
             if (b + 1 < nblk) {
-                if ((has_left || has_right) && !(a.dbg & 2)) {  // wave-uniform
-                    uint32_t v[GPL];
-                    const gu64* src = (const gu64*)(hopp + gbase(src_strip, dir, b) + r0);
-                    poll_granules<GPL>(src, need, tag0 | (uint32_t)(b + 1), v, dead, a.err);
+                if (xchg) {
                     const int wb = (b * HB + HB - 1) & 1;
                     uint32_t mn = 0xFFFFFFFFu;
 #pragma unroll
@@ -342,9 +445,22 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
                     if (PKMIN) mn *= 0x10001u;   // the packed steps keep minLp replicated in both halves
                     if (need && (lane % (VL / 2)) == 0) lmin[wb][dir][col] = mn;
                 }
+                SW_T0(tb2);
                 lds_barrier();
+                SW_ACC(st_bar, tb2);
             }
         }
+#if SWEEP_STATS
+        if (a.stats && lane == 0) {
+            atomicAdd(a.stats + 8 * MODE + 0, (unsigned long long)st_poll);
+            atomicAdd(a.stats + 8 * MODE + 1, (unsigned long long)st_bar);
+            atomicAdd(a.stats + 8 * MODE + 6, (unsigned long long)(__builtin_readcyclecounter() - st_life));
+            const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u;  // HW_REG_XCC_ID
+            const uint32_t lin = blockIdx.x + blockIdx.y * gridDim.x;
+            atomicAdd(a.stats + 8 * MODE + 7, (unsigned long long)(xcc == lin % 8 ? 1 : 0) | (1ull << 32));
+            if (MODE == 0 && lin < 2048) reinterpret_cast<uint8_t*>(a.stats + 128)[lin] = (uint8_t)(xcc | 0x80);
+        }
+#endif
         return;
     }
 
@@ -367,8 +483,9 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
     auto publish_row = [&](int s) {
         __hip_atomic_store(&rowcnt[wave], (uint32_t)(s + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     };
-    auto wait_row = [&](int s) {
-        if (sync_dead) return;
+    [[maybe_unused]] uint64_t st_wait = 0, st_bbar = 0;
+    SW_T0(st_clife);
+    auto wait_row_spin = [&](int s) {
         for (uint32_t spins = 0;; spins++) {
             // both counters in flight at once (relaxed), one acquire for the pair
             const uint32_t nl = __builtin_amdgcn_readfirstlane(
@@ -386,6 +503,12 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
             }
             if (SWEEP_ROW_SLEEP) __builtin_amdgcn_s_sleep(SWEEP_ROW_SLEEP);
         }
+    };
+    auto wait_row = [&](int s) {
+        if (sync_dead) return;
+        SW_T0(tw);
+        wait_row_spin(s);
+        SW_ACC(st_wait, tw);
     };
     auto end_row = [&](int j, int s) {
         if (!ROWSYNC || j == HB - 1) {
@@ -520,6 +643,29 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
                     if constexpr (OWN) mnV = step(LVp, mVl, nV);
                     if constexpr (HAS_A) mnA = step(LA, mA, nA);
                     if constexpr (HAS_B) mnB = step(LB, mB, nB);
+                    // snapshot of the block's last row for the neighbouring strips' halos
+                    // (the strip's boundary own waves; before the block-end barrier with
+                    // SWEEP_EARLY_XCHG, so no wave of the strip waits for the others first)
+                    auto snapshot = [&]() {
+                        if (j == HB - 1 && b + 1 < nblk) {
+                            const bool pa = wave == NCW - 2 && has_right, pb = wave == 1 && has_left;
+                            if (pa || pb) {
+                                const uint32_t tag = tag0 | (uint32_t)(b + 1);
+                                const uint32_t o = (uint32_t)((gbase(wg, pa ? 0 : 1, b) + (size_t)(kl * VL + g) * NG) * 8);
+#pragma unroll
+                                for (int q = 0; q < NG; q++)
+                                    __builtin_amdgcn_raw_buffer_store_b64(u32x2{pa ? nA[q] : nB[q], tag}, rhop, o + 8 * q,
+                                                                          0, 16);
+#if SWEEP_STATS
+                                if (a.stats && lane == 0)  // publish time, [mode][pair][strip][dir][block]
+                                    a.stats[1024 + (size_t)MODE * 65536 +
+                                            ((size_t)(pair * a.nwg + wg) * 2 + (pa ? 0 : 1)) * nblk + b] =
+                                        __builtin_amdgcn_s_memrealtime();
+#endif
+                            }
+                        }
+                    };
+                    if constexpr (OWN && SWEEP_EARLY_XCHG) snapshot();
                     if constexpr (HAS_A) {
                         lds_put_pk<NP>(&lv[wb][0][c + 1][g * DPL], nA);
                         if (g == 0) lmin[wb][0][c + 1] = mnA;
@@ -532,7 +678,9 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
                     // without row sync, closed by a barrier; the poller writes the halo
                     // snapshot after the block-end barrier, while the waves run their WTA
                     if (!ROWSYNC || j == HB - 1) {
+                        SW_T0(tb);
                         if (!(a.dbg & 4)) lds_barrier();
+                        SW_ACC(st_bbar, tb);
                     } else {
                         publish_row(s);
                     }
@@ -540,18 +688,7 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
 #pragma unroll
                         for (int i = 0; i < NP; i++) LVp[i] = nV[i];
                         mVl = mnV;
-                        // snapshot of the block's last row for the neighbouring strips' halos
-                        if (j == HB - 1 && b + 1 < nblk) {
-                            const bool pa = wave == NCW - 2 && has_right, pb = wave == 1 && has_left;
-                            if (pa || pb) {
-                                const uint32_t tag = tag0 | (uint32_t)(b + 1);
-                                const uint32_t o = (uint32_t)((gbase(wg, pa ? 0 : 1, b) + (size_t)(kl * VL + g) * NG) * 8);
-#pragma unroll
-                                for (int q = 0; q < NG; q++)
-                                    __builtin_amdgcn_raw_buffer_store_b64(u32x2{pa ? nA[q] : nB[q], tag}, rhop, o + 8 * q,
-                                                                          0, 16);
-                            }
-                        }
+                        if constexpr (!SWEEP_EARLY_XCHG) snapshot();
                         if constexpr (MODE == 0) {
                             uint32_t out[NP];
 #pragma unroll
@@ -610,8 +747,20 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
                         }
                     }
                 }
-                if (b + 1 < nblk) lds_barrier();  // the poller has written the halo snapshot
+                if (b + 1 < nblk) {
+                    SW_T0(tb);
+                    lds_barrier();  // the poller has written the halo snapshot
+                    SW_ACC(st_bbar, tb);
+                }
             }
+#if SWEEP_STATS
+            if (a.stats && lane == 0) {
+                atomicAdd(a.stats + 8 * MODE + 2, (unsigned long long)st_wait);
+                atomicAdd(a.stats + 8 * MODE + 3, (unsigned long long)st_bbar);
+                atomicAdd(a.stats + 8 * MODE + 4, (unsigned long long)(__builtin_readcyclecounter() - st_clife));
+                atomicAdd(a.stats + 8 * MODE + 5, 1ull);
+            }
+#endif
         };
         if (halo_l) run(std::integral_constant<int, 0>{});
         else if (halo_r) run(std::integral_constant<int, 2>{});

@@ -8,6 +8,10 @@ namespace smk {
 // MODE: 0 = down sweep writing the u16 partial (8 paths, first pass)
 //       1 = down sweep + E/W + WTA (MODE_SGBM: 5 paths)
 //       2 = up sweep + E/W + down partial + WTA (8 paths, second pass)
+#ifndef SWEEP_STATS
+#define SWEEP_STATS 0  // sm_sweep.hpp: wait-cycle counters (variant builds)
+#endif
+
 struct SweepArgs {
     const uint8_t* cost;  // [pair][H][W1][D] of CT
     size_t cost_pair;     // bytes
@@ -25,6 +29,7 @@ struct SweepArgs {
     int nwg;
     uint32_t epoch;  // 1..65535, distinct from the previous launches on the same hop buffer
     int dbg;         // timing ablations only: 1 no waiting in the halo polls, 2 no polls, 4 no row barriers
+    unsigned long long* stats;  // SWEEP_STATS builds only: per-mode wait-cycle counters (else null)
 };
 
 

@@ -50,7 +50,8 @@ __device__ __forceinline__ int bt_pair(uint2 l, uint2 r)
 
 // Horizontal box sums of one row strip: pixel costs of TX columns + 2*SW2 halo
 // (clamped to [0, width1)) into LDS, then the (2*SW2+1)-wide window per
-// (x1, d).  Exact: |hsum| <= 23 * 3 * 189 < 2^15.  blockIdx = (strip, y, pair).
+// (x1, d): OpenCV's running sums exactly while no window sum can pass 32767 (the host
+// checks (2*SW2+1) * cn * (2*ftzero + 63); else k_wide_hsum_scan).  blockIdx = (strip, y, pair).
 template <int TX>
 __global__ void __launch_bounds__(256) k_wide_hsum(WideArgs a)
 {
@@ -77,6 +78,40 @@ __global__ void __launch_bounds__(256) k_wide_hsum(WideArgs a)
         int s = 0;
         for (int j = -SW2; j <= SW2; j++) s += pix[(min(max(x1 + j, 0), W1 - 1) - ca) * D + d];
         out[(size_t)x1 * D + d] = (int16_t)s;
+    }
+}
+
+// k_wide_hsum where a window sum can pass 32767 ((2*SW2+1) * cn * (2*ftzero + 63) above
+// it): OpenCV's own running scan along x, one thread per (row, d).  The rows it reads
+// while the C rows are initialised (k <= SH2, y == 0) wrap like its scalar loop; the rows
+// entering during the scan (k > SH2) saturate like its int16 SIMD update
+//   hv = sat16(sat16(hv - pix[max(x - SW2 - 1, 0)]) + pix[min(x + SW2, width1 - 1)]).
+// blockIdx = (row, pair).
+__global__ void __launch_bounds__(256) k_wide_hsum_scan(WideArgs a)
+{
+    const int y = blockIdx.x, pair = blockIdx.y;
+    const int D = a.D, W = a.W, W1 = a.width1, SW2 = a.SW2, cn = a.cn;
+    const uint2* Lp = a.planes + (size_t)(pair * 2) * cn * a.H * W + (size_t)y * W;
+    const uint2* Rp = Lp + (size_t)cn * a.H * W;
+    const size_t plane = (size_t)a.H * W;
+    const bool sat = y > a.SH2;
+    int16_t* out = a.hsum + (size_t)pair * a.vol + (size_t)y * W1 * D;
+    for (int d = threadIdx.x; d < D; d += 256) {
+        auto pix = [&](int x1) {
+            const int X = x1 + a.minX1, Xr = X - a.minD - d;
+            int s = 0;
+            for (int ch = 0; ch < cn; ch++) s += bt_pair(Lp[ch * plane + X], Rp[ch * plane + Xr]);
+            return s;
+        };
+        int hv = pix(0) * (SW2 + 1);
+        for (int x = 1; x <= SW2; x++) hv += pix(min(x, W1 - 1));
+        hv = wrap16(hv);
+        out[d] = (int16_t)hv;
+        for (int x = 1; x < W1; x++) {
+            const int add = pix(min(x + SW2, W1 - 1)), sub = pix(max(x - SW2 - 1, 0));
+            hv = sat ? sat16(sat16(hv - sub) + add) : wrap16(hv + add - sub);
+            out[(size_t)x * D + d] = (int16_t)hv;
+        }
     }
 }
 

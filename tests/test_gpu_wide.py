@@ -115,3 +115,23 @@ def test_wide_batch_device_bgr(eng):
         eng.set_stream(None)
     for i, (a, b) in enumerate(pairs):
         assert np.array_equal(got[i], ref_c.compute(a, b, p)), i
+
+
+def test_box_sums_past_int16_saturate_like_opencv(eng):
+    """blockSize 55, BGR, preFilterCap 126: a 55-wide window of 3-channel BT costs
+    (up to 3 * (2*127 + 63) each) passes 32767, where OpenCV's running int16 sums
+    saturate (rows entering during the scan) or wrap (the rows of the first C row);
+    k_wide_hsum_scan reproduces both (sm_wide.hpp hsum)."""
+    rng = np.random.default_rng(5)
+    H, W, D = 70, 200, 16
+    gl = rng.integers(0, 256, (H, W), dtype=np.uint8)
+    gr = (255 - gl).astype(np.uint8)
+    left, right = _bgr(gl, 3), _bgr(gr, 4)
+    p = dict(minDisparity=0, numDisparities=D, blockSize=55, P1=100, P2=800, disp12MaxDiff=1000000,
+             uniquenessRatio=0, preFilterCap=126, mode=5, cost=0)
+    out = _run(eng, left, right, p)
+    C_ref = ref_c.cost_volume(left, right, p)
+    assert (C_ref == 32767).any() and (C_ref < 0).any()  # both the saturation and the wrap happen
+    C = np.frombuffer(eng.debug_fetch(0), np.int16).reshape(C_ref.shape)
+    assert np.array_equal(C, C_ref), f"{int((C != C_ref).sum())} cost cells differ"
+    assert np.array_equal(out, ref_c.compute(left, right, p))

@@ -234,3 +234,42 @@ def test_compute_disparity_repeatable_with_side_stream_prepare():
                 assert np.array_equal(fo.cpu().numpy(), alone), (D, i)
         finally:
             eng.close()
+
+
+def test_compute_disparity_on_caller_stream():
+    """After sm_set_stream the right matcher (twin context, own stream) and the WLS
+    guide work (third stream) still fork from and join into the caller's stream:
+    the maps written there equal the default-stream call's, read right after a
+    synchronize of that stream only (twin ordering after sm_set_stream)."""
+    import torch
+
+    H, W, D, n = 80, 260, 32, 2
+    pairs = [synthetic.random_dot_pair(H, W, D, seed=70 + i)[:2] for i in range(n)]
+    sp = synthetic.to_sm_params(synthetic.parity_params(D))
+    wp = _lib.wls_default_params(sp)
+    wp.lambda_, wp.sigma_color = 8000.0, 1.5
+    eng = _lib.Engine(0)
+    try:
+        L = torch.tensor(np.stack([a for a, _ in pairs]), device="cuda")
+        R = torch.tensor(np.stack([b for _, b in pairs]), device="cuda")
+        outs = []
+        for use_stream in (False, True):
+            dl, dr, fo = (torch.full((n, H, W), 99, dtype=torch.int16, device="cuda") for _ in range(3))
+            s = torch.cuda.Stream()
+            torch.cuda.synchronize()  # the inputs and the 99-filled outputs are in place
+            if use_stream:
+                eng.set_stream(s.cuda_stream)
+            try:
+                eng.compute_disparity_batch_device(L.data_ptr(), R.data_ptr(), n, H * W, H, W, W, sp, wp,
+                                                   dl.data_ptr(), dr.data_ptr(), fo.data_ptr())
+                if use_stream:
+                    s.synchronize()
+                else:
+                    eng.synchronize()
+                outs.append([t.cpu().numpy() for t in (dl, dr, fo)])
+            finally:
+                eng.set_stream(None)
+        for a, b in zip(*outs):
+            assert np.array_equal(a, b)
+    finally:
+        eng.close()
