@@ -16,12 +16,13 @@ __device__ __forceinline__ uint32_t line_or(uint32_t v)
     return v;
 }
 
-// minimum over aligned groups of N lanes (N = 4, 8 or 16)
+// minimum over aligned groups of N lanes (N = 1, 2, 4, 8 or 16)
 template <int N>
 __device__ __forceinline__ uint32_t group_min(uint32_t v)
 {
-    v = ::min(v, perm_dpp<DPP_QP_XOR1>(v));
-    v = ::min(v, perm_dpp<DPP_QP_XOR2>(v));
+    static_assert(N == 1 || N == 2 || N == 4 || N == 8 || N == 16, "lane group of 1-16 lanes");
+    if constexpr (N >= 2) v = ::min(v, perm_dpp<DPP_QP_XOR1>(v));
+    if constexpr (N >= 4) v = ::min(v, perm_dpp<DPP_QP_XOR2>(v));
     if constexpr (N >= 8) v = ::min(v, perm_dpp<DPP_ROW_HALF_MIRROR>(v));
     if constexpr (N >= 16) v = ::min(v, perm_dpp<DPP_ROW_MIRROR>(v));
     return v;
@@ -30,8 +31,9 @@ __device__ __forceinline__ uint32_t group_min(uint32_t v)
 template <int N>
 __device__ __forceinline__ uint32_t group_sum(uint32_t v)
 {
-    v += perm_dpp<DPP_QP_XOR1>(v);
-    v += perm_dpp<DPP_QP_XOR2>(v);
+    static_assert(N == 1 || N == 2 || N == 4 || N == 8 || N == 16, "lane group of 1-16 lanes");
+    if constexpr (N >= 2) v += perm_dpp<DPP_QP_XOR1>(v);
+    if constexpr (N >= 4) v += perm_dpp<DPP_QP_XOR2>(v);
     if constexpr (N >= 8) v += perm_dpp<DPP_ROW_HALF_MIRROR>(v);
     if constexpr (N >= 16) v += perm_dpp<DPP_ROW_MIRROR>(v);
     return v;
@@ -40,8 +42,9 @@ __device__ __forceinline__ uint32_t group_sum(uint32_t v)
 template <int N>
 __device__ __forceinline__ uint32_t group_max(uint32_t v)
 {
-    v = ::max(v, perm_dpp<DPP_QP_XOR1>(v));
-    v = ::max(v, perm_dpp<DPP_QP_XOR2>(v));
+    static_assert(N == 1 || N == 2 || N == 4 || N == 8 || N == 16, "lane group of 1-16 lanes");
+    if constexpr (N >= 2) v = ::max(v, perm_dpp<DPP_QP_XOR1>(v));
+    if constexpr (N >= 4) v = ::max(v, perm_dpp<DPP_QP_XOR2>(v));
     if constexpr (N >= 8) v = ::max(v, perm_dpp<DPP_ROW_HALF_MIRROR>(v));
     if constexpr (N >= 16) v = ::max(v, perm_dpp<DPP_ROW_MIRROR>(v));
     return v;

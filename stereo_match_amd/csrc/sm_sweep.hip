@@ -89,7 +89,7 @@ struct InfoF {
             if (per_cu < 1) return hipErrorInvalidValue;
             out->cw = SG::CW;
             out->hb = SG::HB;
-            out->ngr = SG::NGR;
+            out->ngr = SG::SNG;
             out->threads = SG::THREADS;
             out->blocks_per_cu = per_cu;
             out->impl = SWEEP_WIDE ? 1 : 0;

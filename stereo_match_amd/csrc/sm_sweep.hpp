@@ -101,21 +101,36 @@ constexpr uint32_t SW_SPIN_LIMIT = 1u << 19;
 // census8 sweeps 244 -> 217 us per pair at NCW 7 -> 11, sgbm5 247 -> 235, sgbm8 321 -> 287
 // at NCW 13 (u16 costs); 9, 12, 14 and 15 are slower (the strip count against 256 CUs).
 constexpr int kNarrowNcw = 7;
+// HM: column sets per halo wave in the packed row loops.  A halo of HM*LPW columns stays
+// exact for HM*LPW rows after a snapshot, so the strips hand off once per HM*LPW rows; the
+// hand-off latency (us under the sweeps' streaming traffic, SWEEP_STATS) is paid half as
+// often at HM = 2, for halo waves that step two column sets of their one direction.
+#ifndef SWEEP_HM
+#define SWEEP_HM 2
+#endif
 template <int VL, int DPL, int NCW_ = kNarrowNcw>
 struct SweepGeo {
-    static constexpr int LPW = 64 / VL;             // columns per wave
+    static constexpr int LPW = 64 / VL;             // columns per wave (per column set)
+    static constexpr int HM = (DPL % 2 == 0 && !SWEEP_U32) ? SWEEP_HM : 1;  // column sets per halo wave
     static constexpr int NCW = NCW_;                // compute waves: left halo, NCW-2 own, right halo
     static constexpr int THREADS = (NCW + 1) * 64;  // + the poller wave
-    static constexpr int HB = LPW;                  // rows per block = halo width
-    static constexpr int NCOL = NCW * LPW;          // columns held by the compute waves
+    static constexpr int HW = HM * LPW;             // halo columns per side
+    static constexpr int HB = HW;                   // rows per block = halo width
+    static constexpr int NCOL = (NCW - 2) * LPW + 2 * HW;  // columns held by the compute waves
     static constexpr int COLS = NCOL + 2;           // + one never-written zero column each side
     static constexpr int CW = (NCW - 2) * LPW;      // own columns per workgroup
     static constexpr int D = VL * DPL;
     static constexpr int NG = (DPL + 1) / 2;        // granules per lane (two u16 per granule)
-    static constexpr int NGR = 64 * NG;             // granules per (strip, direction, block)
+    // snapshot record of one (strip, direction, block): the HW boundary columns' states,
+    // granule r = (q * HW + column) * VL + lane slice (q: the slice's q-th u16 pair), so
+    // that each producer store instruction and each poller load instruction covers 64
+    // consecutive granules, then one granule per column with its minimum
+    static constexpr int NDAT = NG * HW * VL;
+    static constexpr int SNG = NDAT + HW;           // granules per record
     // rows of inputs in flight per lane (a divisor of HB: the ring slot is the row's index in
     // its block); 2 where the wide strips' register budget needs it (12 waves, <= 168 VGPRs)
     static constexpr int PF = (DPL >= 10 && NCW_ >= 11) ? 2 : 4;
+    static_assert(NCW - 2 >= 2 * HM, "the snapshot's own waves of the two sides are distinct");
     static_assert(HB % PF == 0, "the input ring is indexed by the row within a block");
 };
 
@@ -248,84 +263,30 @@ __device__ __forceinline__ void lds_barrier()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-// Strip placement: workgroups are dispatched to the 8 XCDs round-robin by linear id
-// (from an offset that carries over between launches), so the (strip, pair) of a
-// workgroup is taken from its linear id such that one pair's strips share a residue
-// mod 8, i.e. one XCD and its L2: the halo hand-offs then stay inside that L2
-// (SWEEP_XCD_MAP; the protocol stays correct for any placement, see poll_granules).
-#ifndef SWEEP_XCD_MAP
-#define SWEEP_XCD_MAP 0  // measured: census8 3475 vs 4713 pairs per second (one pair per XCD is slower)
-#endif
-// first-phase poll loads (same-XCD source strips): cache policy bits of the
-// buffer load (1 = sc0: past the CU's L1, served by the shared L2); 0 = no first phase
-#ifndef SWEEP_POLL_FAST_AUX
-#define SWEEP_POLL_FAST_AUX 0  // sc0 polls never saw the sc1 snapshot stores (516 pairs per second)
-#endif
-#ifndef SWEEP_POLL_FAST_SPINS
-#define SWEEP_POLL_FAST_SPINS 256
-#endif
 // the strip's boundary waves publish their snapshot before the block-end barrier (1; 0:
 // after it), and with 2 the poller also polls the neighbours' before that barrier
 #ifndef SWEEP_EARLY_XCHG
 #define SWEEP_EARLY_XCHG 1
 #endif
 
-__device__ __forceinline__ void sweep_place(int nwg, int& strip, int& pair)
-{
-    if (!SWEEP_XCD_MAP) {
-        strip = blockIdx.x;
-        pair = blockIdx.y;
-        return;
-    }
-    const uint32_t n = (uint32_t)nwg * gridDim.y;
-    const uint32_t lin = blockIdx.x + blockIdx.y * (uint32_t)nwg;
-    const uint32_t r = lin % 8u, q = lin / 8u, base = n / 8u, extra = n % 8u;
-    const uint32_t w = r * base + min(r, extra) + q;  // pair-major item of residue class r
-    strip = (int)(w % (uint32_t)nwg);
-    pair = (int)(w / (uint32_t)nwg);
-}
-
-// the linear id sweep_place gives item (strip, pair) (same-XCD test of two strips)
-__device__ __forceinline__ uint32_t sweep_lin(int nwg, int strip, int pair)
-{
-    const uint32_t n = (uint32_t)nwg * gridDim.y, base = n / 8u, extra = n % 8u;
-    const uint32_t w = (uint32_t)pair * (uint32_t)nwg + (uint32_t)strip;
-    // residue class r holds items [r*base + min(r, extra), ... + base + (r < extra))
-    const uint32_t big = extra * (base + 1);
-    const uint32_t r = w < big ? w / (base + 1) : extra + (w - big) / max(base, 1u);
-    const uint32_t q = w - (r * base + min(r, extra));
-    return q * 8u + r;
-}
-
-// Poll N granules of one lane until every tag equals `tag` (lanes with !need
-// do not load).  Wave-uniform exit; gives up after SW_SPIN_LIMIT passes.  With
-// fast (the source strip runs on this XCD), the first SWEEP_POLL_FAST_SPINS passes
-// load through the XCD's L2 (the producer's sc1 store writes it through); a stale
-// line there (the source on another XCD after all) cannot carry the awaited tag,
-// so correctness never depends on the placement: the later passes load sc1.
-// (rs, off: the same granules as a wave-uniform buffer resource + this lane's byte offset)
+// Poll N granules per lane (granule k at src[k], polled where need[k]) until every tag
+// equals `tag`.  Wave-uniform exit; gives up after SW_SPIN_LIMIT passes.
 template <int N>
-__device__ __forceinline__ void poll_granules(const gu64* src, bool need, uint32_t tag, uint32_t (&v)[N], bool& dead,
-                                              uint32_t* err, bool fast, rsrc_t rs, uint32_t off)
+__device__ __forceinline__ void poll_set(const gu64* const (&src)[N], const bool (&need)[N], uint32_t tag,
+                                         uint32_t (&v)[N], bool& dead, uint32_t* err)
 {
     for (uint32_t spins = 0;; spins++) {
+        // every load unconditional (src[k] always points into the hop buffer), so the N
+        // loads of a pass are in flight together: a load inside a lane-divergent branch
+        // gets its own wait before the branch closes, one memory round trip per granule
+        unsigned long long x[N];
+#pragma unroll
+        for (int k = 0; k < N; k++) x[k] = __hip_atomic_load(src[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         bool ok = true;
-        if (need) {
-            if (SWEEP_POLL_FAST_AUX && fast && spins < SWEEP_POLL_FAST_SPINS) {
 #pragma unroll
-                for (int k = 0; k < N; k++) {
-                    const u32x2 x = __builtin_amdgcn_raw_buffer_load_b64(rs, off + k * 8, 0, SWEEP_POLL_FAST_AUX);
-                    v[k] = x[0];
-                    ok &= x[1] == tag;
-                }
-            } else {
-#pragma unroll
-                for (int k = 0; k < N; k++) {
-                    const unsigned long long x = __hip_atomic_load(src + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    v[k] = (uint32_t)x;
-                    ok &= (uint32_t)(x >> 32) == tag;
-                }
-            }
+        for (int k = 0; k < N; k++) {
+            v[k] = (uint32_t)x[k];
+            ok &= !need[k] || (uint32_t)(x[k] >> 32) == tag;
         }
         if (__all(ok) || dead) return;
         if (spins >= SW_SPIN_LIMIT) {
@@ -335,6 +296,21 @@ __device__ __forceinline__ void poll_granules(const gu64* src, bool need, uint32
         }
         __builtin_amdgcn_s_sleep(2);
     }
+}
+
+// Poll N consecutive granules of one lane (the k_sweep2 ablation's layout).
+template <int N>
+__device__ __forceinline__ void poll_granules(const gu64* src, bool need, uint32_t tag, uint32_t (&v)[N], bool& dead,
+                                              uint32_t* err)
+{
+    const gu64* p[N];
+    bool nd[N];
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+        p[k] = src + k;
+        nd[k] = need;
+    }
+    poll_set<N>(p, nd, tag, v, dead, err);
 }
 
 template <int VL, int DPL, typename CT, int MODE, int NCW_ = kNarrowNcw>
@@ -349,7 +325,7 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
     constexpr bool ROWSYNC = SWEEP_ROW_SYNC && MODE != 1;
     constexpr bool PKMIN = DPL % 2 == 0 && !SWEEP_U32;  // packed loop: lmin words hold m | m << 16
     constexpr int LPW = G::LPW, NCW = G::NCW, HB = G::HB, NCOL = G::NCOL, COLS = G::COLS, CW = G::CW, D = G::D;
-    constexpr int NG = G::NG, NGR = G::NGR, PF = G::PF;
+    constexpr int NG = G::NG, SNG = G::SNG, PF = G::PF, HM = G::HM, HW = G::HW;
     constexpr int CB = DPL * (int)sizeof(CT);  // cost / E / W bytes per lane and cell
     __shared__ __attribute__((aligned(16))) uint16_t lv[2][2][COLS][D];  // [buf][A=+dx, B=-dx][col+1][d]
     __shared__ uint32_t lmin[2][2][COLS];
@@ -367,48 +343,53 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
     __syncthreads();
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    int wg, pair;
-    sweep_place(a.nwg, wg, pair);
+    const int wg = blockIdx.x, pair = blockIdx.y;
     const int H = a.H, W1 = a.W1;
     const int nblk = (H + HB - 1) / HB;
     const bool has_left = wg > 0, has_right = wg + 1 < a.nwg;
     const uint32_t tag0 = a.epoch << 16;
     unsigned long long* hopp = a.hop + (size_t)pair * a.hop_pair;
-    auto gbase = [&](int strip, int dir, int b) -> size_t { return ((size_t)(strip * 2 + dir) * nblk + b) * NGR; };
+    auto gbase = [&](int strip, int dir, int b) -> size_t { return ((size_t)(strip * 2 + dir) * nblk + b) * SNG; };
 
     if (wave == NCW) {
-        // ---- poller: halo snapshots of the neighbouring strips, once per block
-        constexpr int GPL = 2 * NG;            // granules per poller lane (both directions: 2*NGR / 64)
-        const int q0 = lane * GPL;
-        const int dir = q0 / NGR;              // lanes 0-31: A from the left strip, 32-63: B from the right
-        const int r0 = q0 - dir * NGR;         // (kl * VL + g) * NG + t of the publishing wave
-        const int pkl = r0 / (VL * NG);
-        const int g0 = (r0 % (VL * NG)) / NG;  // this lane covers lane slices g0 and g0 + 1
-        const bool need = dir == 0 ? has_left : has_right;
-        const int src_strip = need ? (dir == 0 ? wg - 1 : wg + 1) : wg;
-        const int col = (dir == 0 ? pkl : NCOL - LPW + pkl) + 1;  // LDS column slot
+        // ---- poller: halo snapshots of the neighbouring strips, once per block.  Granule
+        // k*64 + lane of the two records (A from the left strip, then B from the right)
+        constexpr int NDAT = G::NDAT;
+        constexpr int GPL = (2 * SNG + 63) / 64;  // granules per poller lane
+        int gdir[GPL], grec[GPL];
+        bool gneed[GPL];
+#pragma unroll
+        for (int k = 0; k < GPL; k++) {
+            const int r2 = k * 64 + lane;
+            gdir[k] = r2 >= SNG ? 1 : 0;
+            grec[k] = r2 - gdir[k] * SNG;
+            gneed[k] = r2 < 2 * SNG && (gdir[k] == 0 ? has_left : has_right);
+        }
         bool dead = (a.dbg & 1) != 0;
         [[maybe_unused]] uint64_t st_poll = 0, st_bar = 0;
         SW_T0(st_life);
-        // the source strip on this XCD (sweep_place): poll through the shared L2 first
-        const bool fast = SWEEP_XCD_MAP && (sweep_lin(a.nwg, src_strip, pair) & 7u) == ((blockIdx.x + blockIdx.y * (uint32_t)a.nwg) & 7u);
         const bool xchg = (has_left || has_right) && !(a.dbg & 2);  // wave-uniform
-        const rsrc_t rhop_p = make_rsrc(hopp, (uint64_t)a.hop_pair * 8);
         for (int b = 0; b < nblk; b++) {
             // the neighbours' snapshot of block b (published before their block-end barrier),
-            // fetched before ours (SWEEP_EARLY_XCHG) or after it
+            // fetched before ours (SWEEP_EARLY_XCHG == 2) or after it
             uint32_t v[GPL];
             auto poll = [&]() {
                 if (b + 1 < nblk && xchg) {
-                    const gu64* src = (const gu64*)(hopp + gbase(src_strip, dir, b) + r0);
+                    const gu64* src[GPL];
+#pragma unroll
+                    for (int k = 0; k < GPL; k++)
+                        src[k] = (const gu64*)(hopp + gbase(gneed[k] ? wg + (gdir[k] ? 1 : -1) : wg, gdir[k], b) + grec[k]);
                     SW_T0(tp);
-                    poll_granules<GPL>(src, need, tag0 | (uint32_t)(b + 1), v, dead, a.err, fast, rhop_p,
-                                       (uint32_t)((gbase(src_strip, dir, b) + r0) * 8));
+                    poll_set<GPL>(src, gneed, tag0 | (uint32_t)(b + 1), v, dead, a.err);
                     SW_ACC(st_poll, tp);
 #if SWEEP_STATS
-                    if (a.stats && (lane == 0 || lane == 32) && need)  // observed time of (source strip, dir, block)
-                        a.stats[1024 + 3 * 65536 + (size_t)MODE * 65536 +
-                                ((size_t)(pair * a.nwg + src_strip) * 2 + dir) * nblk + b] = __builtin_amdgcn_s_memrealtime();
+                    if (a.stats && (lane == 0 || lane == 32)) {  // observed time of (source strip, dir, block)
+                        const int dir = lane == 0 ? 0 : 1;
+                        if (dir == 0 ? has_left : has_right)
+                            a.stats[1024 + 3 * 65536 + (size_t)MODE * 65536 +
+                                    ((size_t)(pair * a.nwg + wg + (dir ? 1 : -1)) * 2 + dir) * nblk + b] =
+                                __builtin_amdgcn_s_memrealtime();
+                    }
 #endif
                 }
             };
@@ -428,22 +409,21 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
             if (b + 1 < nblk) {
                 if (xchg) {
                     const int wb = (b * HB + HB - 1) & 1;
-                    uint32_t mn = 0xFFFFFFFFu;
 #pragma unroll
-                    for (int t = 0; t < GPL; t++) {
-                        const int g = g0 + t / NG, tt = t % NG;
-                        const int d = g * DPL + 2 * tt;
-                        const uint32_t lo = v[t] & 0xFFFFu, hi = v[t] >> 16;
-                        if (need) {
-                            lv[wb][dir][col][d] = (uint16_t)lo;
-                            if (2 * tt + 1 < DPL) lv[wb][dir][col][d + 1] = (uint16_t)hi;
+                    for (int k = 0; k < GPL; k++) {
+                        if (!gneed[k]) continue;
+                        const int r = grec[k], dir = gdir[k];
+                        if (r < NDAT) {
+                            const int q = r / (HW * VL), pcol = (r / VL) % HW, gg = r % VL;
+                            const int col = (dir == 0 ? pcol : NCOL - HW + pcol) + 1;  // LDS column slot
+                            const int d = gg * DPL + 2 * q;
+                            if (2 * q + 1 < DPL) *reinterpret_cast<uint32_t*>(&lv[wb][dir][col][d]) = v[k];
+                            else lv[wb][dir][col][d] = (uint16_t)v[k];
+                        } else {
+                            const int pcol = r - NDAT;
+                            lmin[wb][dir][(dir == 0 ? pcol : NCOL - HW + pcol) + 1] = v[k];
                         }
-                        mn = min(mn, lo);
-                        if (2 * tt + 1 < DPL) mn = min(mn, hi);
                     }
-                    mn = group_min<VL / 2>(mn);  // over the VL/2 poller lanes of one column
-                    if (PKMIN) mn *= 0x10001u;   // the packed steps keep minLp replicated in both halves
-                    if (need && (lane % (VL / 2)) == 0) lmin[wb][dir][col] = mn;
                 }
                 SW_T0(tb2);
                 lds_barrier();
@@ -466,8 +446,9 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
 
     // ---- compute waves
     const int kl = lane / VL, g = lane % VL;
-    const int c = wave * LPW + kl;  // column slot among the compute waves
-    const int x1 = wg * CW + c - LPW;
+    // column slot among the compute waves (halo waves: of their first column set)
+    const int c = wave == 0 ? kl : wave == NCW - 1 ? NCOL - HW + kl : HW + (wave - 1) * LPW + kl;
+    const int x1 = wg * CW + c - HW;
     const bool active = x1 >= 0 && x1 < W1;
     const bool halo_l = wave == 0, halo_r = wave == NCW - 1, own = !halo_l && !halo_r;  // wave-uniform
     const int wx0 = wg * CW + wave * LPW - LPW;
@@ -583,14 +564,25 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
         auto run = [&](auto role_c) {
             constexpr int ROLE = decltype(role_c)::value;  // 0 left halo (A), 1 own (A, B, V), 2 right halo (B)
             constexpr bool HAS_A = ROLE != 2, HAS_B = ROLE != 0, OWN = ROLE == 1;
+            constexpr int NS = OWN ? 1 : HM;  // column sets of this wave (halo waves: HM)
+            // this lane's column of set h: slot c + h*LPW, x1 + h*LPW
+            auto cell_h = [&](int h, int y) -> uint32_t {
+                const int xh = x1 + h * LPW;
+                return xh >= 0 && xh < W1 ? ((uint32_t)y * (uint32_t)W1 + (uint32_t)xh) * (uint32_t)D + (uint32_t)(g * DPL)
+                                          : NONE;
+            };
+            RawBytes<CB> rcs[PF][NS];
             auto issue_r = [&](int k, int s) {
-                const uint32_t en = s < H ? cell(UP ? H - 1 - s : s) : NONE;
-                rc_[k].template load<WTA ? SWEEP_COST_AUX : 0>(rc, boff(en, sizeof(CT)));
+                const int yy = UP ? H - 1 - s : s;
+#pragma unroll
+                for (int h = 0; h < NS; h++)
+                    rcs[k][h].template load<WTA ? SWEEP_COST_AUX : 0>(rc, boff(s < H ? cell_h(h, yy) : NONE, sizeof(CT)));
                 if constexpr (OWN && WTA) {
+                    const uint32_t en = s < H ? cell(yy) : NONE;
                     re_[k].template load<SWEEP_STREAM_AUX>(re, boff(en, sizeof(CT)));
                     rw_[k].template load<SWEEP_STREAM_AUX>(rw, boff(en, sizeof(CT)));
                 }
-                if constexpr (OWN && MODE == 2) rp_[k].template load<SWEEP_STREAM_AUX>(rp, boff(en, 2));
+                if constexpr (OWN && MODE == 2) rp_[k].template load<SWEEP_STREAM_AUX>(rp, boff(s < H ? cell(yy) : NONE, 2));
             };
 #pragma unroll
             for (int k = 0; k < PF; k++) issue_r(k, k);
@@ -611,8 +603,9 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
                     const int y = UP ? H - 1 - s : s;
                     const int rb = (s + 1) & 1, wb = s & 1;
                     const uint32_t e = live ? cell(y) : NONE;
-                    uint32_t C[NP], Ein[NP], Win[NP], Pin[NP];
-                    unpack_ct_pk<CT, DPL>(rc_[k], C);
+                    uint32_t C[NS][NP], Ein[NP], Win[NP], Pin[NP];
+#pragma unroll
+                    for (int h = 0; h < NS; h++) unpack_ct_pk<CT, DPL>(rcs[k][h], C[h]);
                     if constexpr (OWN && WTA) {
                         unpack_ct_pk<CT, DPL>(re_[k], Ein);
                         unpack_ct_pk<CT, DPL>(rw_[k], Win);
@@ -620,44 +613,57 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
                     if constexpr (OWN && MODE == 2) unpack_ct_pk<uint16_t, DPL>(rp_[k], Pin);
 #pragma unroll
                     for (int i = 0; i < NP; i++) {  // before the refill (see the u32 loop)
-                        asm volatile("" : "+v"(C[i])::"memory");
+#pragma unroll
+                        for (int h = 0; h < NS; h++) asm volatile("" : "+v"(C[h][i])::"memory");
                         if constexpr (OWN && WTA) asm volatile("" : "+v"(Ein[i]), "+v"(Win[i])::"memory");
                         if constexpr (OWN && MODE == 2) asm volatile("" : "+v"(Pin[i])::"memory");
                     }
                     issue_r(k, s + PF);
                     if (ROWSYNC && j > 0) wait_row(s);
                     // diagonal predecessors: column c-1 (A) and c+1 (B) of the previous row
-                    uint32_t LA[NP], LB[NP], mA = 0, mB = 0;
-                    if constexpr (HAS_A) {
-                        lds_get_pk<NP>(&lv[rb][0][c][g * DPL], LA);
-                        mA = lmin[rb][0][c];
+                    uint32_t LA[NS][NP], LB[NS][NP], mA[NS], mB[NS];
+#pragma unroll
+                    for (int h = 0; h < NS; h++) {
+                        const int ch = c + h * LPW;
+                        if constexpr (HAS_A) {
+                            lds_get_pk<NP>(&lv[rb][0][ch][g * DPL], LA[h]);
+                            mA[h] = lmin[rb][0][ch];
+                        }
+                        if constexpr (HAS_B) {
+                            lds_get_pk<NP>(&lv[rb][1][ch + 2][g * DPL], LB[h]);
+                            mB[h] = lmin[rb][1][ch + 2];
+                        }
                     }
-                    if constexpr (HAS_B) {
-                        lds_get_pk<NP>(&lv[rb][1][c + 2][g * DPL], LB);
-                        mB = lmin[rb][1][c + 2];
-                    }
-                    uint32_t nV[NP], nA[NP], nB[NP], mnV = 0, mnA = 0, mnB = 0;
-                    auto step = [&](const uint32_t(&Lp)[NP], uint32_t m, uint32_t(&Ln)[NP]) {
-                        return sweep_step2<VL, NP, H16>(Lp, m, C, P1p, P2p, eL, eR, Ln);
+                    uint32_t nV[NP], nA[NS][NP], nB[NS][NP], mnV = 0, mnA[NS], mnB[NS];
+                    auto step = [&](const uint32_t(&Lp)[NP], uint32_t m, const uint32_t(&Ch)[NP], uint32_t(&Ln)[NP]) {
+                        return sweep_step2<VL, NP, H16>(Lp, m, Ch, P1p, P2p, eL, eR, Ln);
                     };
-                    if constexpr (OWN) mnV = step(LVp, mVl, nV);
-                    if constexpr (HAS_A) mnA = step(LA, mA, nA);
-                    if constexpr (HAS_B) mnB = step(LB, mB, nB);
-                    // snapshot of the block's last row for the neighbouring strips' halos
-                    // (the strip's boundary own waves; before the block-end barrier with
-                    // SWEEP_EARLY_XCHG, so no wave of the strip waits for the others first)
+                    if constexpr (OWN) mnV = step(LVp, mVl, C[0], nV);
+#pragma unroll
+                    for (int h = 0; h < NS; h++) {
+                        if constexpr (HAS_A) mnA[h] = step(LA[h], mA[h], C[h], nA[h]);
+                        if constexpr (HAS_B) mnB[h] = step(LB[h], mB[h], C[h], nB[h]);
+                    }
+                    // snapshot of the block's last row for the neighbouring strips' halos: the
+                    // strip's HM boundary own waves on each side (before the block-end barrier
+                    // with SWEEP_EARLY_XCHG, so no wave of the strip waits for the others first)
                     auto snapshot = [&]() {
                         if (j == HB - 1 && b + 1 < nblk) {
-                            const bool pa = wave == NCW - 2 && has_right, pb = wave == 1 && has_left;
+                            const bool pa = wave >= NCW - 1 - HM && has_right, pb = wave <= HM && has_left;
                             if (pa || pb) {
                                 const uint32_t tag = tag0 | (uint32_t)(b + 1);
-                                const uint32_t o = (uint32_t)((gbase(wg, pa ? 0 : 1, b) + (size_t)(kl * VL + g) * NG) * 8);
+                                const int pcol = (pa ? wave - (NCW - 1 - HM) : wave - 1) * LPW + kl;
+                                const size_t rec = gbase(wg, pa ? 0 : 1, b);
 #pragma unroll
-                                for (int q = 0; q < NG; q++)
-                                    __builtin_amdgcn_raw_buffer_store_b64(u32x2{pa ? nA[q] : nB[q], tag}, rhop, o + 8 * q,
-                                                                          0, 16);
+                                for (int q = 0; q < NG; q++)  // 64 consecutive granules per store
+                                    __builtin_amdgcn_raw_buffer_store_b64(
+                                        u32x2{pa ? nA[0][q] : nB[0][q], tag}, rhop,
+                                        (uint32_t)((rec + (size_t)(q * HW + pcol) * VL + g) * 8), 0, 16);
+                                if (g == 0)  // the column's minimum (replicated halves, as lmin holds it)
+                                    __builtin_amdgcn_raw_buffer_store_b64(u32x2{pa ? mnA[0] : mnB[0], tag}, rhop,
+                                                                          (uint32_t)((rec + G::NDAT + pcol) * 8), 0, 16);
 #if SWEEP_STATS
-                                if (a.stats && lane == 0)  // publish time, [mode][pair][strip][dir][block]
+                                if (a.stats && lane == 0 && (wave == NCW - 2 || wave == 1))  // publish time
                                     a.stats[1024 + (size_t)MODE * 65536 +
                                             ((size_t)(pair * a.nwg + wg) * 2 + (pa ? 0 : 1)) * nblk + b] =
                                         __builtin_amdgcn_s_memrealtime();
@@ -666,13 +672,17 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
                         }
                     };
                     if constexpr (OWN && SWEEP_EARLY_XCHG) snapshot();
-                    if constexpr (HAS_A) {
-                        lds_put_pk<NP>(&lv[wb][0][c + 1][g * DPL], nA);
-                        if (g == 0) lmin[wb][0][c + 1] = mnA;
-                    }
-                    if constexpr (HAS_B) {
-                        lds_put_pk<NP>(&lv[wb][1][c + 1][g * DPL], nB);
-                        if (g == 0) lmin[wb][1][c + 1] = mnB;
+#pragma unroll
+                    for (int h = 0; h < NS; h++) {
+                        const int ch = c + h * LPW;
+                        if constexpr (HAS_A) {
+                            lds_put_pk<NP>(&lv[wb][0][ch + 1][g * DPL], nA[h]);
+                            if (g == 0) lmin[wb][0][ch + 1] = mnA[h];
+                        }
+                        if constexpr (HAS_B) {
+                            lds_put_pk<NP>(&lv[wb][1][ch + 1][g * DPL], nB[h]);
+                            if (g == 0) lmin[wb][1][ch + 1] = mnB[h];
+                        }
                     }
                     // the row is published (neighbour counters) or, at a block end and
                     // without row sync, closed by a barrier; the poller writes the halo
@@ -692,7 +702,7 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
                         if constexpr (MODE == 0) {
                             uint32_t out[NP];
 #pragma unroll
-                            for (int i = 0; i < NP; i++) out[i] = pk_add(pk_add(nV[i], nA[i]), nB[i]);
+                            for (int i = 0; i < NP; i++) out[i] = pk_add(pk_add(nV[i], nA[0][i]), nB[0][i]);
                             bstore_n<uint32_t, NP, SWEEP_STREAM_AUX>(rp, boff(e, 2), out);
                         } else {
                             uint32_t Sp[NP];
@@ -703,12 +713,12 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
                                 if constexpr (SAT) {
                                     uint32_t ew = pk_adds(Ein[i], Win[i]);
                                     if constexpr (MODE == 2) ew = pk_adds(ew, Pin[i]);
-                                    t = pk_adds(pk_adds(nV[i], nA[i]), pk_adds(nB[i], ew));
+                                    t = pk_adds(pk_adds(nV[i], nA[0][i]), pk_adds(nB[0][i], ew));
                                     t = pk_min(t, 0x7FFF7FFFu);  // min(sum, 32767)
                                 } else {
                                     uint32_t ew = pk_add(Ein[i], Win[i]);
                                     if constexpr (MODE == 2) ew = pk_add(ew, Pin[i]);
-                                    t = pk_add(pk_add(nV[i], nA[i]), pk_add(nB[i], ew));
+                                    t = pk_add(pk_add(nV[i], nA[0][i]), pk_add(nB[0][i], ew));
                                 }
                                 Sp[i] = t;
                                 key = min(key, min((t << 16) | wta_rank(g * DPL + 2 * i, MODE == 1),
@@ -831,13 +841,17 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
                 const bool pa = wave == NCW - 2 && has_right, pb = wave == 1 && has_left;  // wave-uniform
                 if (pa || pb) {
                     const uint32_t tag = tag0 | (uint32_t)(b + 1);
-                    const uint32_t o = (uint32_t)((gbase(wg, pa ? 0 : 1, b) + (size_t)(kl * VL + g) * NG) * 8);
+                    const size_t rec = gbase(wg, pa ? 0 : 1, b);  // HM = 1 here: column kl of the record
 #pragma unroll
                     for (int q = 0; q < NG; q++) {
                         const uint32_t lo = pa ? nA[2 * q] : nB[2 * q];
                         const uint32_t hi = 2 * q + 1 < DPL ? (pa ? nA[2 * q + 1] : nB[2 * q + 1]) : 0u;
-                        __builtin_amdgcn_raw_buffer_store_b64(u32x2{lo | (hi << 16), tag}, rhop, o + 8 * q, 0, 16);
+                        __builtin_amdgcn_raw_buffer_store_b64(u32x2{lo | (hi << 16), tag}, rhop,
+                                                              (uint32_t)((rec + (size_t)(q * HW + kl) * VL + g) * 8), 0, 16);
                     }
+                    if (g == 0)
+                        __builtin_amdgcn_raw_buffer_store_b64(u32x2{pa ? mnA : mnB, tag}, rhop,
+                                                              (uint32_t)((rec + G::NDAT + kl) * 8), 0, 16);
                 }
             }
 

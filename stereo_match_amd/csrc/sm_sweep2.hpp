@@ -170,7 +170,7 @@ __global__ void __launch_bounds__((Sweep2Geo<NW, CPW, NP>::THREADS)) k_sweep2(Sw
                 if ((has_left || has_right) && !(a.dbg & 2)) {  // wave-uniform
                     uint32_t v[NP + 1];
                     const gu64* src = (const gu64*)(hopp + gbase(src_strip, dir, b) + (size_t)(p % NPUB) * (NP + 1));
-                    poll_granules<NP + 1>(src, need, tag0 | (uint32_t)(b + 1), v, dead, a.err, false, make_rsrc(nullptr, 0), 0);
+                    poll_granules<NP + 1>(src, need, tag0 | (uint32_t)(b + 1), v, dead, a.err);
                     if (need) {
                         const int col = p % HB, qq = p / HB;
                         uint32_t w[NP];
