@@ -84,6 +84,7 @@ def parse():
                     help="rank 0, N=1: timed calls of the reference surface compute_disparity (host numpy in/out, "
                          "settings.ini, KITTI size); 0 = skip")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
+    ap.add_argument("--valu-file", default=os.path.join(ROOT, "profiles", "valu_latest.json"))
     ap.add_argument("--selftest-cpu", action="store_true",
                     help="rank-path self-test: main's own sharding / timing / gather / JSON code over gloo on CPU with "
                          "a stand-in step (no disparity computed, not a measurement)")
@@ -614,7 +615,7 @@ def read_valu(args, dom, pairs_per_launch, sweep, launch_s, H, W, D, path=None):
     on the same sources, configuration, mode, engine and launch size as this run.
     ``frac`` = SQ_INSTS_VALU x 4 cycles / (1024 SIMDs x the profiled launch's
     cycles); ``frac_live`` divides by this run's launch time at 2.4 GHz."""
-    path = path or os.path.join(ROOT, "profiles", "valu_latest.json")
+    path = path or args.valu_file
     if not os.path.exists(path):
         return {"note": "no VALU counter file"}
     try:

@@ -7,7 +7,7 @@
 #   bash tools/gpu_round.sh <tag> B : the other bench modes / engines / configs
 # Each GPU step is time-limited; a failure (other than pytest's rc 1) stops the script.
 set -u
-TAG=${1:-r02}; PART=${2:-A}
+TAG=${1:-r03}; PART=${2:-A}
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/$TAG; mkdir -p "$OUT"
 export TMPDIR=/tmp
@@ -23,11 +23,14 @@ if [ "$PART" = A ] || [ "$PART" = T ]; then
     [ "$PART" = T ] || find "$OUT/prof_$m" -name "*kernel_stats.csv" -exec cp {} "$OUT/${m}_kernel_stats.csv" \;
     step traffic_$m 300 bash tools/traffic.sh kitti $m
     cp gpurun_out/traffic/summary.json "$OUT/${m}_traffic.json"
-    rm -rf gpurun_out/traffic "$OUT/prof_$m"
+    step valu_$m 300 bash tools/valu.sh kitti $m
+    cp gpurun_out/valu/summary.json "$OUT/${m}_valu.json"
+    rm -rf gpurun_out/traffic gpurun_out/valu "$OUT/prof_$m"
   done
   cp "$OUT/census8_traffic.json" profiles/traffic_latest.json
+  cp "$OUT/census8_valu.json" profiles/valu_latest.json
   step bench 400 python -u bench.py --traffic-file "$OUT/census8_traffic.json"
-  step bench_sgbm5 400 python -u bench.py --mode sgbm5 --traffic-file "$OUT/sgbm5_traffic.json"
+  step bench_sgbm5 400 python -u bench.py --mode sgbm5 --traffic-file "$OUT/sgbm5_traffic.json" --valu-file "$OUT/sgbm5_valu.json"
 else
   step bench_census8_perdir 300 python -u bench.py --engine perdir --cpu-baseline-pairs 0 --host-surface-calls 0
   step bench_sgbm5_perdir 300 python -u bench.py --mode sgbm5 --engine perdir --cpu-baseline-pairs 0 --host-surface-calls 0
