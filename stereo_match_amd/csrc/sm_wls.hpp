@@ -549,6 +549,143 @@ struct FgsSolveArgs {
     float lam;
 };
 
+// One full 64-step chunk of a line's forward (d' = (f - lam c'[j-1] d'[j-1]) r) or backward
+// (x = d' - c' x[j+1]) sweep, the same float32 operations in the same order as the generic
+// loops below.  The chunk runs in register sub-blocks of FGS_SB steps whose LDS operands are
+// read before the previous sub-block's results are written back: the compiler cannot prove
+// that U0[t'] (next step) and U0[t] (this step) differ, so the plain loop waited for each
+// read after the preceding write (an LDS round trip per step on the dependent chain:
+// ~180 cycles per step on the KITTI row pass).
+#ifndef FGS_SB
+#define FGS_SB 16
+#endif
+#ifndef FGS_NOCOMPUTE
+#define FGS_NOCOMPUTE 0
+#endif
+// materialise a loaded value at this point of the program (the read cannot sink below it)
+__device__ __forceinline__ void fgs_pin(float& x) { asm volatile("" : "+v"(x)); }
+template <int NRHS, bool ROWS>
+__device__ __forceinline__ void fgs_fwd_chunk(const float* RT, float* U0, float* U1, const float* Ct, int lane,
+                                              float lam, float& p0, float& p1, float& cp)
+{
+#pragma clang fp contract(off)
+    constexpr int SB = FGS_SB, NSB = FT / SB;
+    float r[2][SB], u0[2][SB], u1[2][NRHS == 2 ? SB : 1], cc[2][SB];
+#pragma unroll
+    for (int k = 0; k < SB; k++) {
+        const int t = TileMap<ROWS>::tix(lane, k);
+        r[0][k] = RT[t];
+        u0[0][k] = U0[t];
+        if (NRHS == 2) u1[0][k] = U1[t];
+        cc[0][k] = Ct[t];
+    }
+#pragma unroll
+    for (int k = 0; k < SB; k++) {
+        fgs_pin(r[0][k]);
+        fgs_pin(u0[0][k]);
+        if (NRHS == 2) fgs_pin(u1[0][k]);
+        fgs_pin(cc[0][k]);
+    }
+#pragma unroll
+    for (int b = 0; b < NSB; b++) {
+        const int cur = b & 1, nxt = cur ^ 1;
+        if (b + 1 < NSB) {
+#pragma unroll
+            for (int k = 0; k < SB; k++) {
+                const int t = TileMap<ROWS>::tix(lane, (b + 1) * SB + k);
+                r[nxt][k] = RT[t];
+                u0[nxt][k] = U0[t];
+                if (NRHS == 2) u1[nxt][k] = U1[t];
+                cc[nxt][k] = Ct[t];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < SB; k++) {
+            const float lcp = lam * cp;
+            p0 = (u0[cur][k] - lcp * p0) * r[cur][k];
+            u0[cur][k] = p0;
+            if (NRHS == 2) {
+                p1 = (u1[cur][k] - lcp * p1) * r[cur][k];
+                u1[cur][k] = p1;
+            }
+            cp = cc[cur][k];
+        }
+        if (b + 1 < NSB) {  // the next sub-block's reads complete here, not inside the chain
+#pragma unroll
+            for (int k = 0; k < SB; k++) {
+                fgs_pin(r[nxt][k]);
+                fgs_pin(u0[nxt][k]);
+                if (NRHS == 2) fgs_pin(u1[nxt][k]);
+                fgs_pin(cc[nxt][k]);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < SB; k++) {
+            const int t = TileMap<ROWS>::tix(lane, b * SB + k);
+            U0[t] = u0[cur][k];
+            if (NRHS == 2) U1[t] = u1[cur][k];
+        }
+    }
+}
+
+// backward over a full chunk, positions 63 .. 0 (RT holds c')
+template <int NRHS, bool ROWS>
+__device__ __forceinline__ void fgs_bwd_chunk(const float* RT, float* U0, float* U1, int lane, float& p0, float& p1)
+{
+#pragma clang fp contract(off)
+    constexpr int SB = FGS_SB, NSB = FT / SB;
+    float f[2][SB], u0[2][SB], u1[2][NRHS == 2 ? SB : 1];
+#pragma unroll
+    for (int k = 0; k < SB; k++) {
+        const int t = TileMap<ROWS>::tix(lane, FT - 1 - k);
+        f[0][k] = RT[t];
+        u0[0][k] = U0[t];
+        if (NRHS == 2) u1[0][k] = U1[t];
+    }
+#pragma unroll
+    for (int k = 0; k < SB; k++) {
+        fgs_pin(f[0][k]);
+        fgs_pin(u0[0][k]);
+        if (NRHS == 2) fgs_pin(u1[0][k]);
+    }
+#pragma unroll
+    for (int b = 0; b < NSB; b++) {
+        const int cur = b & 1, nxt = cur ^ 1;
+        if (b + 1 < NSB) {
+#pragma unroll
+            for (int k = 0; k < SB; k++) {
+                const int t = TileMap<ROWS>::tix(lane, FT - 1 - (b + 1) * SB - k);
+                f[nxt][k] = RT[t];
+                u0[nxt][k] = U0[t];
+                if (NRHS == 2) u1[nxt][k] = U1[t];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < SB; k++) {
+            p0 = u0[cur][k] - f[cur][k] * p0;
+            u0[cur][k] = p0;
+            if (NRHS == 2) {
+                p1 = u1[cur][k] - f[cur][k] * p1;
+                u1[cur][k] = p1;
+            }
+        }
+        if (b + 1 < NSB) {
+#pragma unroll
+            for (int k = 0; k < SB; k++) {
+                fgs_pin(f[nxt][k]);
+                fgs_pin(u0[nxt][k]);
+                if (NRHS == 2) fgs_pin(u1[nxt][k]);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < SB; k++) {
+            const int t = TileMap<ROWS>::tix(lane, FT - 1 - b * SB - k);
+            U0[t] = u0[cur][k];
+            if (NRHS == 2) U1[t] = u1[cur][k];
+        }
+    }
+}
+
 // the right-hand-side sweeps of one pass given the pivots (64 lines per one-wave workgroup)
 template <int NRHS, bool ROWS>
 __global__ void __launch_bounds__(64) k_fgs_solve(FgsSolveArgs a)
@@ -590,18 +727,23 @@ __global__ void __launch_bounds__(64) k_fgs_solve(FgsSolveArgs a)
             if (NRHS == 2) tile_load<ROWS>(r1, u1, vn, wp);
         }
         const int m = min(FT, n - j0);
+        if (FGS_NOCOMPUTE) {  // timing ablation (results wrong): the tile traffic alone
+        } else if (m == FT) {
+            fgs_fwd_chunk<NRHS, ROWS>(RT, U0, U1, Ct, lane, lam, p0, p1, cp);
+        } else {
 #pragma unroll 8
-        for (int jj = 0; jj < m; jj++) {
-            const int t = TileMap<ROWS>::tix(lane, jj);
-            const float r = RT[t];
-            const float lcp = lam * cp;
-            p0 = (U0[t] - lcp * p0) * r;
-            U0[t] = p0;
-            if (NRHS == 2) {
-                p1 = (U1[t] - lcp * p1) * r;
-                U1[t] = p1;
+            for (int jj = 0; jj < m; jj++) {
+                const int t = TileMap<ROWS>::tix(lane, jj);
+                const float r = RT[t];
+                const float lcp = lam * cp;
+                p0 = (U0[t] - lcp * p0) * r;
+                U0[t] = p0;
+                if (NRHS == 2) {
+                    p1 = (U1[t] - lcp * p1) * r;
+                    U1[t] = p1;
+                }
+                cp = Ct[t];
             }
-            cp = Ct[t];
         }
         __syncthreads();
         const uint32_t vc = voff0 + c * cstep;
@@ -639,15 +781,20 @@ __global__ void __launch_bounds__(64) k_fgs_solve(FgsSolveArgs a)
             if (NRHS == 2) p1 = U1[t];
             jj--;
         }
+        if (FGS_NOCOMPUTE) {
+        } else if (jj == FT - 1) {
+            fgs_bwd_chunk<NRHS, ROWS>(RT, U0, U1, lane, p0, p1);
+        } else {
 #pragma unroll 8
-        for (; jj >= 0; jj--) {
-            const int t = TileMap<ROWS>::tix(lane, jj);
-            const float f = RT[t];
-            p0 = U0[t] - f * p0;
-            U0[t] = p0;
-            if (NRHS == 2) {
-                p1 = U1[t] - f * p1;
-                U1[t] = p1;
+            for (; jj >= 0; jj--) {
+                const int t = TileMap<ROWS>::tix(lane, jj);
+                const float f = RT[t];
+                p0 = U0[t] - f * p0;
+                U0[t] = p0;
+                if (NRHS == 2) {
+                    p1 = U1[t] - f * p1;
+                    U1[t] = p1;
+                }
             }
         }
         __syncthreads();
