@@ -1635,8 +1635,8 @@ int wls_prepare(sm_ctx* ctx, const uint8_t* guide, size_t guide_pair, int guide_
 template <int NRHS>
 void launch_fgs_solve(bool rows, dim3 grid, hipStream_t st, const smk::FgsSolveArgs& fa)
 {
-    if (rows) hipLaunchKernelGGL((smk::k_fgs_solve<NRHS, true>), grid, dim3(64), 0, st, fa);
-    else hipLaunchKernelGGL((smk::k_fgs_solve<NRHS, false>), grid, dim3(64), 0, st, fa);
+    if (rows) hipLaunchKernelGGL((smk::k_fgs_solve<NRHS, true>), grid, dim3(64 * FGS_WAVES), 0, st, fa);
+    else hipLaunchKernelGGL((smk::k_fgs_solve<NRHS, false>), grid, dim3(64 * FGS_WAVES), 0, st, fa);
 }
 
 // npairs maps; pair i: displ/dispr at +i*disp_pair elements, guide at +i*guide_pair bytes.

@@ -360,6 +360,49 @@ __device__ inline void tile_store(rsrc_t rs, uint32_t voff, const float* T, int 
     }
 }
 
+// The same tile I/O split over the waves of a workgroup: wave w moves the tile's loads
+// k0 .. k0+NK-1 (k0 = NK*w, wave-uniform).
+template <bool ROWS, int NK>
+__device__ inline void tile_load_part(float4 (&r)[NK], rsrc_t rs, uint32_t voff, int wp, int k0)
+{
+#pragma unroll
+    for (int k = 0; k < NK; k++) {
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, (k0 + k) * 16 * wp, 0);
+        r[k] = make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+    }
+}
+
+template <bool ROWS, int NK>
+__device__ inline void tile_to_lds_part(const float4 (&r)[NK], float* T, int lane, int k0)
+{
+#pragma unroll
+    for (int k = 0; k < NK; k++) {
+        int ll, pl;
+        TileMap<ROWS>::at(k0 + k, lane, ll, pl);
+        T[TileMap<ROWS>::tix_e(ll, pl, 0)] = r[k].x;
+        T[TileMap<ROWS>::tix_e(ll, pl, 1)] = r[k].y;
+        T[TileMap<ROWS>::tix_e(ll, pl, 2)] = r[k].z;
+        T[TileMap<ROWS>::tix_e(ll, pl, 3)] = r[k].w;
+    }
+}
+
+template <bool ROWS, int NK>
+__device__ inline void tile_store_part(rsrc_t rs, uint32_t voff, const float* T, int wp, int lane, int k0)
+{
+#pragma unroll
+    for (int k = 0; k < NK; k++) {
+        int ll, pl;
+        TileMap<ROWS>::at(k0 + k, lane, ll, pl);
+        u32x4 v;
+        v[0] = __float_as_uint(T[TileMap<ROWS>::tix_e(ll, pl, 0)]);
+        v[1] = __float_as_uint(T[TileMap<ROWS>::tix_e(ll, pl, 1)]);
+        v[2] = __float_as_uint(T[TileMap<ROWS>::tix_e(ll, pl, 2)]);
+        v[3] = __float_as_uint(T[TileMap<ROWS>::tix_e(ll, pl, 3)]);
+        // offset in the VGPR (see tile_store)
+        __builtin_amdgcn_raw_buffer_store_b128(v, rs, voff + (uint32_t)((k0 + k) * 16 * wp), 0, 0);
+    }
+}
+
 template <int NRHS, bool ROWS, bool FAST = false>
 __global__ void __launch_bounds__(64) k_fgs(FgsArgs a)
 {
@@ -686,13 +729,25 @@ __device__ __forceinline__ void fgs_bwd_chunk(const float* RT, float* U0, float*
     }
 }
 
-// the right-hand-side sweeps of one pass given the pivots (64 lines per one-wave workgroup)
+// the right-hand-side sweeps of one pass given the pivots: 64 lines per workgroup of
+// FGS_WAVES waves.  Each wave moves 1/FGS_WAVES of every 64 x 64 tile between HBM and LDS
+// and runs the chains of 64/FGS_WAVES lines (its 64 lanes compute them FGS_WAVES times over
+// and store equal values).  With one wave per 64 lines a chunk's tile traffic (4 arrays in,
+// 2 out, 96 KB) was bound by what one wave keeps in flight: the KITTI row pass took 147 us,
+// of which the tile traffic alone (timing ablation FGS_NOCOMPUTE) was ~60.
+#ifndef FGS_WAVES
+#define FGS_WAVES 4
+#endif
 template <int NRHS, bool ROWS>
-__global__ void __launch_bounds__(64) k_fgs_solve(FgsSolveArgs a)
+__global__ void __launch_bounds__(64 * FGS_WAVES) k_fgs_solve(FgsSolveArgs a)
 {
 #pragma clang fp contract(off)
+    constexpr int NK = 16 / FGS_WAVES;  // tile loads per wave and array
     __shared__ float Ct[FT * FP], RT[FT * FP], U0[FT * FP], U1[NRHS == 2 ? FT * FP : 1];
-    const int lane = threadIdx.x, pair = blockIdx.y;
+    const int lane = threadIdx.x & 63, pair = blockIdx.y;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int k0 = wave * NK;
+    const int cl = wave * (64 / FGS_WAVES) + (lane % (64 / FGS_WAVES));  // the line this lane's chain runs
     const int n = ROWS ? a.w : a.h;
     const int l0 = blockIdx.x * FT, wp = a.wp;
     const uint64_t bytes = a.roi_pair * 4;
@@ -705,15 +760,15 @@ __global__ void __launch_bounds__(64) k_fgs_solve(FgsSolveArgs a)
     const uint32_t cstep = ROWS ? FT * 4 : (uint32_t)FT * wp * 4;
     const float lam = a.lam;
     const int nchunks = (n + FT - 1) / FT;
-    float4 rc[16], rr[16], r0[16], r1[16];
-    tile_load<ROWS>(rc, C, voff0, wp);
-    tile_load<ROWS>(rr, R, voff0, wp);
-    tile_load<ROWS>(r0, u0, voff0, wp);
-    if (NRHS == 2) tile_load<ROWS>(r1, u1, voff0, wp);
-    tile_to_lds<ROWS>(rc, Ct, lane);
-    tile_to_lds<ROWS>(rr, RT, lane);
-    tile_to_lds<ROWS>(r0, U0, lane);
-    if (NRHS == 2) tile_to_lds<ROWS>(r1, U1, lane);
+    float4 rc[NK], rr[NK], r0[NK], r1[NK];
+    tile_load_part<ROWS, NK>(rc, C, voff0, wp, k0);
+    tile_load_part<ROWS, NK>(rr, R, voff0, wp, k0);
+    tile_load_part<ROWS, NK>(r0, u0, voff0, wp, k0);
+    if (NRHS == 2) tile_load_part<ROWS, NK>(r1, u1, voff0, wp, k0);
+    tile_to_lds_part<ROWS, NK>(rc, Ct, lane, k0);
+    tile_to_lds_part<ROWS, NK>(rr, RT, lane, k0);
+    tile_to_lds_part<ROWS, NK>(r0, U0, lane, k0);
+    if (NRHS == 2) tile_to_lds_part<ROWS, NK>(r1, U1, lane, k0);
     float p0 = 0.f, p1 = 0.f, cp = 0.f;
     for (int c = 0; c < nchunks; c++) {
         const int j0 = c * FT;
@@ -721,19 +776,19 @@ __global__ void __launch_bounds__(64) k_fgs_solve(FgsSolveArgs a)
         __syncthreads();
         if (next) {  // prefetch chunk c+1 (consumed after the sweep)
             const uint32_t vn = voff0 + (c + 1) * cstep;
-            tile_load<ROWS>(rc, C, vn, wp);
-            tile_load<ROWS>(rr, R, vn, wp);
-            tile_load<ROWS>(r0, u0, vn, wp);
-            if (NRHS == 2) tile_load<ROWS>(r1, u1, vn, wp);
+            tile_load_part<ROWS, NK>(rc, C, vn, wp, k0);
+            tile_load_part<ROWS, NK>(rr, R, vn, wp, k0);
+            tile_load_part<ROWS, NK>(r0, u0, vn, wp, k0);
+            if (NRHS == 2) tile_load_part<ROWS, NK>(r1, u1, vn, wp, k0);
         }
         const int m = min(FT, n - j0);
         if (FGS_NOCOMPUTE) {  // timing ablation (results wrong): the tile traffic alone
         } else if (m == FT) {
-            fgs_fwd_chunk<NRHS, ROWS>(RT, U0, U1, Ct, lane, lam, p0, p1, cp);
+            fgs_fwd_chunk<NRHS, ROWS>(RT, U0, U1, Ct, cl, lam, p0, p1, cp);
         } else {
 #pragma unroll 8
             for (int jj = 0; jj < m; jj++) {
-                const int t = TileMap<ROWS>::tix(lane, jj);
+                const int t = TileMap<ROWS>::tix(cl, jj);
                 const float r = RT[t];
                 const float lcp = lam * cp;
                 p0 = (U0[t] - lcp * p0) * r;
@@ -747,21 +802,21 @@ __global__ void __launch_bounds__(64) k_fgs_solve(FgsSolveArgs a)
         }
         __syncthreads();
         const uint32_t vc = voff0 + c * cstep;
-        tile_store<ROWS>(u0, vc, U0, wp, lane);
-        if (NRHS == 2) tile_store<ROWS>(u1, vc, U1, wp, lane);
+        tile_store_part<ROWS, NK>(u0, vc, U0, wp, lane, k0);
+        if (NRHS == 2) tile_store_part<ROWS, NK>(u1, vc, U1, wp, lane, k0);
         if (next) {
             __syncthreads();
-            tile_to_lds<ROWS>(rc, Ct, lane);
-            tile_to_lds<ROWS>(rr, RT, lane);
-            tile_to_lds<ROWS>(r0, U0, lane);
-            if (NRHS == 2) tile_to_lds<ROWS>(r1, U1, lane);
+            tile_to_lds_part<ROWS, NK>(rc, Ct, lane, k0);
+            tile_to_lds_part<ROWS, NK>(rr, RT, lane, k0);
+            tile_to_lds_part<ROWS, NK>(r0, U0, lane, k0);
+            if (NRHS == 2) tile_to_lds_part<ROWS, NK>(r1, U1, lane, k0);
         }
     }
     // backward substitution; the last chunk's d' is still in LDS (RT takes c')
     {
         __syncthreads();
-        tile_load<ROWS>(rr, I, voff0 + (nchunks - 1) * cstep, wp);
-        tile_to_lds<ROWS>(rr, RT, lane);
+        tile_load_part<ROWS, NK>(rr, I, voff0 + (nchunks - 1) * cstep, wp, k0);
+        tile_to_lds_part<ROWS, NK>(rr, RT, lane, k0);
     }
     for (int c = nchunks - 1; c >= 0; c--) {
         const int j0 = c * FT;
@@ -769,25 +824,25 @@ __global__ void __launch_bounds__(64) k_fgs_solve(FgsSolveArgs a)
         __syncthreads();
         if (prev) {
             const uint32_t vp = voff0 + (c - 1) * cstep;
-            tile_load<ROWS>(rr, I, vp, wp);
-            tile_load<ROWS>(r0, u0, vp, wp);
-            if (NRHS == 2) tile_load<ROWS>(r1, u1, vp, wp);
+            tile_load_part<ROWS, NK>(rr, I, vp, wp, k0);
+            tile_load_part<ROWS, NK>(r0, u0, vp, wp, k0);
+            if (NRHS == 2) tile_load_part<ROWS, NK>(r1, u1, vp, wp, k0);
         }
         const int m = min(FT, n - j0);
         int jj = m - 1;
         if (c == nchunks - 1) {  // x[n-1] = d'[n-1]
-            const int t = TileMap<ROWS>::tix(lane, jj);
+            const int t = TileMap<ROWS>::tix(cl, jj);
             p0 = U0[t];
             if (NRHS == 2) p1 = U1[t];
             jj--;
         }
         if (FGS_NOCOMPUTE) {
         } else if (jj == FT - 1) {
-            fgs_bwd_chunk<NRHS, ROWS>(RT, U0, U1, lane, p0, p1);
+            fgs_bwd_chunk<NRHS, ROWS>(RT, U0, U1, cl, p0, p1);
         } else {
 #pragma unroll 8
             for (; jj >= 0; jj--) {
-                const int t = TileMap<ROWS>::tix(lane, jj);
+                const int t = TileMap<ROWS>::tix(cl, jj);
                 const float f = RT[t];
                 p0 = U0[t] - f * p0;
                 U0[t] = p0;
@@ -799,13 +854,13 @@ __global__ void __launch_bounds__(64) k_fgs_solve(FgsSolveArgs a)
         }
         __syncthreads();
         const uint32_t vc = voff0 + c * cstep;
-        tile_store<ROWS>(u0, vc, U0, wp, lane);
-        if (NRHS == 2) tile_store<ROWS>(u1, vc, U1, wp, lane);
+        tile_store_part<ROWS, NK>(u0, vc, U0, wp, lane, k0);
+        if (NRHS == 2) tile_store_part<ROWS, NK>(u1, vc, U1, wp, lane, k0);
         if (prev) {
             __syncthreads();
-            tile_to_lds<ROWS>(rr, RT, lane);
-            tile_to_lds<ROWS>(r0, U0, lane);
-            if (NRHS == 2) tile_to_lds<ROWS>(r1, U1, lane);
+            tile_to_lds_part<ROWS, NK>(rr, RT, lane, k0);
+            tile_to_lds_part<ROWS, NK>(r0, U0, lane, k0);
+            if (NRHS == 2) tile_to_lds_part<ROWS, NK>(r1, U1, lane, k0);
         }
     }
 }
