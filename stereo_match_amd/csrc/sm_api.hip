@@ -95,6 +95,9 @@ constexpr int DBG_NARROW_SWEEPS = 1 << 19, DBG_WIDE_SWEEPS = 1 << 21;
 // 4096: per-direction engine (one path volume per direction + k_wta) instead of the fused sweeps
 constexpr int DBG_LEGACY = 4096, DBG_SWEEP1 = 8192, DBG_SWEEP8 = 16384, DBG_HYBRID = 32768;
 constexpr int DBG_COST_TILE = 1 << 22;
+// 1 << 20 (valid results): compute_disparity runs its right matcher beside the left one on
+// the twin context's stream instead of before it on the caller's stream
+constexpr int DBG_CONCURRENT_LR = 1 << 20;
 // 1 << 23 (valid results): raise every fused-sweep group's give-up flag, so the
 // guarded per-direction fallback recomputes the group (tests the recovery path)
 constexpr int DBG_FORCE_FALLBACK = 1 << 23;
@@ -126,7 +129,7 @@ struct sm_ctx {
     void* pin = nullptr;    // page-locked host staging of the host-pointer entry points (HostStage)
     size_t pin_n = 0;
     // compute_disparity: the right matcher runs on a twin context (own streams and
-    // buffers) beside the left one; created on first use, destroyed with this one
+    // buffers); created on first use, destroyed with this one
     sm_ctx* twin = nullptr;
     hipEvent_t ev_lr_fork = nullptr, ev_lr_join = nullptr;
     std::vector<uint32_t> cu_mask;  // sm_set_cu_mask words (applied to the twin too)
@@ -2246,8 +2249,8 @@ int sm_compute_disparity_batch_device(sm_ctx* ctx, const uint8_t* dL, const uint
     lm.uniqueness_ratio = 0;             // createDisparityWLSFilter (:172) mutates the left one
     lm.disp12_max_diff = 1000000;
     lm.speckle_window_size = 0;
-    // the two matchers are independent: the right one runs on the twin context's
-    // stream beside the left one (a single pair fills a fraction of the chip)
+    // the two matchers are independent: the right one runs on the twin context (its own
+    // buffers), on the caller's stream before the left one (flag 1 << 20: beside it)
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     int rc;
     if (!ctx->twin) {
@@ -2278,10 +2281,17 @@ int sm_compute_disparity_batch_device(sm_ctx* ctx, const uint8_t* dL, const uint
         HIP_TRY(ctx, hipEventRecord(ctx->ev_wls_ready, ctx->wls_stream));
     }
     HIP_TRY(ctx, hipEventRecord(ctx->ev_lr_fork, ctx->stream));
+    // one matcher after the other: side by side they only shared the HBM bandwidth (KITTI
+    // D = 160, one pair: matchers 1.32 ms concurrent, 1.22 ms in sequence; per matcher the
+    // per-direction path kernel took 665 vs 332 us)
+    const bool serial = (ctx->dbg_flags & DBG_CONCURRENT_LR) == 0;
+    const hipStream_t tw_stream = tw->stream;
+    if (serial) tw->stream = ctx->stream;
     HIP_TRY(ctx, hipStreamWaitEvent(tw->stream, ctx->ev_lr_fork, 0));
     rc = sm_compute_batch_device(tw, dR, dL, npairs, pair_stride, H, W, stride, &rm, d_dispr);
+    tw->stream = tw_stream;
     if (rc != SM_OK) return fail(ctx, rc, "right matcher: %s", tw->err.c_str());
-    HIP_TRY(ctx, hipEventRecord(ctx->ev_lr_join, tw->stream));
+    HIP_TRY(ctx, hipEventRecord(ctx->ev_lr_join, serial ? ctx->stream : tw->stream));
     rc = sm_compute_batch_device(ctx, dL, dR, npairs, pair_stride, H, W, stride, &lm, d_displ);
     HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_lr_join, 0));  // joined on every path
     if (prep) HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_wls_ready, 0));

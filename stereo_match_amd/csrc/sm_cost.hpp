@@ -98,6 +98,14 @@ struct Cost8Args {
 #endif
 constexpr int C8_TX = 64, C8_RY = CENSUS_COST_RY;
 
+// (a << 8) | b in one VALU op (hipcc re-associates the shift-or chain into separate shifts)
+__device__ __forceinline__ uint32_t lshl8_or(uint32_t a, uint32_t b)
+{
+    uint32_t r;
+    asm("v_lshl_or_b32 %0, %1, 8, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
 __global__ void __launch_bounds__(256) k_census_cost8(Cost8Args a)
 {
     __shared__ uint64_t lc[C8_TX];
@@ -127,8 +135,12 @@ __global__ void __launch_bounds__(256) k_census_cost8(Cost8Args a)
                 uint32_t w[4];
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
-                    w[q] = (uint32_t)__popcll(l ^ rr[-4 * q]) | ((uint32_t)__popcll(l ^ rr[-4 * q - 1]) << 8) |
-                           ((uint32_t)__popcll(l ^ rr[-4 * q - 2]) << 16) | ((uint32_t)__popcll(l ^ rr[-4 * q - 3]) << 24);
+                    // packed as a shift-or chain (one v_lshl_or_b32 per byte; the or-tree of
+                    // separate shifts took two VALU ops per byte)
+                    uint32_t v = (uint32_t)__popcll(l ^ rr[-4 * q - 3]);
+                    v = lshl8_or(v, (uint32_t)__popcll(l ^ rr[-4 * q - 2]));
+                    v = lshl8_or(v, (uint32_t)__popcll(l ^ rr[-4 * q - 1]));
+                    w[q] = lshl8_or(v, (uint32_t)__popcll(l ^ rr[-4 * q]));
                 }
                 tile[xl * pitch + ch] = make_uint4(w[0], w[1], w[2], w[3]);
             }
