@@ -738,6 +738,9 @@ __device__ __forceinline__ void fgs_bwd_chunk(const float* RT, float* U0, float*
 #ifndef FGS_WAVES
 #define FGS_WAVES 4
 #endif
+#ifndef FGS_SPLIT
+#define FGS_SPLIT 1
+#endif
 template <int NRHS, bool ROWS>
 __global__ void __launch_bounds__(64 * FGS_WAVES) k_fgs_solve(FgsSolveArgs a)
 {
@@ -769,6 +772,13 @@ __global__ void __launch_bounds__(64 * FGS_WAVES) k_fgs_solve(FgsSolveArgs a)
     tile_to_lds_part<ROWS, NK>(rr, RT, lane, k0);
     tile_to_lds_part<ROWS, NK>(r0, U0, lane, k0);
     if (NRHS == 2) tile_to_lds_part<ROWS, NK>(r1, U1, lane, k0);
+    // FGS_SPLIT: the two right-hand sides run on different lanes (lanes with bit 4 set take
+    // u[1]), so every chain is scalar single-issue arithmetic instead of packed pairs
+    constexpr bool SPLIT = NRHS == 2 && FGS_SPLIT;
+    static_assert(!SPLIT || 64 / FGS_WAVES <= 16, "split chains need lanes 16..31 to repeat lanes 0..15's lines");
+    constexpr int NC = SPLIT ? 1 : NRHS;  // chains per lane
+    float* const UA = SPLIT && (lane & 16) ? U1 : U0;
+    float* const UB = U1;
     float p0 = 0.f, p1 = 0.f, cp = 0.f;
     for (int c = 0; c < nchunks; c++) {
         const int j0 = c * FT;
@@ -784,18 +794,18 @@ __global__ void __launch_bounds__(64 * FGS_WAVES) k_fgs_solve(FgsSolveArgs a)
         const int m = min(FT, n - j0);
         if (FGS_NOCOMPUTE) {  // timing ablation (results wrong): the tile traffic alone
         } else if (m == FT) {
-            fgs_fwd_chunk<NRHS, ROWS>(RT, U0, U1, Ct, cl, lam, p0, p1, cp);
+            fgs_fwd_chunk<NC, ROWS>(RT, UA, UB, Ct, cl, lam, p0, p1, cp);
         } else {
 #pragma unroll 8
             for (int jj = 0; jj < m; jj++) {
                 const int t = TileMap<ROWS>::tix(cl, jj);
                 const float r = RT[t];
                 const float lcp = lam * cp;
-                p0 = (U0[t] - lcp * p0) * r;
-                U0[t] = p0;
-                if (NRHS == 2) {
-                    p1 = (U1[t] - lcp * p1) * r;
-                    U1[t] = p1;
+                p0 = (UA[t] - lcp * p0) * r;
+                UA[t] = p0;
+                if (NC == 2) {
+                    p1 = (UB[t] - lcp * p1) * r;
+                    UB[t] = p1;
                 }
                 cp = Ct[t];
             }
@@ -832,23 +842,23 @@ __global__ void __launch_bounds__(64 * FGS_WAVES) k_fgs_solve(FgsSolveArgs a)
         int jj = m - 1;
         if (c == nchunks - 1) {  // x[n-1] = d'[n-1]
             const int t = TileMap<ROWS>::tix(cl, jj);
-            p0 = U0[t];
-            if (NRHS == 2) p1 = U1[t];
+            p0 = UA[t];
+            if (NC == 2) p1 = UB[t];
             jj--;
         }
         if (FGS_NOCOMPUTE) {
         } else if (jj == FT - 1) {
-            fgs_bwd_chunk<NRHS, ROWS>(RT, U0, U1, cl, p0, p1);
+            fgs_bwd_chunk<NC, ROWS>(RT, UA, UB, cl, p0, p1);
         } else {
 #pragma unroll 8
             for (; jj >= 0; jj--) {
                 const int t = TileMap<ROWS>::tix(cl, jj);
                 const float f = RT[t];
-                p0 = U0[t] - f * p0;
-                U0[t] = p0;
-                if (NRHS == 2) {
-                    p1 = U1[t] - f * p1;
-                    U1[t] = p1;
+                p0 = UA[t] - f * p0;
+                UA[t] = p0;
+                if (NC == 2) {
+                    p1 = UB[t] - f * p1;
+                    UB[t] = p1;
                 }
             }
         }
