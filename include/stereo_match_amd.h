@@ -316,7 +316,9 @@ long long sm_debug_fetch(sm_ctx* ctx, int what, void* host, size_t bytes);
  *   8, 512   16-lane vertical / 64-lane horizontal lines in the per-direction engine;
  *   1024, 2048  census Hamming costs on the fly (all / horizontal directions);
  *   1 << 22  tiled SGBM cost kernel;  bits 16-18 launch-group size cap;
- *   1 << 30  no Infinity-Cache-sized launch groups for the per-direction engine.
+ *   1 << 30  no Infinity-Cache-sized launch groups for the per-direction engine;
+ *   1 << 20  sm_compute_disparity*: the right matcher beside the left one on the twin
+ *            context's stream (default: before it, on the caller's stream).
  * The measured ablations (row-WTA kernel 16/32, k_sweep2 128 / 1 << 27, hybrid engine
  * 32768) and the timing switches whose results are wrong (1, 2, 4, 1 << 24..26,
  * 1 << 28, 1 << 29, 1 << 31) exist only in the ablation build (make ablation ->

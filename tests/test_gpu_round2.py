@@ -228,7 +228,7 @@ def test_valid_result_flags_leave_compute_disparity_unchanged(eng, D):
     wp = wf.params(H, W)
     ref = eng.compute_disparity(gl, gr, prm, wp)
     for f in (8, 64, 128, 256, 1 << 12, 1 << 13, 1 << 14, (1 << 14) | 128, (1 << 14) | 256, (1 << 14) | (1 << 19), 1 << 15,
-              1 << 19, 1 << 21, 1 << 22, 1 << 23, 1 << 27, 1 << 30, 2 << 16):
+              1 << 19, 1 << 20, (1 << 20) | (1 << 14), 1 << 21, 1 << 22, 1 << 23, 1 << 27, 1 << 30, 2 << 16):
         if f & ABLATION_FLAGS and not ablation_build():
             continue
         eng.set_debug_flags(f)
@@ -237,6 +237,38 @@ def test_valid_result_flags_leave_compute_disparity_unchanged(eng, D):
         finally:
             eng.set_debug_flags(0)
         assert np.array_equal(got[0], ref[0]) and np.array_equal(got[1], ref[1]), f
+
+
+def test_compute_disparity_on_a_caller_stream(eng):
+    """After sm_set_stream the right matcher (twin context) still forks from and joins back
+    into the caller's stream, in sequence (default) and side by side (flag 1 << 20)."""
+    import torch
+
+    import stereo_match_amd as sm
+    from stereo_match_amd import wls
+    from stereo_match_amd.stereo_vision import matcher_from_settings
+
+    D = 64
+    s = dict(sm.DEFAULT_SETTINGS, window_size=5, num_disparities=D)
+    H, W = 96, 300
+    gl, gr, _ = synthetic.random_dot_pair(H, W, D, seed=11)
+    lm = matcher_from_settings(s)
+    prm = lm.params()
+    wf = wls.createDisparityWLSFilter(lm)
+    wf.setLambda(s["lmbda"])
+    wf.setSigmaColor(s["sigma"])
+    wp = wf.params(H, W)
+    ref = eng.compute_disparity(gl, gr, prm, wp)
+    st = torch.cuda.Stream()
+    eng.set_stream(st.cuda_stream)
+    try:
+        for f in (0, 1 << 20):
+            eng.set_debug_flags(f)
+            got = eng.compute_disparity(gl, gr, prm, wp)
+            assert np.array_equal(got[0], ref[0]) and np.array_equal(got[1], ref[1]), f
+    finally:
+        eng.set_debug_flags(0)
+        eng.set_stream(None)
 
 
 def test_product_library_rejects_ablation_flags(eng):

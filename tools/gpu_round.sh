@@ -29,6 +29,8 @@ if [ "$PART" = A ] || [ "$PART" = T ]; then
   done
   cp "$OUT/census8_traffic.json" profiles/traffic_latest.json
   cp "$OUT/census8_valu.json" profiles/valu_latest.json
+  [ "$PART" = T ] || step valu_rate 120 ./tools/ubench/valu_rate
+  [ "$PART" = T ] || FLAGS=0 step single 400 bash tools/gpu_single.sh $TAG
   step bench 400 python -u bench.py --traffic-file "$OUT/census8_traffic.json"
   step bench_sgbm5 400 python -u bench.py --mode sgbm5 --traffic-file "$OUT/sgbm5_traffic.json" --valu-file "$OUT/sgbm5_valu.json"
 else
