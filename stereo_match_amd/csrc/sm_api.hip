@@ -1279,6 +1279,12 @@ int run_group(sm_ctx* ctx, const Src& src, const Geo& g, const Norm& n, int16_t*
     }
     if ((rc = ensure(ctx, bs.L, g.L_pair * G)) != SM_OK) return rc;
     if ((rc = ensure(ctx, bs.raw, (size_t)G * H * W * 2)) != SM_OK) return rc;
+    // the sweeps' give-up flag of this buffer set, cleared by the group's first kernel
+    uint32_t* gflag = nullptr;
+    if (g.sweep) {
+        if ((rc = ensure_sweep_err(ctx)) != SM_OK) return rc;
+        gflag = (uint32_t*)ctx->sweep_err.p + ERR_GROUP0 + s;
+    }
     if (n.wide) {
         if ((rc = run_wide(ctx, src, g, n, bs)) != SM_OK) return rc;
         return finish_group(ctx, g, n, bs, s, d_out, ctx->stream);
@@ -1297,6 +1303,7 @@ int run_group(sm_ctx* ctx, const Src& src, const Geo& g, const Norm& n, int16_t*
             ca.H = H;
             ca.W = W;
             ca.stride = g.stride;
+            ca.zero_word = gflag;
             hipLaunchKernelGGL(smk::k_census9x7,
                                dim3((W + smk::CT_W - 1) / smk::CT_W, (H + smk::CT_H - 1) / smk::CT_H, 2 * G),
                                dim3(256), 0, ctx->stream, ca);
@@ -1337,6 +1344,7 @@ int run_group(sm_ctx* ctx, const Src& src, const Geo& g, const Norm& n, int16_t*
             va.offset = src.offset;
             va.scale = src.scale;
             va.nt = cost_nt(g, 2);
+            va.zero_word = gflag;
             // 64-column tiles measured faster than 128 (117 vs 130 us/pair at D=192)
             hipLaunchKernelGGL(smk::k_cost_volume_f32<64>, dim3((n.width1 + 63) / 64, H, G), dim3(256),
                                (size_t)64 * (n.D / 2 + 1) * 4, ctx->stream, va);
@@ -1354,6 +1362,7 @@ int run_group(sm_ctx* ctx, const Src& src, const Geo& g, const Norm& n, int16_t*
             pf.stride = g.stride;
             pf.ftzero = n.ftzero;
             pf.cn = 1;
+            pf.zero_word = gflag;
             hipLaunchKernelGGL(smk::k_sgbm_prefilter, dim3((W + 255) / 256, (H + smk::PF_ROWS - 1) / smk::PF_ROWS, 2 * G), dim3(256), 0, ctx->stream, pf);
             HIP_TRY(ctx, hipGetLastError());
             smk::SgbmCostArgs sc{};
@@ -1395,9 +1404,6 @@ int run_group(sm_ctx* ctx, const Src& src, const Geo& g, const Norm& n, int16_t*
         // 5 paths: the WTA sweep of this group overlaps the next group's cost + E/W
         // (the 8-path sweeps keep the second stream for their E/W fork)
         const hipStream_t ws = n.ndirs == 5 ? stream_b(ctx) : ctx->stream;
-        if ((rc = ensure_sweep_err(ctx)) != SM_OK) return rc;
-        uint32_t* gflag = (uint32_t*)ctx->sweep_err.p + ERR_GROUP0 + s;
-        HIP_TRY(ctx, hipMemsetAsync(gflag, 0, 4, ctx->stream));
         if ((rc = run_sweep(ctx, n, g, bs, ws, gflag)) != SM_OK) return rc;
         // Strips of a sweep wait on their neighbours, so all of a launch's strips must be
         // resident together; the grid is sized for that (sweep_pass), but work on other

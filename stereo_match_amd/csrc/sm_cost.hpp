@@ -17,7 +17,14 @@ struct CensusArgs {
     uint64_t* out[2];       // census left / right [pair][H][W]
     size_t in_pair;         // bytes between consecutive pairs' images
     int H, W, stride;
+    uint32_t* zero_word;    // non-null: cleared by the first thread (the launch group's sweep flag)
 };
+
+// the launch group's first kernel clears its sweep give-up flag (instead of a memset node)
+__device__ __forceinline__ void clear_group_flag(uint32_t* w)
+{
+    if (w && threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0) *w = 0u;
+}
 
 constexpr int CT_W = 64, CT_H = 16, CT_PY = 4;  // tile; pixels per thread (vertical)
 constexpr int CT_LW = CT_W + 12;                 // LDS row: 4 left halo + 64 + 4 right halo, dword padded
@@ -32,6 +39,7 @@ constexpr int CT_LW = CT_W + 12;                 // LDS row: 4 left halo + 64 + 
 // 7-row windows share their LDS reads.
 __global__ void __launch_bounds__(256) k_census9x7(CensusArgs a)
 {
+    clear_group_flag(a.zero_word);
     __shared__ uint32_t tile[CT_H + 6][CT_LW / 4];
     const int which = blockIdx.z & 1, pair = blockIdx.z >> 1;
     const uint8_t* img = a.img[which] + (size_t)pair * a.in_pair;
@@ -197,6 +205,7 @@ struct PrefilterArgs {
     uint8_t* planes;  // packed uint2 per pixel, [pair][view][channel][H][W]
     int H, W, stride, ftzero;
     int cn;  // channels per pixel (1 gray, 3 BGR interleaved; 0 = 1); stride in bytes
+    uint32_t* zero_word;  // see CensusArgs
 };
 
 // Packed per-pixel planes for the BT cost: one uint2 per pixel per view,
@@ -215,6 +224,7 @@ constexpr int PF_ROWS = PREFILTER_ROWS;
 // left the launch dominated by its 2*H*pairs tiny workgroups).
 __global__ void __launch_bounds__(256) k_sgbm_prefilter(PrefilterArgs a)
 {
+    clear_group_flag(a.zero_word);
     __shared__ uint8_t rows[PF_ROWS + 2][260];
     __shared__ int gs[PF_ROWS][258];
     const int cn = a.cn > 0 ? a.cn : 1;
@@ -668,6 +678,7 @@ struct VolArgs {
     int H, W, width1, D, minX1;
     int nt;  // 1: nontemporal stores (the launch group's volume exceeds the Infinity Cache)
     float offset, scale;
+    uint32_t* zero_word;  // see CensusArgs
 };
 
 __device__ inline uint32_t quant_cost(float c, float off, float sc)
@@ -684,6 +695,7 @@ __device__ inline uint32_t quant_cost(float c, float off, float sc)
 template <int TX>
 __global__ void __launch_bounds__(256) k_cost_volume_f32(VolArgs a)
 {
+    clear_group_flag(a.zero_word);
     constexpr int PL = TX / 64;         // floats per lane per plane row
     extern __shared__ uint32_t tile[];  // [TX][D/2 + 1] packed u16 pairs (d even | d odd << 16)
     const int half = a.D >> 1, rowdw = half + 1;
