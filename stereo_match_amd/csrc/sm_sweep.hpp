@@ -319,6 +319,12 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
     using G = SweepGeo<VL, DPL, NCW_>;
     constexpr bool UP = MODE == 2;
     constexpr bool WTA = MODE != 0;
+    // the down sweep shares its SIMDs with the E/W kernel (8 paths): its waves take issue
+    // priority, the E/W waves fill the cycles it leaves (SWEEP_PRIO 0 = default priority)
+#ifndef SWEEP_PRIO
+#define SWEEP_PRIO 2
+#endif
+    if constexpr (MODE == 0 && SWEEP_PRIO > 0) __builtin_amdgcn_s_setprio(SWEEP_PRIO);
     // neighbour-counter row sync: KITTI 8 pairs, down sweep census8 96.4 -> 92.0 us per pair,
     // sgbm8 124.0 -> 120.8, census8 WTA sweep level (96.6 / 96.0); the 5-path WTA sweep is
     // slower with it (95.3 -> 97.9) and keeps the row barriers
