@@ -26,6 +26,13 @@
 extern "C" {
 #endif
 
+/* ABI version.  3: sm_compute takes the nullable wta_out (9 arguments; SURVEY §8b's
+ * signature).  The shared object carries it in its soname (libstereo_match_amd.so.3), so a
+ * binary linked against an older ABI fails to load instead of passing a stray pointer as
+ * wta_out; dlopen/ctypes callers compare sm_abi_version() with the value they were written
+ * against (stereo_match_amd/_lib.py does). */
+#define SM_ABI_VERSION 3
+
 #define SM_OK 0
 #define SM_E_ARG (-1)         /* bad argument: mirrors OpenCV's CV_Assert failures */
 #define SM_E_HIP (-2)         /* HIP runtime / launch error */
@@ -43,7 +50,7 @@ extern "C" {
  * and normalised exactly as OpenCV does (P1<=0 -> 2, ...). */
 typedef struct sm_params {
     int min_disparity;
-    int num_disparities; /* > 0, multiple of 16 (OpenCV asserts this) */
+    int num_disparities; /* > 0, multiple of 16 (OpenCV asserts this); cost volumes: any 1..256 */
     int block_size;      /* SADWindowSize; <= 0 -> 5 */
     int P1, P2;
     int disp12_max_diff;
@@ -116,7 +123,10 @@ int sm_compute_batch_device_cn(sm_ctx* ctx, const uint8_t* d_left, const uint8_t
  * one as float32 (1, D, H, W) at mapTo3D_mc_cnn.py:71 and feeds its
  * disparities to the WLS filter, :81-100).  cost: float32 [D][H][W], d-major,
  * plane d = cost of left x against right x - (min_disparity + d); D must equal
- * p->num_disparities.  Costs are quantised q = rint((c + offset) * scale)
+ * p->num_disparities, any value in 1..256 (OpenCV's multiple-of-16 rule is
+ * StereoSGBM's own; mc-cnn's -disp_max 228 volume has 228 planes: the kernels
+ * run the next multiple of 16 with pad planes that never win).
+ * Costs are quantised q = rint((c + offset) * scale)
  * (float32), clamped to [0, 4095], NaN -> 4095, then aggregated with the
  * path recurrence / WTA / uniqueness / sub-pixel / LR / median of
  * sm_compute (p->mode paths; block_size and pre_filter_cap unused;
@@ -330,6 +340,8 @@ const char* sm_last_error(sm_ctx* ctx);
 
 /* Library version string. */
 const char* sm_version(void);
+/* SM_ABI_VERSION the library was built with. */
+int sm_abi_version(void);
 
 #ifdef __cplusplus
 }

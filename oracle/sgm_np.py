@@ -380,10 +380,12 @@ def wta(S: np.ndarray, H, W, prm):
            & (np.abs(best[..., None] - dd) > 1)).any(-1)
     sat = minS >= MAX_COST                               # OpenCV bestDisp == -1
     valid = ~bad & ~sat
-    bi = np.clip(best, 1, D - 2)
-    Sm = np.take_along_axis(S, (bi - 1)[..., None], -1)[..., 0]
+    # neighbours clamped into [0, D) (only 0 < best < D-1 uses them; an external volume may
+    # have D < 3 planes)
+    bi = np.clip(best, 0, D - 1)
+    Sm = np.take_along_axis(S, np.clip(bi - 1, 0, D - 1)[..., None], -1)[..., 0]
     S0 = np.take_along_axis(S, bi[..., None], -1)[..., 0]
-    Sq = np.take_along_axis(S, (bi + 1)[..., None], -1)[..., 0]
+    Sq = np.take_along_axis(S, np.clip(bi + 1, 0, D - 1)[..., None], -1)[..., 0]
     den = np.maximum(Sm + Sq - 2 * S0, 1)
     sub = best * DISP_SCALE + _cdiv((Sm - Sq) * DISP_SCALE + den, 2 * den)
     inner = (best > 0) & (best < D - 1)

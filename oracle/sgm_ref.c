@@ -234,7 +234,9 @@ static int compute_core(const uint8_t* img1, const uint8_t* img2, int H, int W, 
         W <= 0)
         return -1;
     int minD = prm->min_disparity, D = prm->num_disparities, maxD = minD + D;
-    if (D <= 0 || D % 16) return -1;
+    /* OpenCV's StereoSGBM asserts D % 16 == 0; an external cost volume (mc-cnn: D = 228,
+     * mapTo3D_mc_cnn.py:71) has as many planes as it was made with, so D is free there */
+    if (D <= 0 || (D % 16 && !vol)) return -1;
     int bs = prm->block_size > 0 ? prm->block_size : 5;
     int ftzero = imax(prm->pre_filter_cap, 15) | 1;
     int uniq = prm->uniqueness_ratio >= 0 ? prm->uniqueness_ratio : 10;

@@ -60,9 +60,12 @@ class SmBmParams(ctypes.Structure):
         return {n: getattr(self, n) for n, _ in self._fields_}
 
 
+ABI_VERSION = 3  # include/stereo_match_amd.h SM_ABI_VERSION this binding is written against
+
 _c = ctypes
 _SIGS = {
     "sm_version": (_c.c_char_p, []),
+    "sm_abi_version": (_c.c_int, []),
     "sm_create": (_c.c_int, [_c.c_int, _c.POINTER(_c.c_void_p)]),
     "sm_destroy": (None, [_c.c_void_p]),
     "sm_set_stream": (_c.c_int, [_c.c_void_p, _c.c_void_p]),
@@ -182,6 +185,10 @@ def load():
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
+        abi = lib.sm_abi_version()
+        if abi != ABI_VERSION:
+            raise ImportError(f"{LIB_PATH} has C-ABI version {abi}, this binding needs {ABI_VERSION}: rebuild it "
+                              "with `make -C stereo_match_amd/csrc`")
         _lib = lib
         return lib
 

@@ -1,11 +1,21 @@
 """Pair-level data parallelism: one process per GPU, pairs sharded in
-contiguous blocks, optional gather of the int16 disparity maps to rank 0.
+contiguous blocks, gather of the int16 disparity maps to rank 0.
 
 The reference processes one pair per call (``disparity_calculation.py:289``)
 and has no distributed code.  Pairs are independent, so the
 data path needs no collective; the only exchange is delivering results to
 the root (BASELINE config "64 KITTI pairs sharded 8-per-GPU, gather over
-xGMI"), done with ``torch.distributed.gather`` (RCCL on ROCm, gloo on CPU).
+xGMI").
+
+The gather is a set of point-to-point transfers (``torch.distributed``
+``batch_isend_irecv``: RCCL on ROCm, gloo on CPU): rank r sends its block,
+rank 0 receives it straight into rows ``[start_r, start_r + count_r)`` of a
+preallocated ``[npairs, H, W]`` result, so there is no padding of uneven
+blocks and no concatenation on the root, and rank 0 computes its own block
+directly into its rows.  Each peer uses its own xGMI link to the root, so the
+transfers form a one-hop star, not a ring.  ``OverlappedGather`` runs step k's
+transfers on a side stream while step k+1 computes into the other of two
+buffers ("gather pair i while computing pair i+1").
 """
 from __future__ import annotations
 
@@ -26,33 +36,192 @@ def shard_range(npairs: int, rank: int, world: int):
     return start, base + (1 if rank < extra else 0)
 
 
-def gather_to_root(local, npairs: int, group=None):
-    """Gather each rank's [count, H, W] int16 block to rank 0 (pair order kept).
+def _bytes(t):
+    """Raw-byte view of a contiguous tensor (RCCL and gloo have no int16 type)."""
+    import torch
+
+    return t.contiguous().view(torch.uint8)
+
+
+def _gather_ops(local, out, npairs: int, group=None):
+    """P2P operations of one gather: non-root ranks send ``local`` to rank 0;
+    rank 0 receives every other rank's block into its rows of ``out``."""
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    ops = []
+    if rank == 0:
+        for r in range(1, world):
+            s, c = shard_range(npairs, r, world)
+            if c:
+                ops.append(dist.P2POp(dist.irecv, _bytes(out[s:s + c]), dist.get_global_rank(group, r)
+                                      if group is not None else r, group))
+    elif local.shape[0]:
+        ops.append(dist.P2POp(dist.isend, _bytes(local), dist.get_global_rank(group, 0)
+                              if group is not None else 0, group))
+    return ops
+
+
+def gather_to_root(local, npairs: int, group=None, out=None):
+    """Gather each rank's [count, H, W] block to rank 0 (pair order kept).
 
     ``local`` is a torch tensor on this rank's device (CUDA under RCCL, CPU
-    under gloo).  Ranks with uneven counts are padded to the largest block.
-    Returns the [npairs, H, W] tensor on rank 0 and None elsewhere.
+    under gloo).  On rank 0 the blocks land in ``out`` (a preallocated
+    [npairs, H, W] tensor of local's dtype and device; allocated if None) by
+    point-to-point receives into its row ranges: uneven blocks need no padding
+    and the root concatenates nothing.  Rank 0's own block is copied into its
+    rows unless ``local`` already is that view.  Returns ``out`` on rank 0 and
+    None elsewhere.  Synchronous for the caller's stream.
     """
     import torch
     import torch.distributed as dist
 
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    counts = [shard_range(npairs, r, world)[1] for r in range(world)]
-    cmax = max(counts) if counts else 0
     H, W = local.shape[1:]
-    buf = local
-    if local.shape[0] < cmax:
-        buf = torch.zeros((cmax, H, W), dtype=local.dtype, device=local.device)
-        buf[:local.shape[0]] = local
-    # RCCL/NCCL and gloo have no int16 type: move the maps as raw bytes.
-    raw = buf.contiguous().view(torch.uint8)
     if rank == 0:
-        parts = [torch.empty_like(raw) for _ in range(world)]
-        dist.gather(raw, gather_list=parts, dst=0, group=group)
-        return torch.cat([p.view(local.dtype)[:c] for p, c in zip(parts, counts)], 0)
-    dist.gather(raw, dst=0, group=group)
-    return None
+        if out is None:
+            out = torch.empty((npairs, H, W), dtype=local.dtype, device=local.device)
+        s, c = shard_range(npairs, 0, world)
+        if c and local.data_ptr() != out[s:s + c].data_ptr():
+            out[s:s + c].copy_(local)
+    ops = _gather_ops(local, out, npairs, group)
+    if ops:
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+    return out if rank == 0 else None
+
+
+class OverlappedGather:
+    """Double-buffered gather of each step's maps to rank 0, overlapped with the
+    next step's compute.
+
+    Step k computes into ``buffer(k)``: on rank 0 that is a view of the rows
+    it owns in ``result(k)`` (the [npairs, H, W] maps of step k), elsewhere a
+    [count, H, W] block.  ``launch(k)`` starts step k's transfers once the
+    caller's current stream has produced the block; on CUDA they run on a side
+    stream (RCCL's own stream waits for it), so the caller's stream goes on
+    with step k+1 at once.  ``buffer(k + depth)`` makes the caller's stream
+    wait for step k's transfers before the buffer is overwritten.  On CPU
+    (gloo) the transfers are asynchronous works completed at the same points.
+
+    ``exposed_ms()`` (CUDA): the time the caller's stream stood waiting for a
+    gather (events around every wait, ``drain`` included), i.e. the part of
+    the gather that compute did not hide.
+    """
+
+    def __init__(self, npairs: int, count: int, H: int, W: int, dtype, device, group=None, depth: int = 2):
+        import torch
+        import torch.distributed as dist
+
+        self.torch, self.dist, self.group = torch, dist, group
+        self.npairs, self.depth = npairs, depth
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.start, c = shard_range(npairs, self.rank, self.world)
+        if c != count:
+            raise ValueError(f"rank {self.rank} owns {c} pairs, got count {count}")
+        self.count = count
+        self.cuda = getattr(device, "type", str(device)).startswith("cuda")
+        if self.rank == 0:
+            self.results = [torch.empty((npairs, H, W), dtype=dtype, device=device) for _ in range(depth)]
+            self.blocks = [r[self.start:self.start + count] for r in self.results]
+        else:
+            self.results = [None] * depth
+            self.blocks = [torch.empty((count, H, W), dtype=dtype, device=device) for _ in range(depth)]
+        self.pending = [None] * depth  # CUDA: event on the side stream; CPU: list of works
+        self.stream = torch.cuda.Stream(device) if self.cuda else None
+        self.timing = False
+        self.stalls = []  # CUDA: (start, end) events around each wait on the caller's stream
+        self.spans = []   # CUDA: (start, end) events around each step's transfers on the side stream
+        self.cpu_stall_s = 0.0  # CPU: host time spent completing works
+
+    def buffer(self, k: int):
+        """The block step k computes into (waits for step k - depth's transfers)."""
+        slot = k % self.depth
+        self._wait(slot)
+        return self.blocks[slot]
+
+    def result(self, k: int):
+        """Rank 0: step k's [npairs, H, W] maps (complete after ``wait(k)``)."""
+        return self.results[k % self.depth]
+
+    def launch(self, k: int):
+        """Start step k's transfers after the work already on the caller's stream."""
+        slot = k % self.depth
+        ops = _gather_ops(self.blocks[slot], self.results[slot], self.npairs, self.group)
+        if not ops:  # world 1 (or an empty block): rank 0 computed into its rows already
+            return
+        if self.cuda:
+            torch = self.torch
+            cur = torch.cuda.current_stream()
+            with torch.cuda.stream(self.stream):
+                self.stream.wait_stream(cur)
+                a = None
+                if self.timing:
+                    a = torch.cuda.Event(enable_timing=True)
+                    a.record(self.stream)
+                for w in self.dist.batch_isend_irecv(ops):
+                    w.wait()  # the side stream waits for RCCL's stream (no host wait)
+                ev = torch.cuda.Event(enable_timing=self.timing)
+                ev.record(self.stream)
+                if a is not None:
+                    self.spans.append((a, ev))
+            # the caller's allocator must not reuse the block before the transfer has read it
+            self.blocks[slot].record_stream(self.stream)
+            self.pending[slot] = ev
+        else:
+            self.pending[slot] = self.dist.batch_isend_irecv(ops)
+
+    def wait(self, k: int):
+        """The caller (its stream on CUDA) waits for step k's transfers."""
+        self._wait(k % self.depth)
+
+    def drain(self):
+        for slot in range(self.depth):
+            self._wait(slot)
+
+    def _wait(self, slot: int):
+        p = self.pending[slot]
+        if p is None:
+            return
+        self.pending[slot] = None
+        if self.cuda:
+            torch = self.torch
+            cur = torch.cuda.current_stream()
+            if self.timing:
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record(cur)
+                cur.wait_event(p)
+                b.record(cur)
+                self.stalls.append((a, b))
+            else:
+                cur.wait_event(p)
+        else:
+            import time
+
+            t0 = time.perf_counter()
+            for w in p:
+                w.wait()
+            if self.timing:
+                self.cpu_stall_s += time.perf_counter() - t0
+
+    def exposed_ms(self) -> float:
+        """Summed stall of the caller on gathers since ``reset_stats`` (CUDA: of its
+        stream, read after a device sync; CPU: host time completing the works)."""
+        if self.cuda:
+            return sum(a.elapsed_time(b) for a, b in self.stalls)
+        return self.cpu_stall_s * 1e3
+
+    def transfer_ms(self) -> float:
+        """Summed duration of the transfers on the side stream (CUDA; rank 0: all
+        receives of a step, other ranks: their send) since ``reset_stats``."""
+        return sum(a.elapsed_time(b) for a, b in self.spans)
+
+    def reset_stats(self, timing: bool = True):
+        self.timing = timing
+        self.stalls, self.spans, self.cpu_stall_s = [], [], 0.0
 
 
 def run_sharded(lefts: Sequence, rights: Sequence, compute_fn: Callable, gather: bool = True, group=None):

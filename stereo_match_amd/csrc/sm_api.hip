@@ -59,7 +59,12 @@ struct DevBuf {
 };
 
 struct Norm {
-    int minD, D, maxD, bs, P1, P2, ftzero, uniq, disp12, speckle_ws, speckle_range, cost, mode;
+    // D: disparities the kernels run (a multiple of 16); Dv: the caller's numDisparities.
+    // They differ only for an external cost volume whose plane count is not a multiple of
+    // 16 (mc-cnn: 228, mapTo3D_mc_cnn.py:71): its planes Dv..D-1 carry the pad cost
+    // VOL_CMAX + P2 (k_cost_volume_f32), which no path value of a real disparity ever takes
+    // as its minimum (vol_pad_cost), and the WTA kernels ignore them.
+    int minD, D, Dv, maxD, bs, P1, P2, ftzero, uniq, disp12, speckle_ws, speckle_range, cost, mode;
     int minX1, maxX1, width1, ndirs, dpl;
     int cn;    // input channels (1 gray, 3 BGR)
     bool wide;  // SGBM cost outside the int16-exact range (or BGR): sm_wide.hpp path
@@ -198,11 +203,17 @@ int normalize(sm_ctx* ctx, const sm_params* p, int H, int W, Norm& n, int cn = 1
     if (H <= 0 || W <= 0) return fail(ctx, SM_E_ARG, "empty image (%dx%d)", W, H);
     if (W > 32767) return fail(ctx, SM_E_UNSUPPORTED, "width %d > 32767", W);
     n.minD = p->min_disparity;
-    n.D = p->num_disparities;
-    if (n.D <= 0 || n.D % 16 != 0)
+    n.D = n.Dv = p->num_disparities;
+    if (p->cost_kind == SM_COST_VOLUME) {
+        // an external volume has the planes it was made with (OpenCV's %16 assert belongs
+        // to StereoSGBM's own cost); the kernels run the next multiple of 16
+        if (n.Dv <= 0) return fail(ctx, SM_E_ARG, "cost volume needs at least one disparity plane (got %d)", n.Dv);
+        n.D = (n.Dv + 15) & ~15;
+    } else if (n.D <= 0 || n.D % 16 != 0) {
         return fail(ctx, SM_E_ARG, "numDisparities must be a positive multiple of 16 (got %d)", n.D);
-    if (n.D > 256) return fail(ctx, SM_E_UNSUPPORTED, "numDisparities %d > 256 not built", n.D);
-    n.maxD = n.minD + n.D;
+    }
+    if (n.D > 256) return fail(ctx, SM_E_UNSUPPORTED, "numDisparities %d > 256 not built", n.Dv);
+    n.maxD = n.minD + n.Dv;
     n.bs = p->block_size > 0 ? p->block_size : 5;
     n.ftzero = std::max(p->pre_filter_cap, 15) | 1;
     n.uniq = p->uniqueness_ratio >= 0 ? p->uniqueness_ratio : 10;
@@ -374,6 +385,9 @@ const int kVdx[6] = {1, 0, -1, 1, 0, -1};
 enum { DIRS_ALL = 0, DIRS_EW = 1, DIRS_EW_UP = 2 };
 const int kVdy[6] = {1, 1, 1, -1, -1, -1};
 
+// dynamic LDS a row kernel (k_wta, k_wide_wta, k_lr_rows: one image row's disp2 keys and
+// sub-pixel values) may request: HIP's default per-workgroup limit
+constexpr size_t kRowLds = 65536;
 constexpr size_t kSetBudget = size_t(12) << 30;  // bytes of path volumes per buffer set
 constexpr int kMaxGroup = 16;
 // smallest launch group the fused sweeps run by default: their time per launch is nearly
@@ -415,7 +429,10 @@ struct Geo {  // per-group geometry shared by the launches
     bool hybrid;  // 8 paths: down sweep (u16 partial) beside a per-direction launch of E, W, NE, N, NW
 };
 
-bool row_mode(const sm_ctx* ctx, const Norm& n) { return SM_ABLATIONS && (ctx->dbg_flags & DBG_ROW) && n.D % 64 == 0; }
+bool row_mode(const sm_ctx* ctx, const Norm& n)
+{
+    return SM_ABLATIONS && (ctx->dbg_flags & DBG_ROW) && n.D % 64 == 0 && n.D == n.Dv;
+}
 bool overlap(const sm_ctx* ctx) { return (ctx->dbg_flags & DBG_OVERLAP) != 0; }
 // census mode: the path kernels read a precomputed u8 Hamming cost volume
 // (k_census_cost8) instead of computing popcounts per direction; ablation
@@ -556,6 +573,7 @@ int launch_wta_t(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs)
     wa.W = g.W;
     wa.width1 = n.width1;
     wa.D = n.D;
+    wa.Dv = n.Dv;
     wa.minD = n.minD;
     wa.minX1 = n.minX1;
     wa.uniq = n.uniq;
@@ -565,6 +583,9 @@ int launch_wta_t(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs)
     wa.lane8 = n.ndirs == 5;
     dim3 grid(g.H, g.G);
     const size_t smem = (size_t)g.W * (ctx->wta_dst ? 10 : 8) + 16;
+    if (smem > kRowLds)
+        return fail(ctx, SM_E_UNSUPPORTED, "width %d: the WTA row kernel's %zu B of LDS exceed %zu%s", g.W, smem,
+                    kRowLds, ctx->wta_dst ? " (with the WTA index output)" : "");
     if (ctx->fb_guard) {
         wa.guard = ctx->fb_guard;
         wa.fallbacks = (uint32_t*)ctx->sweep_err.p + ERR_FALLBACKS;
@@ -650,7 +671,8 @@ bool use_sweep(const sm_ctx* ctx, const Norm& n, int H)
     const int cmax = n.cost == SM_COST_CENSUS ? 64 : n.cost == SM_COST_VOLUME ? smk::VOL_CMAX : 0;
     if (cmax + n.P2 > 16383) return false;
     if (H > 65535 || n.width1 <= 0) return false;                      // row index lives in 16 tag bits
-    if ((size_t)n.maxX1 * 6 + 16 > 65536) return false;                 // k_lr_rows keeps a row in LDS
+    const size_t W = (size_t)(n.maxX1 - std::min(n.minD, 0));
+    if (W * 6 + 16 > kRowLds) return false;                              // k_lr_rows keeps a row in LDS
     return (uint64_t)H * n.width1 * n.D * 2 <= smk::kMaxRecords;
 }
 
@@ -809,6 +831,7 @@ int sweep_pass(sm_ctx* ctx, const Norm& n, const Geo& g, const SweepJob& j, int 
         a.W = g.W;
         a.W1 = n.width1;
         a.D = n.D;
+        a.Dv = n.Dv;
         a.minD = n.minD;
         a.minX1 = n.minX1;
         a.P1 = n.P1;
@@ -921,7 +944,7 @@ int run_sweep(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs, hipStream_t 
         if ((rc = sweep_pass(ctx, n, g, j, n.ndirs == 8 ? 2 : 1)) != SM_OK) return rc;
     }
     HIP_TRY(ctx, smk::lr_rows_launch((const uint32_t*)bs.key2.p, (const uint32_t*)bs.pre.p, (int16_t*)bs.raw.p,
-                                     ctx->wta_dst, G, g.H, g.W, n.D, n.minD, n.minX1, n.maxX1, n.disp12, ctx->stream));
+                                     ctx->wta_dst, G, g.H, g.W, n.Dv, n.minD, n.minX1, n.maxX1, n.disp12, ctx->stream));
     return SM_OK;
 }
 
@@ -1180,9 +1203,12 @@ int wide_paths_wta(sm_ctx* ctx, const Geo& g, const Norm& n, BufSet& bs)
     wa.ndirs = n.ndirs;
     wa.disp = (int16_t*)bs.raw.p;
     wa.wta = ctx->wta_dst;
+    const size_t smem = (size_t)g.W * (wa.wta ? 10 : 8) + 16;
+    if (smem > kRowLds)
+        return fail(ctx, SM_E_UNSUPPORTED, "width %d: the WTA row kernel's %zu B of LDS exceed %zu%s", g.W, smem,
+                    kRowLds, wa.wta ? " (with the WTA index output)" : "");
     StageTimer t(ctx, ctx->stream, SM_STAGE_WTA, g.G);
-    hipLaunchKernelGGL((smk::k_wide_wta<DPL, 1024>), dim3(g.H, g.G), dim3(1024), (size_t)g.W * (wa.wta ? 10 : 8) + 16,
-                       ctx->stream, wa);
+    hipLaunchKernelGGL((smk::k_wide_wta<DPL, 1024>), dim3(g.H, g.G), dim3(1024), smem, ctx->stream, wa);
     HIP_TRY(ctx, hipGetLastError());
     return SM_OK;
 }
@@ -1340,6 +1366,8 @@ int run_group(sm_ctx* ctx, const Src& src, const Geo& g, const Norm& n, int16_t*
             va.W = W;
             va.width1 = n.width1;
             va.D = n.D;
+            va.Dv = n.Dv;
+            va.cpad = smk::vol_pad_cost(n.P2);
             va.minX1 = n.minX1;
             va.offset = src.offset;
             va.scale = src.scale;
@@ -1665,6 +1693,11 @@ int run_wls(sm_ctx* ctx, const int16_t* dl, const int16_t* dr, size_t disp_pair,
     if (prepared && G < npairs) return fail(ctx, SM_E_ARG, "internal: prepared WLS batch exceeds one chunk");
     StageTimer t(ctx, ctx->stream, SM_STAGE_WLS, npairs);
     const bool pivots = n.num_iter <= kWlsMaxPivotIters;
+    // the smoother's timing ablations live in k_fgs (num_iter > kWlsMaxPivotIters); the pivot
+    // path's k_fgs_solve has no such switches, so an ablation run must not silently measure it
+    if (pivots && (ctx->dbg_flags & (DBG_FGS_NO_SWEEP | DBG_FGS_NO_MEM)))
+        return fail(ctx, SM_E_UNSUPPORTED, "WLS timing ablations need num_iter > %d (the k_fgs path)",
+                    kWlsMaxPivotIters);
     for (int p0 = 0; p0 < npairs; p0 += G) {
         const int g = std::min(G, npairs - p0);
         if (roi) {
@@ -1931,6 +1964,8 @@ int ensure_wls_stream(sm_ctx* ctx)
 extern "C" {
 
 const char* sm_version(void) { return SM_VERSION; }
+
+int sm_abi_version(void) { return SM_ABI_VERSION; }
 
 int sm_create(int device, sm_ctx** out)
 {
@@ -2248,6 +2283,8 @@ int sm_compute_disparity_batch_device(sm_ctx* ctx, const uint8_t* dL, const uint
                                       int16_t* d_filtered)
 {
     if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
+    if (npairs < 0) return fail(ctx, SM_E_ARG, "npairs < 0");
+    if (npairs == 0) return SM_OK;  // before wls_geo / wls_prepare size any launch from it
     if (!left || !wls) return fail(ctx, SM_E_ARG, "NULL params");
     if (!d_displ || !d_dispr || !d_filtered) return fail(ctx, SM_E_ARG, "NULL output pointer");
     sm_params lm = *left, rm;
@@ -2291,11 +2328,13 @@ int sm_compute_disparity_batch_device(sm_ctx* ctx, const uint8_t* dL, const uint
     // D = 160, one pair: matchers 1.32 ms concurrent, 1.22 ms in sequence; per matcher the
     // per-direction path kernel took 665 vs 332 us)
     const bool serial = (ctx->dbg_flags & DBG_CONCURRENT_LR) == 0;
-    const hipStream_t tw_stream = tw->stream;
-    if (serial) tw->stream = ctx->stream;
-    HIP_TRY(ctx, hipStreamWaitEvent(tw->stream, ctx->ev_lr_fork, 0));
-    rc = sm_compute_batch_device(tw, dR, dL, npairs, pair_stride, H, W, stride, &rm, d_dispr);
-    tw->stream = tw_stream;
+    {
+        // serial: the twin enqueues on the caller's stream for this call only (restored on
+        // every exit path, so the twin never keeps a stream it does not own)
+        StreamSwap sw(tw, serial ? ctx->stream : tw->stream);
+        HIP_TRY(ctx, hipStreamWaitEvent(tw->stream, ctx->ev_lr_fork, 0));
+        rc = sm_compute_batch_device(tw, dR, dL, npairs, pair_stride, H, W, stride, &rm, d_dispr);
+    }
     if (rc != SM_OK) return fail(ctx, rc, "right matcher: %s", tw->err.c_str());
     HIP_TRY(ctx, hipEventRecord(ctx->ev_lr_join, serial ? ctx->stream : tw->stream));
     rc = sm_compute_batch_device(ctx, dL, dR, npairs, pair_stride, H, W, stride, &lm, d_displ);

@@ -669,6 +669,18 @@ __global__ void __launch_bounds__(256) k_sgbm_cost_tail(uint16_t* C, size_t C_pa
 // FMA, so the two IEEE roundings match the oracle's.
 constexpr int VOL_CMAX = 4095;
 
+// Cost of the pad planes Dv..D-1 of a volume whose plane count Dv is not a multiple of 16
+// (the kernels run D = the next multiple).  With C_pad >= VOL_CMAX + P2 no real disparity's
+// path value ever takes a pad value as its minimum:
+//  * every path keeps min over the real d of L <= VOL_CMAX (at the predecessor's argmin d0,
+//    min(Lp[d0], ...) - minLp = 0, so L[d0] = C[d0]; the first step has Lp = 0);
+//  * every pad value L >= C_pad (min(...) - minLp >= 0), so minLp over all D planes is the
+//    minimum over the real ones, and at d = Dv-1 the term Lp[Dv] + P1 > minLp + P2 never
+//    undercuts the min(...) of the unpadded recurrence (its edge Lp[Dv] = MAX).
+// Pad values stay <= C_pad + P2 <= 28671 (normalize: P2 <= 12288), so no u16 path arithmetic
+// wraps on them; the WTA kernels give the pad planes S = 0xFFFF (never the minimum, never
+// "far") and take the sub-pixel step only for 0 < best < Dv - 1.
+__host__ __device__ constexpr int vol_pad_cost(int P2) { return VOL_CMAX + P2; }
 
 struct VolArgs {
     const float* vol;
@@ -676,6 +688,8 @@ struct VolArgs {
     uint16_t* C;
     size_t C_pair;  // elements between pairs
     int H, W, width1, D, minX1;
+    int Dv;    // planes of the input volume (<= D); planes Dv..D-1 of C get cpad
+    int cpad;  // vol_pad_cost(P2)
     int nt;  // 1: nontemporal stores (the launch group's volume exceeds the Infinity Cache)
     float offset, scale;
     uint32_t* zero_word;  // see CensusArgs
@@ -705,32 +719,45 @@ __global__ void __launch_bounds__(256) k_cost_volume_f32(VolArgs a)
     const float* v = a.vol + pair * a.vol_pair + (size_t)y * a.W + a.minX1 + x0;
     for (int i = threadIdx.x; i < 64 * half; i += 256) {
         const int xl = (i & 63) * PL, dp = i >> 6;
+        // planes 2dp, 2dp + 1 inside the input volume (wave-uniform); the pad planes are
+        // never read and get the pad cost (vol_pad_cost)
+        const bool in0 = 2 * dp < a.Dv, in1 = 2 * dp + 1 < a.Dv;
         const float* p0 = v + (size_t)(2 * dp) * plane + xl;
         const float* p1 = p0 + plane;
         float c0[PL], c1[PL];
+#pragma unroll
+        for (int k = 0; k < PL; k++) c0[k] = c1[k] = 0.f;
         if (xl + PL <= nx) {
             if constexpr (PL == 2) {
                 typedef float f2v __attribute__((ext_vector_type(2)));
-                const f2v a0 = __builtin_nontemporal_load(reinterpret_cast<const f2v*>(p0));
-                const f2v a1 = __builtin_nontemporal_load(reinterpret_cast<const f2v*>(p1));
-                c0[0] = a0[0]; c0[1] = a0[1]; c1[0] = a1[0]; c1[1] = a1[1];
+                if (in0) {
+                    const f2v a0 = __builtin_nontemporal_load(reinterpret_cast<const f2v*>(p0));
+                    c0[0] = a0[0]; c0[1] = a0[1];
+                }
+                if (in1) {
+                    const f2v a1 = __builtin_nontemporal_load(reinterpret_cast<const f2v*>(p1));
+                    c1[0] = a1[0]; c1[1] = a1[1];
+                }
             } else {
 #pragma unroll
                 for (int k = 0; k < PL; k++) {
-                    c0[k] = __builtin_nontemporal_load(p0 + k);
-                    c1[k] = __builtin_nontemporal_load(p1 + k);
+                    if (in0) c0[k] = __builtin_nontemporal_load(p0 + k);
+                    if (in1) c1[k] = __builtin_nontemporal_load(p1 + k);
                 }
             }
         } else {
 #pragma unroll
             for (int k = 0; k < PL; k++) {
-                c0[k] = xl + k < nx ? p0[k] : 0.f;
-                c1[k] = xl + k < nx ? p1[k] : 0.f;
+                c0[k] = in0 && xl + k < nx ? p0[k] : 0.f;
+                c1[k] = in1 && xl + k < nx ? p1[k] : 0.f;
             }
         }
 #pragma unroll
-        for (int k = 0; k < PL; k++)
-            tile[(xl + k) * rowdw + dp] = quant_cost(c0[k], a.offset, a.scale) | (quant_cost(c1[k], a.offset, a.scale) << 16);
+        for (int k = 0; k < PL; k++) {
+            const uint32_t q0 = in0 ? quant_cost(c0[k], a.offset, a.scale) : (uint32_t)a.cpad;
+            const uint32_t q1 = in1 ? quant_cost(c1[k], a.offset, a.scale) : (uint32_t)a.cpad;
+            tile[(xl + k) * rowdw + dp] = q0 | (q1 << 16);
+        }
     }
     __syncthreads();
     uint32_t* out = reinterpret_cast<uint32_t*>(a.C + pair * a.C_pair + ((size_t)y * a.width1 + x0) * a.D);

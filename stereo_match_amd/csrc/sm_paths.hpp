@@ -498,6 +498,7 @@ struct WtaArgs {
     size_t slot_bytes, L_pair_bytes;
     int nslots;
     int H, W, width1, D, minD, minX1, uniq, disp12;
+    int Dv;         // real disparities (< D only for a padded cost volume: planes >= Dv are ignored)
     int16_t* disp;  // [pair][H][W] pre-median
     int16_t* wta;   // [pair][H][W] integer WTA index (best, -1 rejected / outside the domain), or null
     const uint16_t* part;  // hybrid engine: u16 S + SE + SW sums [pair][H][width1][D], or null
@@ -594,6 +595,7 @@ __device__ __forceinline__ void wta_row(const WtaArgs& a, const int y, const int
 #pragma unroll
         for (int i = 0; i < DPL; i++) {
             S[i] = min(S[i], 32767u);
+            if (g * DPL + i >= a.Dv) S[i] = 0xFFFFu;  // pad planes of a cost volume: never the minimum
             key = min(key, (S[i] << 16) | wta_rank(g * DPL + i, a.lane8));
         }
         key = row16_min(key);
@@ -603,7 +605,7 @@ __device__ __forceinline__ void wta_row(const WtaArgs& a, const int y, const int
         for (int i = 0; i < DPL; i++) {
             const int d = g * DPL + i;
             const int dd = best - d;
-            bad |= ((int)S[i] * (100 - u) < minS * 100 && (dd > 1 || dd < -1)) ? 1u : 0u;
+            bad |= ((int)S[i] * (100 - u) < minS * 100 && (dd > 1 || dd < -1) && d < a.Dv) ? 1u : 0u;
             nb |= d == best - 1 ? S[i] : 0u;
             nb |= d == best + 1 ? (S[i] << 16) : 0u;
         }
@@ -614,7 +616,7 @@ __device__ __forceinline__ void wta_row(const WtaArgs& a, const int y, const int
             const int x2 = X - best - minD;
             atomicMin(&key2[x2], ((uint32_t)minS << 16) | (uint32_t)(0xFFFF - X));
             int d16;
-            if (best > 0 && best < D - 1) {
+            if (best > 0 && best < a.Dv - 1) {
                 const int Sm = (int)(nb & 0xFFFF), Sq = (int)(nb >> 16);
                 const int den = max(Sm + Sq - 2 * minS, 1);
                 d16 = best * 16 + ((Sm - Sq) * 16 + den) / (den * 2);  // C truncation

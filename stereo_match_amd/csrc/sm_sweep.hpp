@@ -329,7 +329,6 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
     // sgbm8 124.0 -> 120.8, census8 WTA sweep level (96.6 / 96.0); the 5-path WTA sweep is
     // slower with it (95.3 -> 97.9) and keeps the row barriers
     constexpr bool ROWSYNC = SWEEP_ROW_SYNC && MODE != 1;
-    constexpr bool PKMIN = DPL % 2 == 0 && !SWEEP_U32;  // packed loop: lmin words hold m | m << 16
     constexpr int LPW = G::LPW, NCW = G::NCW, HB = G::HB, NCOL = G::NCOL, COLS = G::COLS, CW = G::CW, D = G::D;
     constexpr int NG = G::NG, SNG = G::SNG, PF = G::PF, HM = G::HM, HW = G::HW;
     constexpr int CB = DPL * (int)sizeof(CT);  // cost / E / W bytes per lane and cell
@@ -713,6 +712,10 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
                         } else {
                             uint32_t Sp[NP];
                             uint32_t key = 0xFFFFFFFFu;
+                            // a padded cost volume (u16 costs only): its pad planes d >= Dv take
+                            // S = 0xFFFF, above every real S <= 32767 (never the minimum, never
+                            // below the uniqueness threshold)
+                            const bool pad = SAT && a.Dv < D;  // wave-uniform
 #pragma unroll
                             for (int i = 0; i < NP; i++) {
                                 uint32_t t;
@@ -721,6 +724,10 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
                                     if constexpr (MODE == 2) ew = pk_adds(ew, Pin[i]);
                                     t = pk_adds(pk_adds(nV[i], nA[0][i]), pk_adds(nB[0][i], ew));
                                     t = pk_min(t, 0x7FFF7FFFu);  // min(sum, 32767)
+                                    if (pad) {
+                                        const int d0 = g * DPL + 2 * i;
+                                        t |= (d0 >= a.Dv ? 0x0000FFFFu : 0u) | (d0 + 1 >= a.Dv ? 0xFFFF0000u : 0u);
+                                    }
                                 } else {
                                     uint32_t ew = pk_add(Ein[i], Win[i]);
                                     if constexpr (MODE == 2) ew = pk_add(ew, Pin[i]);
@@ -753,7 +760,9 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
                                 m2p = pk_min(m2p, pk_adds(Sp[i], mask));
                             }
                             const uint32_t m2 = group_min<VL>(min(m2p & 0xFFFFu, m2p >> 16));
-                            const bool ok = !(__mul24((int)m2, ku) < __mul24((int)minS, 100)) && minS < 32767u;
+                            // (m2 = 0xFFFF: no real far entry, only pad planes of a volume with Dv <= 3)
+                            const bool ok = !(__mul24((int)m2, ku) < __mul24((int)minS, 100) && (!pad || m2 <= 32767u)) &&
+                                            minS < 32767u;
                             const uint32_t recw = ok ? ((minS << 16) | (uint32_t)best) : 0xFFFFFFFFu;
                             const uint32_t nbw = Sm | (Sq << 16);
                             const bool wpx = g == 0 && active && live;
@@ -878,11 +887,13 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
                 } else {
                     uint32_t S[DPL];
                     uint32_t key = 0xFFFFFFFFu;
+                    const bool pad = sizeof(CT) == 2 && a.Dv < D;  // padded cost volume (wave-uniform)
 #pragma unroll
                     for (int i = 0; i < DPL; i++) {
                         uint32_t t = nV[i] + nA[i] + nB[i] + Ein[i] + Win[i];
                         if constexpr (MODE == 2) t += Pin[i];
                         if constexpr (sizeof(CT) == 2) t = min(t, 32767u);  // census sums stay below 2^11
+                        if (pad && g * DPL + i >= a.Dv) t = 0xFFFFu;  // pad plane: never the minimum
                         S[i] = t;
                         key = min(key, (t << 16) | wta_rank(g * DPL + i, MODE == 1));
                     }
@@ -896,12 +907,15 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
                     if (ku > 0) {  // S, minS < 2^15, ku <= 100: 24-bit multiplies are exact (full rate)
                         const uint32_t lim = __umul24(minS, 100u);
 #pragma unroll
+                        // (S <= 32767: not a pad plane; real sums never exceed it)
                         for (int i = 0; i < DPL; i++)
-                            far = max(far, __umul24(S[i], (uint32_t)ku) < lim ? (uint32_t)(gb + i) : 0u);
+                            far = max(far, __umul24(S[i], (uint32_t)ku) < lim && (sizeof(CT) == 1 || S[i] <= 32767u)
+                                               ? (uint32_t)(gb + i) : 0u);
                     } else {  // uniquenessRatio >= 100: the product form (rare)
 #pragma unroll
                         for (int i = 0; i < DPL; i++)
-                            far = max(far, (int)S[i] * ku < (int)minS * 100 ? (uint32_t)(gb + i) : 0u);
+                            far = max(far, (int)S[i] * ku < (int)minS * 100 && (sizeof(CT) == 1 || S[i] <= 32767u)
+                                               ? (uint32_t)(gb + i) : 0u);
                     }
                     far = group_max<VL>(far);
                     const bool ok = far <= 2u && minS < 32767u;

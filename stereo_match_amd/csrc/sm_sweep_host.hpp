@@ -25,6 +25,7 @@ struct SweepArgs {
     uint32_t* nb;    // [pair][H][W] S[best-1] | S[best+1] << 16 (sub-pixel inputs)
     uint32_t* err;   // bit 0: a halo poll timed out
     int H, W, W1, D, minD, minX1, P1, P2, uniq;
+    int Dv;        // real disparities (< D only for a padded cost volume: the WTA ignores d >= Dv)
     float inv_ku;  // 1 / (100 - uniq) (uniqueness threshold estimate; exact fix-up on the device)
     int nwg;
     uint32_t epoch;  // 1..65535, distinct from the previous launches on the same hop buffer

@@ -70,6 +70,14 @@ def volume_cases():
     yield "vol_absdiff_d32_p5", v32, dict(synthetic.cost_volume_params(32), mode=5), 0.0, synthetic.VOLUME_SCALE
     yield "vol_signed_nan_d16", vr, dict(synthetic.cost_volume_params(16), P1=3, P2=40), 1.0, 1.0
     yield "vol_minD_neg3_d16", v16, dict(synthetic.cost_volume_params(16), minDisparity=-3), 0.0, 1000.0
+    # plane counts that are not a multiple of 16 (the reference's own mc-cnn volume has 228,
+    # mapTo3D_mc_cnn.py:71): an external volume keeps the planes it was made with
+    l20, r20, _ = synthetic.random_dot_pair(32, 84, 20, seed=14)
+    l37, r37, _ = synthetic.random_dot_pair(30, 96, 37, seed=15)
+    yield "vol_absdiff_d20_p8", synthetic.absdiff_volume(l20, r20, 20)[0], dict(synthetic.cost_volume_params(20)), \
+        0.0, synthetic.VOLUME_SCALE
+    yield "vol_absdiff_d37_p5_minD2", synthetic.absdiff_volume(l37, r37, 37, minD=2)[0], \
+        dict(synthetic.cost_volume_params(37), mode=5, minDisparity=2), 0.0, synthetic.VOLUME_SCALE
 
 
 def wls_cases():

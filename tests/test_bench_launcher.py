@@ -48,8 +48,22 @@ def test_selftest_runs_mains_rank_path_three_ranks():
     assert r.returncode == 0, r.stderr[-3000:]
     d = _json_line(r.stdout)
     assert d["distributed"]["world_size"] == 3
-    assert d["distributed"]["gather_bytes_to_root"] == 6 * 288 * 384 * 2
+    # ranks 1, 2 send their blocks; rank 0 computed into its rows of the result
+    assert d["distributed"]["gather_bytes_to_root"] == 4 * 288 * 384 * 2
     assert d["distributed"]["gathered_in_pair_order"] is True
+    assert d["distributed"]["gather_exposed_ms_per_step"] >= 0
+
+
+def test_selftest_four_ranks_overlapped_gather():
+    # BASELINE config 4's shape at 4 ranks: double-buffered gather beside the next step
+    r = _run(["--gpus", "4", "--selftest-cpu", "--steps", "3", "--warmup", "2", "--config", "tsukuba",
+              "--pairs-per-gpu", "2"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_line(r.stdout)
+    dd = d["distributed"]
+    assert dd["world_size"] == 4 and dd["gathered_in_pair_order"] is True
+    assert dd["gather_bytes_to_root"] == 6 * 288 * 384 * 2
+    assert "double-buffered" in dd["gather"]
 
 
 def test_dist_flag_one_rank():
@@ -59,7 +73,7 @@ def test_dist_flag_one_rank():
     d = _json_line(r.stdout)
     assert d["n_gpus"] == 1
     assert d["distributed"]["backend"] == "gloo" and d["distributed"]["world_size"] == 1
-    assert d["distributed"]["gather_bytes_to_root"] == 8 * 288 * 384 * 2
+    assert d["distributed"]["gather_bytes_to_root"] == 0  # rank 0 computes into the result itself
     assert d["distributed"]["gathered_in_pair_order"] is True
 
 

@@ -112,3 +112,85 @@ def test_gloo_sharded_matches_single_process(world, n):
     for i in range(n):
         a, b, _ = synthetic.random_dot_pair(20, 70, 16, seed=200 + i)
         assert np.array_equal(got[i], ref_c.compute(a, b, p)), i
+
+
+def _overlap_worker(rank, world, port, n, steps, q):
+    """OverlappedGather over gloo: step k writes pair i's block as (k, i)-coded maps; every
+    step's result on rank 0 must hold all pairs in order, although step k+1 computes while
+    step k's transfers are in flight."""
+    from stereo_match_amd.batch import OverlappedGather
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        start, count = shard_range(n, rank, world)
+        og = OverlappedGather(n, count, 3, 4, torch.int16, torch.device("cpu"))
+        og.reset_stats(timing=True)
+        ok = []
+        for k in range(steps):
+            buf = og.buffer(k)
+            assert buf.shape == (count, 3, 4)
+            for j in range(count):
+                buf[j].fill_(100 * k + start + j)
+            og.launch(k)
+            if rank == 0 and k >= 1:  # the previous step's maps, completed after wait(k - 1)
+                og.wait(k - 1)
+                got = og.result(k - 1)
+                ok.append(all(bool((got[i] == 100 * (k - 1) + i).all()) for i in range(n)))
+        og.drain()
+        if rank == 0:
+            got = og.result(steps - 1)
+            ok.append(all(bool((got[i] == 100 * (steps - 1) + i).all()) for i in range(n)))
+            # rank 0's own block is a view of its rows (nothing copied)
+            assert og.buffer(steps).data_ptr() == og.result(steps)[start:].data_ptr()
+            q.put((ok, og.exposed_ms()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n", [(2, 4), (4, 8), (4, 6), (3, 2)])
+def test_gloo_overlapped_gather_pair_order(world, n):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_overlap_worker, args=(r, world, port, n, 5, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    ok, exposed = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert ok and all(ok), ok
+    assert exposed >= 0
+
+
+def _root_out_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n = 5
+        s, c = shard_range(n, rank, world)
+        local = torch.stack([torch.full((2, 3), i, dtype=torch.int16) for i in range(s, s + c)])
+        out = torch.full((n, 2, 3), -1, dtype=torch.int16) if rank == 0 else None
+        res = gather_to_root(local, n, out=out)
+        if rank == 0:
+            q.put((res.data_ptr() == out.data_ptr(), res.tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gather_to_root_fills_preallocated_out():
+    # uneven blocks (3 + 2 pairs) land in the caller's tensor, no padding, no concatenation
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_root_out_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    same, got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert same
+    assert got == [[[i] * 3] * 2 for i in range(5)]

@@ -380,6 +380,68 @@ def test_volume_full_size_mccnn(eng, mode, flags):
     assert np.mean(np.abs(((out.astype(np.int64) + 8) >> 4) - gt)[valid] <= 1) > 0.97
 
 
+_DVCASES = [dict(H=int(_rng.integers(1, 60)), W=int(_rng.integers(8, 260)), D=int(d),
+                 minD=int(_rng.integers(-6, 6)), mode=int(_rng.choice([5, 8])), seed=int(_rng.integers(0, 1 << 30)))
+            for d in (1, 2, 3, 5, 17, 20, 37, 100, 127, 150, 228, 255)]
+
+
+@pytest.mark.parametrize("flags", [0, 4096, 16384])
+@pytest.mark.parametrize("c", _DVCASES, ids=lambda c: "H{H}W{W}D{D}m{minD}p{mode}".format(**c))
+def test_volume_any_plane_count_vs_c_oracle(eng, c, flags):
+    """An external volume keeps the planes it was made with (mc-cnn: 228,
+    mapTo3D_mc_cnn.py:71): D not a multiple of 16 runs on padded kernels whose
+    pad planes never win (sm_cost.hpp vol_pad_cost), on every engine (flags: 0
+    default, 4096 per-direction, 16384 fused sweeps)."""
+    rng = np.random.default_rng(c["seed"])
+    vol = rng.random((c["D"], c["H"], c["W"]), dtype=np.float32)
+    vol[rng.random(vol.shape) < 0.02] = np.nan
+    p = dict(synthetic.cost_volume_params(c["D"]), minDisparity=c["minD"], mode=c["mode"])
+    eng.set_debug_flags(flags)
+    try:
+        out = eng.aggregate_cost_f32(vol, synthetic.to_sm_params(p), 0.0, synthetic.VOLUME_SCALE)
+    finally:
+        eng.set_debug_flags(0)
+    assert np.array_equal(out, ref_c.compute_volume(vol, p, 0.0, synthetic.VOLUME_SCALE))
+
+
+@pytest.mark.parametrize("uniq", [0, 15, 60, 99])
+def test_volume_d3_uniqueness_no_far_planes(eng, uniq):
+    """D <= 3: no disparity is 'far' from the winner, so the uniqueness test can never reject;
+    the pad planes must not act as far entries either (any uniquenessRatio)."""
+    rng = np.random.default_rng(uniq)
+    vol = rng.random((3, 20, 50), dtype=np.float32)
+    p = dict(synthetic.cost_volume_params(3), uniquenessRatio=uniq, mode=8)
+    out = eng.aggregate_cost_f32(vol, synthetic.to_sm_params(p), 0.0, synthetic.VOLUME_SCALE)
+    assert np.array_equal(out, ref_c.compute_volume(vol, p, 0.0, synthetic.VOLUME_SCALE))
+
+
+def test_volume_reference_mccnn_memmap_as_documented(tmp_path):
+    """The reference's own mc-cnn volume shape, (1, 228, 1280, 720) float32 memmapped at
+    mapTo3D_mc_cnn.py:71 (made with -disp_max 228, mc_cnn/script.py:9-10), through the
+    call INTEGRATION.md §2 shows, bit-exact against the C oracle (synthetic content: the
+    reference ships no volume)."""
+    import stereo_match_amd as sma
+
+    D, H, W = 228, 1280, 720
+    left, right, gt = synthetic.random_dot_pair(H, W, D, seed=228)
+    path = tmp_path / "left.bin"
+    mm = np.memmap(path, dtype=np.float32, mode="w+", shape=(1, D, H, W))
+    mm[:] = synthetic.absdiff_volume(left, right, D)
+    mm.flush()
+    del mm
+    # INTEGRATION.md §2, as written
+    vm = sma.StereoSGBM_create(numDisparities=228, P1=200, P2=2000, disp12MaxDiff=1, uniquenessRatio=15,
+                               mode=sma.STEREO_SGBM_MODE_HH)
+    disp = vm.computeFromCost(np.memmap(path, np.float32, mode="r", shape=(1, 228, 1280, 720)),
+                              offset=0.0, scale=4000.0)
+    vol = np.memmap(path, np.float32, mode="r", shape=(1, D, H, W))[0]
+    p = dict(synthetic.cost_volume_params(D), P1=200, P2=2000, mode=8)
+    assert np.array_equal(disp, ref_c.compute_volume(np.asarray(vol), p, 0.0, 4000.0))
+    valid = disp >= 0
+    assert valid.mean() > 0.6
+    assert np.mean(np.abs(((disp.astype(np.int64) + 8) >> 4) - gt)[valid] <= 1) > 0.95
+
+
 def test_volume_torch_batch_and_matcher():
     import torch
 

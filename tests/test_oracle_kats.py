@@ -265,6 +265,31 @@ def test_volume_numpy_c_bit_exact(H, W, Dk, minD, mode, scale, nan_frac, seed):
     assert np.array_equal(sgm_np.compute_volume(vol, p, 0.25, scale), ref_c.compute_volume(vol, p, 0.25, scale))
 
 
+@settings(max_examples=20, deadline=None)
+@given(H=st.integers(1, 16), W=st.integers(4, 70), D=st.integers(1, 45), minD=st.integers(-4, 4),
+       mode=st.sampled_from([5, 8]), uniq=st.sampled_from([0, 15, 70]), seed=st.integers(0, 2**31 - 1))
+def test_volume_any_plane_count_numpy_c_bit_exact(H, W, D, minD, mode, uniq, seed):
+    """External volumes with any plane count (mc-cnn's 228, mapTo3D_mc_cnn.py:71): both
+    restatements take D as given (OpenCV's %16 assert is StereoSGBM's own-cost rule)."""
+    rng = np.random.default_rng(seed)
+    vol = rng.random((D, H, W), dtype=np.float32)
+    p = dict(synthetic.cost_volume_params(D), minDisparity=minD, mode=mode, uniquenessRatio=uniq)
+    assert np.array_equal(sgm_np.compute_volume(vol, p, 0.0, 4000.0), ref_c.compute_volume(vol, p, 0.0, 4000.0))
+
+
+def test_volume_reference_plane_count_kat():
+    """KAT: 228 planes (the reference's mc-cnn volume), 0 at d = 227 (the last plane, where
+    no sub-pixel step applies) and 1 elsewhere -> raw WTA 227·16 on the domain."""
+    H, W, D = 6, 240, 228
+    vol = np.ones((D, H, W), np.float32)
+    vol[D - 1] = 0
+    p = dict(synthetic.cost_volume_params(D))
+    out, st = sgm_np.compute_volume(vol, p, 0.0, 1000.0, return_stages=True)
+    assert np.all(st["raw"][:, D:] == (D - 1) * 16)
+    assert np.all(st["raw"][:, :D] == -16)
+    assert np.array_equal(out, ref_c.compute_volume(vol, p, 0.0, 1000.0))
+
+
 def test_volume_rejects_bad_shapes():
     with pytest.raises(ValueError):
         sgm_np.compute_volume(np.zeros((16, 4, 40), np.float32), dict(numDisparities=32))
