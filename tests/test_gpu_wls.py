@@ -273,3 +273,28 @@ def test_compute_disparity_on_caller_stream():
             assert np.array_equal(a, b)
     finally:
         eng.close()
+
+
+@pytest.mark.gpu
+def test_compute_disparity_batch_device_npairs_guard():
+    """npairs < 0 -> SM_E_ARG before any launch is sized from it; npairs == 0 is a no-op
+    that leaves the outputs untouched (the WLS preparation used to launch first)."""
+    import torch
+
+    H, W, D = 40, 120, 16
+    sp = synthetic.to_sm_params(synthetic.parity_params(D))
+    wp = _lib.wls_default_params(sp)
+    L = torch.zeros((1, H, W), dtype=torch.uint8, device="cuda")
+    outs = [torch.full((1, H, W), 7, dtype=torch.int16, device="cuda") for _ in range(3)]
+    eng = _lib.engine(0)
+    eng.set_stream(torch.cuda.current_stream().cuda_stream)
+    try:
+        with pytest.raises(ValueError):
+            eng.compute_disparity_batch_device(L.data_ptr(), L.data_ptr(), -1, H * W, H, W, W, sp, wp,
+                                               *(o.data_ptr() for o in outs))
+        eng.compute_disparity_batch_device(L.data_ptr(), L.data_ptr(), 0, H * W, H, W, W, sp, wp,
+                                           *(o.data_ptr() for o in outs))
+        eng.synchronize()
+        assert all(bool((o == 7).all()) for o in outs)
+    finally:
+        eng.set_stream(None)

@@ -95,3 +95,24 @@ def test_wta_index_no_domain(eng):
     disp, wta = eng.compute_wta(left, right, synthetic.to_sm_params(p))
     assert (wta == -1).all()
     assert (disp == -16).all()
+
+
+def test_wta_index_row_lds_limit(eng):
+    """The WTA row kernels keep a row's keys, sub-pixel values and (with the index output)
+    the index in LDS: W * 10 + 16 bytes.  Past 64 KB (W > 6551) the call reports
+    SM_E_UNSUPPORTED with a message, instead of failing at launch."""
+    H, W, D = 2, 6600, 16
+    left, right, _ = synthetic.random_dot_pair(H, W, D, seed=4)
+    p = synthetic.to_sm_params(synthetic.parity_params(D))
+    eng.set_debug_flags(PERDIR)
+    try:
+        with pytest.raises(_lib.SmError, match="LDS"):
+            eng.compute_wta(left, right, p)
+        disp = eng.compute(left, right, p)  # without the index: W * 8 + 16 bytes still fit
+    finally:
+        eng.set_debug_flags(0)
+    assert np.array_equal(disp, ref_c.compute(left, right, synthetic.parity_params(D)))
+
+
+def test_abi_version():
+    assert _lib.load().sm_abi_version() == _lib.ABI_VERSION == 3
