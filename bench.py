@@ -296,7 +296,27 @@ class GpuWorkload:
         self.P_dirs = 5 if args.mode in ("sgbm5", "disparity5") else 8
         self.kern, cands = design_kernels(args, self.profile, self.H, self.W, self.D, self.p, self.P_dirs, self.sweep,
                                           self.bm)
-        self.dom = max(cands, key=lambda k: self.profile[k][0])  # the stage with the largest device time
+        self.cands = cands
+        # the dominant kernel is fixed per engine (the stage that moves the most bytes by design:
+        # the WTA sweep, the per-direction path kernel), not picked by a timing race between
+        # stages a few percent apart; every stage's own fraction is reported beside it
+        self.dom = max(cands, key=lambda k: (self.kern[k][1], -cands.index(k)))
+
+    def stage_fracs(self):
+        """Every aggregation / WTA stage's own roofline fraction from the warmup profile (all
+        stages timed there): SURVEY §8(d) bytes the stage owns per launch / its launch time."""
+        out = {}
+        for k in self.cands:
+            ms, launches, pairs = self.profile[k]
+            if launches <= 0:
+                continue
+            launch_s = ms / 1e3 / launches
+            ppl = pairs / launches
+            alg = model_stage_bytes(k, self.args.mode, self.H, self.W, self.D, self.P_dirs, self.sweep) * ppl
+            out[k] = {"kernel": self.kern[k][0], "avg_launch_us": launch_s * 1e6, "alg_bytes_per_launch": alg,
+                      "frac": alg / launch_s / 1e9 / HBM_PEAK_GBS if launch_s > 0 else None,
+                      "design_bytes_per_launch": self.kern[k][1] * ppl, "source": "warmup profile"}
+        return out
 
     def timed_begin(self):
         # timed region: only the dominant kernel's stage records events (every timed stage
@@ -359,6 +379,9 @@ class GpuWorkload:
                 "valu": valu,
                 "pairs_per_launch": pairs_per_launch,
                 "avg_launch_us": launch_s * 1e6,
+                "dominant_rule": "fixed per engine: the stage with the most design bytes (fused sweeps: the WTA "
+                                 "sweep; per-direction: the path kernel)",
+                "stages": self.stage_fracs(),
             },
             "pipeline_roofline": {
                 "model": "SURVEY §8d " + ("H·W·D·(4P+8)" if self.volume else "H·W·(2+4+2+4) (no volume)" if self.bm

@@ -324,6 +324,14 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
 #ifndef SWEEP_PRIO
 #define SWEEP_PRIO 2
 #endif
+    // SWEEP_DYNPRIO (packed row loops): the row hand-off chain (wait for the neighbours' row,
+    // diagonal steps, LDS writes, publish) runs at issue priority PRIO_HI, an own wave's work
+    // that no other wave waits for (V-independent partial sums / WTA) at PRIO_LO, so the SIMD
+    // issues the chain first and fills the gaps with the rest (halo waves: chain only)
+#ifndef SWEEP_DYNPRIO
+#define SWEEP_DYNPRIO 1
+#endif
+    constexpr int PRIO_HI = 3, PRIO_LO = MODE == 0 ? 2 : 1;  // mode 0 stays above the E/W kernel
     if constexpr (MODE == 0 && SWEEP_PRIO > 0) __builtin_amdgcn_s_setprio(SWEEP_PRIO);
     // neighbour-counter row sync: KITTI 8 pairs, down sweep census8 96.4 -> 92.0 us per pair,
     // sgbm8 124.0 -> 120.8, census8 WTA sweep level (96.6 / 96.0); the 5-path WTA sweep is
@@ -599,11 +607,13 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
             uint32_t dpk[NP];
 #pragma unroll
             for (int i = 0; i < NP; i++) dpk[i] = (uint32_t)(g * DPL + 2 * i + 1) * 0x10001u + 0x10000u;
+            if constexpr (SWEEP_DYNPRIO && !OWN) __builtin_amdgcn_s_setprio(PRIO_HI);
             for (int b = 0; b < nblk; b++) {
 #pragma unroll
                 for (int j = 0; j < HB; j++) {
                     const int k = j % PF;
                     const int s = b * HB + j;
+                    if constexpr (SWEEP_DYNPRIO && OWN) __builtin_amdgcn_s_setprio(PRIO_HI);
                     const bool live = s < H;
                     const int y = UP ? H - 1 - s : s;
                     const int rb = (s + 1) & 1, wb = s & 1;
@@ -699,6 +709,7 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
                     } else {
                         publish_row(s);
                     }
+                    if constexpr (SWEEP_DYNPRIO && OWN) __builtin_amdgcn_s_setprio(PRIO_LO);
                     if constexpr (OWN) {
 #pragma unroll
                         for (int i = 0; i < NP; i++) LVp[i] = nV[i];
