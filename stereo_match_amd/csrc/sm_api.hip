@@ -1669,9 +1669,21 @@ int wls_prepare(sm_ctx* ctx, const uint8_t* guide, size_t guide_pair, int guide_
     return SM_OK;
 }
 
+// lines per smoother workgroup: 16 (k_fgs_solve16, one wave: a pass spreads over 4x the CUs
+// of the 64-line tiles) or 64 (k_fgs_solve, FGS_WAVES waves); same chains, same results
+#ifndef FGS_LINES
+#define FGS_LINES 16
+#endif
 template <int NRHS>
-void launch_fgs_solve(bool rows, dim3 grid, hipStream_t st, const smk::FgsSolveArgs& fa)
+void launch_fgs_solve(bool rows, int nlines, int g, hipStream_t st, const smk::FgsSolveArgs& fa)
 {
+    if (FGS_LINES == 16) {
+        const dim3 grid(nlines / smk::FL, g);
+        if (rows) hipLaunchKernelGGL((smk::k_fgs_solve16<NRHS, true>), grid, dim3(64), 0, st, fa);
+        else hipLaunchKernelGGL((smk::k_fgs_solve16<NRHS, false>), grid, dim3(64), 0, st, fa);
+        return;
+    }
+    const dim3 grid(nlines / smk::FT, g);
     if (rows) hipLaunchKernelGGL((smk::k_fgs_solve<NRHS, true>), grid, dim3(64 * FGS_WAVES), 0, st, fa);
     else hipLaunchKernelGGL((smk::k_fgs_solve<NRHS, false>), grid, dim3(64 * FGS_WAVES), 0, st, fa);
 }
@@ -1753,9 +1765,9 @@ int run_wls(sm_ctx* ctx, const int16_t* dl, const int16_t* dr, size_t disp_pair,
                         fa.C = dir == 0 ? ca.Ch : ca.Cv;
                         fa.R = (const float*)ctx->wls_R.p + dir * dirv + it * var;
                         fa.IT = (const float*)ctx->wls_IT.p + dir * dirv + it * var;
-                        const dim3 grid((dir == 0 ? hp : wp) / smk::FT, g);
-                        if (nrhs == 2) launch_fgs_solve<2>(dir == 0, grid, ctx->stream, fa);
-                        else launch_fgs_solve<1>(dir == 0, grid, ctx->stream, fa);
+                        const int nlines = dir == 0 ? hp : wp;  // multiples of FT (and of FL)
+                        if (nrhs == 2) launch_fgs_solve<2>(dir == 0, nlines, g, ctx->stream, fa);
+                        else launch_fgs_solve<1>(dir == 0, nlines, g, ctx->stream, fa);
                         HIP_TRY(ctx, hipGetLastError());
                     }
                 }

@@ -26,6 +26,9 @@ namespace smk {
 #ifndef EW_H16
 #define EW_H16 1  // census: f16 form of the packed recurrence
 #endif
+#ifndef EW_STEPN
+#define EW_STEPN 1  // the step's words stage by stage (no wait states between dependent VOP3P ops)
+#endif
 
 // NP packed u16 pairs -> LT bytes at byte offset off (u8: truncating pack; u16: as is)
 template <typename LT, int NP, int AUX = 0>
@@ -100,8 +103,21 @@ __global__ void __launch_bounds__(256) k_ew(EwArgs a)
 #pragma unroll
             for (int i = 0; i < NP; i++) asm volatile("" : "+v"(C[i])::"memory");
             ring[k].load(rc, s + PF < W1 ? (e + (uint32_t)PF * estep) * (uint32_t)sizeof(CT) : kOOB);
-            uint32_t Ln[NP];
-            const uint32_t mn = sweep_step2<VL, NP, H16>(Lp, minLp, C, P1p, P2p, eL, eR, Ln);  // minLp replicated
+            uint32_t Ln[NP], mn;
+            if constexpr (EW_STEPN) {  // stage-wise over the words (sm_pk.hpp sweep_step2n)
+                uint32_t Lp1[1][NP], m1[1] = {minLp}, C1[1][NP], Ln1[1][NP], mn1[1];
+#pragma unroll
+                for (int i = 0; i < NP; i++) {
+                    Lp1[0][i] = Lp[i];
+                    C1[0][i] = C[i];
+                }
+                sweep_step2n<VL, NP, H16, 1>(Lp1, m1, C1, P1p, P2p, eL, eR, Ln1, mn1);
+#pragma unroll
+                for (int i = 0; i < NP; i++) Ln[i] = Ln1[0][i];
+                mn = mn1[0];
+            } else {
+                mn = sweep_step2<VL, NP, H16>(Lp, minLp, C, P1p, P2p, eL, eR, Ln);  // minLp replicated
+            }
             store_pk<LT, NP, SWEEP_STREAM_AUX>(ro, (line_ok && s < W1) ? e * (uint32_t)sizeof(LT) : kOOB, Ln);
             e += estep;
 #pragma unroll

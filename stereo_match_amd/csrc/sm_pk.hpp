@@ -213,6 +213,141 @@ __device__ __forceinline__ uint32_t sweep_step2(const uint32_t (&Lp)[NP], uint32
     return group_min<VL>(mn);  // replicated halves: u32 minima are exact
 }
 
+// ND independent recurrences of sweep_step2 (e.g. the A and B diagonals of one column, or a
+// halo wave's two column sets), issued word by word across the directions: the packed
+// (VOP3P) operations of one recurrence form a dependent chain, and on gfx950 a VOP3P that
+// reads the VGPR the previous VALU wrote needs a wait state (s_nop 0) — with ND chains
+// interleaved the dependent operations are never adjacent.  The DPP minimum steps are
+// interleaved the same way (a DPP read of a VGPR the previous VALU wrote needs two wait
+// states).  Same operations, same order per recurrence: results identical to sweep_step2.
+template <int N, int ND>
+__device__ __forceinline__ void group_min_n(uint32_t (&v)[ND])
+{
+    static_assert(N == 1 || N == 2 || N == 4 || N == 8 || N == 16, "lane group of 1-16 lanes");
+    if constexpr (N >= 2) {
+#pragma unroll
+        for (int n = 0; n < ND; n++) v[n] = ::min(v[n], perm_dpp<DPP_QP_XOR1>(v[n]));
+    }
+    if constexpr (N >= 4) {
+#pragma unroll
+        for (int n = 0; n < ND; n++) v[n] = ::min(v[n], perm_dpp<DPP_QP_XOR2>(v[n]));
+    }
+    if constexpr (N >= 8) {
+#pragma unroll
+        for (int n = 0; n < ND; n++) v[n] = ::min(v[n], perm_dpp<DPP_ROW_HALF_MIRROR>(v[n]));
+    }
+    if constexpr (N >= 16) {
+#pragma unroll
+        for (int n = 0; n < ND; n++) v[n] = ::min(v[n], perm_dpp<DPP_ROW_MIRROR>(v[n]));
+    }
+}
+
+template <int VL, int NP, bool H16, int ND>
+__device__ __forceinline__ void sweep_step2n(const uint32_t (&Lp)[ND][NP], const uint32_t (&mmp)[ND],
+                                             const uint32_t (&C)[ND][NP], uint32_t P1p, uint32_t P2p, uint32_t eL,
+                                             uint32_t eR, uint32_t (&Ln)[ND][NP], uint32_t (&mn)[ND])
+{
+    constexpr uint32_t EDGE = H16 ? 0x7BFF7BFFu : (kBig | (kBig << 16));
+    uint32_t lm[ND], lq[ND], dl[ND], a1[ND];
+#pragma unroll
+    for (int n = 0; n < ND; n++) {
+        if constexpr (VL == 16) {
+            lm[n] = perm_dpp<DPP_ROW_SHR1>(Lp[n][NP - 1]) | eL;
+            lq[n] = perm_dpp<DPP_ROW_SHL1>(Lp[n][0]) | eR;
+        } else if constexpr (VL == 8 || VL == 4) {
+            const uint32_t pm = perm_dpp<DPP_ROW_SHR1>(Lp[n][NP - 1]), pq = perm_dpp<DPP_ROW_SHL1>(Lp[n][0]);
+            lm[n] = eL ? EDGE : pm;
+            lq[n] = eR ? EDGE : pq;
+        } else {
+            lm[n] = Line<VL>::prev(EDGE, Lp[n][NP - 1]);
+            lq[n] = Line<VL>::next(EDGE, Lp[n][0]);
+        }
+    }
+#pragma unroll
+    for (int n = 0; n < ND; n++) {
+        dl[n] = H16 ? h2add(mmp[n], P2p) : pk_add(mmp[n], P2p);
+        a1[n] = __builtin_amdgcn_alignbit(Lp[n][0], lm[n], 16);
+    }
+    // the words of one recurrence are independent too (a word's d-1 / d+1 neighbours come
+    // from the previous step's L), so every stage runs over all ND x NP words before the next
+    uint32_t v[ND][NP];
+#pragma unroll
+    for (int k = 0; k < NP; k++) {
+#pragma unroll
+        for (int n = 0; n < ND; n++)
+            v[n][k] = __builtin_amdgcn_alignbit(k + 1 < NP ? Lp[n][k + 1] : lq[n], Lp[n][k], 16);
+    }
+    // v[n][k] now holds the (d+1, d+2) neighbours of word k; (d-1, d) = a1 for k = 0, else
+    // v[n][k-1]
+#pragma unroll
+    for (int k = NP - 1; k >= 0; k--) {
+#pragma unroll
+        for (int n = 0; n < ND; n++) {
+            const uint32_t lo = k == 0 ? a1[n] : v[n][k - 1];
+            v[n][k] = H16 ? h2min(lo, v[n][k]) : pk_min(lo, v[n][k]);
+        }
+    }
+    if constexpr (H16) {
+#pragma unroll
+        for (int k = 0; k < NP; k++)
+#pragma unroll
+            for (int n = 0; n < ND; n++) v[n][k] = h2add(v[n][k], P1p);
+#pragma unroll
+        for (int k = 0; k < NP; k++)
+#pragma unroll
+            for (int n = 0; n < ND; n++) v[n][k] = h2min3(v[n][k], Lp[n][k], dl[n]);
+#pragma unroll
+        for (int k = 0; k < NP; k++)
+#pragma unroll
+            for (int n = 0; n < ND; n++) v[n][k] = h2sub(v[n][k], mmp[n]);
+#pragma unroll
+        for (int k = 0; k < NP; k++)
+#pragma unroll
+            for (int n = 0; n < ND; n++) Ln[n][k] = h2add(v[n][k], C[n][k]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < NP; k++)
+#pragma unroll
+            for (int n = 0; n < ND; n++) v[n][k] = pk_add(v[n][k], P1p);
+#pragma unroll
+        for (int k = 0; k < NP; k++)
+#pragma unroll
+            for (int n = 0; n < ND; n++) v[n][k] = pk_min(v[n][k], Lp[n][k]);
+#pragma unroll
+        for (int k = 0; k < NP; k++)
+#pragma unroll
+            for (int n = 0; n < ND; n++) v[n][k] = pk_min(v[n][k], dl[n]);
+#pragma unroll
+        for (int k = 0; k < NP; k++)
+#pragma unroll
+            for (int n = 0; n < ND; n++) v[n][k] = pk_sub(v[n][k], mmp[n]);
+#pragma unroll
+        for (int k = 0; k < NP; k++)
+#pragma unroll
+            for (int n = 0; n < ND; n++) Ln[n][k] = pk_add(C[n][k], v[n][k]);
+    }
+#pragma unroll
+    for (int n = 0; n < ND; n++) mn[n] = Ln[n][0];
+    if constexpr (H16) {
+#pragma unroll
+        for (int k = 1; k < NP; k += 2) {
+#pragma unroll
+            for (int n = 0; n < ND; n++) mn[n] = k + 1 < NP ? h2min3(mn[n], Ln[n][k], Ln[n][k + 1]) : h2min(mn[n], Ln[n][k]);
+        }
+#pragma unroll
+        for (int n = 0; n < ND; n++) mn[n] = h2min(mn[n], __builtin_amdgcn_alignbit(mn[n], mn[n], 16));
+    } else {
+#pragma unroll
+        for (int k = 1; k < NP; k++) {
+#pragma unroll
+            for (int n = 0; n < ND; n++) mn[n] = pk_min(mn[n], Ln[n][k]);
+        }
+#pragma unroll
+        for (int n = 0; n < ND; n++) mn[n] = pk_min(mn[n], __builtin_amdgcn_alignbit(mn[n], mn[n], 16));
+    }
+    group_min_n<VL, ND>(mn);  // replicated halves: u32 minima are exact
+}
+
 // raw cost / E / W bytes of one lane -> NP packed pairs (u16 already pairs; u8 widened)
 template <typename CT, int DPL>
 __device__ __forceinline__ void unpack_ct_pk(const RawBytes<DPL * (int)sizeof(CT)>& r, uint32_t (&C)[DPL / 2])

@@ -93,6 +93,15 @@ constexpr uint32_t SW_SPIN_LIMIT = 1u << 19;
 #ifndef SWEEP_H16
 #define SWEEP_H16 1
 #endif
+// packed row loops: the recurrences that wait on the LDS row (A and B of an own wave, the
+// column sets of a halo wave) issued interleaved (sm_pk.hpp sweep_step2n: no wait states
+// between dependent VOP3P operations)
+#ifndef SWEEP_STEPN
+#define SWEEP_STEPN 1
+#endif
+#ifndef SWEEP_LDS_FIRST
+#define SWEEP_LDS_FIRST 1  // a scheduling barrier after the row's LDS reads (see the row loop)
+#endif
 
 // NCW: compute waves per workgroup (left halo, NCW-2 own, right halo).  Every strip
 // recomputes 2 halo waves' columns, so wider strips cost fewer instructions per own
@@ -336,7 +345,10 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
     // neighbour-counter row sync: KITTI 8 pairs, down sweep census8 96.4 -> 92.0 us per pair,
     // sgbm8 124.0 -> 120.8, census8 WTA sweep level (96.6 / 96.0); the 5-path WTA sweep is
     // slower with it (95.3 -> 97.9) and keeps the row barriers
-    constexpr bool ROWSYNC = SWEEP_ROW_SYNC && MODE != 1;
+#ifndef SWEEP_ROWSYNC_M1
+#define SWEEP_ROWSYNC_M1 0
+#endif
+    constexpr bool ROWSYNC = SWEEP_ROW_SYNC && (MODE != 1 || SWEEP_ROWSYNC_M1);
     constexpr int LPW = G::LPW, NCW = G::NCW, HB = G::HB, NCOL = G::NCOL, COLS = G::COLS, CW = G::CW, D = G::D;
     constexpr int NG = G::NG, SNG = G::SNG, PF = G::PF, HM = G::HM, HW = G::HW;
     constexpr int CB = DPL * (int)sizeof(CT);  // cost / E / W bytes per lane and cell
@@ -649,15 +661,81 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
                             mB[h] = lmin[rb][1][ch + 2];
                         }
                     }
+                    // the LDS reads leave before the V step (which does not need them), so their
+                    // latency overlaps V instead of adding to the row hand-off chain (the
+                    // scheduler otherwise issued V first)
+                    if constexpr (SWEEP_LDS_FIRST) __builtin_amdgcn_sched_barrier(0);
                     uint32_t nV[NP], nA[NS][NP], nB[NS][NP], mnV = 0, mnA[NS], mnB[NS];
                     auto step = [&](const uint32_t(&Lp)[NP], uint32_t m, const uint32_t(&Ch)[NP], uint32_t(&Ln)[NP]) {
                         return sweep_step2<VL, NP, H16>(Lp, m, Ch, P1p, P2p, eL, eR, Ln);
                     };
-                    if constexpr (OWN) mnV = step(LVp, mVl, C[0], nV);
+                    if constexpr (OWN) {
+                        if constexpr (SWEEP_STEPN) {  // stage-wise over the words (sweep_step2n)
+                            uint32_t Lp1[1][NP], m1[1] = {mVl}, C1[1][NP], Ln1[1][NP], mn1[1];
 #pragma unroll
-                    for (int h = 0; h < NS; h++) {
-                        if constexpr (HAS_A) mnA[h] = step(LA[h], mA[h], C[h], nA[h]);
-                        if constexpr (HAS_B) mnB[h] = step(LB[h], mB[h], C[h], nB[h]);
+                            for (int i = 0; i < NP; i++) {
+                                Lp1[0][i] = LVp[i];
+                                C1[0][i] = C[0][i];
+                            }
+                            sweep_step2n<VL, NP, H16, 1>(Lp1, m1, C1, P1p, P2p, eL, eR, Ln1, mn1);
+#pragma unroll
+                            for (int i = 0; i < NP; i++) nV[i] = Ln1[0][i];
+                            mnV = mn1[0];
+                        } else {
+                            mnV = step(LVp, mVl, C[0], nV);
+                        }
+                    }
+                    if constexpr (SWEEP_STEPN && OWN && NS == 1) {
+                        // A and B of the column, interleaved (sm_pk.hpp sweep_step2n)
+                        uint32_t Lp2[2][NP], m2[2], C2[2][NP], Ln2[2][NP], mn2[2];
+#pragma unroll
+                        for (int i = 0; i < NP; i++) {
+                            Lp2[0][i] = LA[0][i];
+                            Lp2[1][i] = LB[0][i];
+                            C2[0][i] = C2[1][i] = C[0][i];
+                        }
+                        m2[0] = mA[0];
+                        m2[1] = mB[0];
+                        sweep_step2n<VL, NP, H16, 2>(Lp2, m2, C2, P1p, P2p, eL, eR, Ln2, mn2);
+#pragma unroll
+                        for (int i = 0; i < NP; i++) {
+                            nA[0][i] = Ln2[0][i];
+                            nB[0][i] = Ln2[1][i];
+                        }
+                        mnA[0] = mn2[0];
+                        mnB[0] = mn2[1];
+                    } else if constexpr (SWEEP_STEPN && !OWN && NS > 1) {
+                        // a halo wave's column sets of its one direction, interleaved
+                        uint32_t Lpn[NS][NP], mn_in[NS], Lnn[NS][NP], mnn[NS];
+#pragma unroll
+                        for (int h = 0; h < NS; h++) {
+                            if constexpr (HAS_A) {
+#pragma unroll
+                                for (int i = 0; i < NP; i++) Lpn[h][i] = LA[h][i];
+                                mn_in[h] = mA[h];
+                            } else {
+#pragma unroll
+                                for (int i = 0; i < NP; i++) Lpn[h][i] = LB[h][i];
+                                mn_in[h] = mB[h];
+                            }
+                        }
+                        sweep_step2n<VL, NP, H16, NS>(Lpn, mn_in, C, P1p, P2p, eL, eR, Lnn, mnn);
+#pragma unroll
+                        for (int h = 0; h < NS; h++) {
+#pragma unroll
+                            for (int i = 0; i < NP; i++) {
+                                if constexpr (HAS_A) nA[h][i] = Lnn[h][i];
+                                else nB[h][i] = Lnn[h][i];
+                            }
+                            if constexpr (HAS_A) mnA[h] = mnn[h];
+                            else mnB[h] = mnn[h];
+                        }
+                    } else {
+#pragma unroll
+                        for (int h = 0; h < NS; h++) {
+                            if constexpr (HAS_A) mnA[h] = step(LA[h], mA[h], C[h], nA[h]);
+                            if constexpr (HAS_B) mnB[h] = step(LB[h], mB[h], C[h], nB[h]);
+                        }
                     }
                     // snapshot of the block's last row for the neighbouring strips' halos: the
                     // strip's HM boundary own waves on each side (before the block-end barrier
@@ -715,39 +793,62 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
                         for (int i = 0; i < NP; i++) LVp[i] = nV[i];
                         mVl = mnV;
                         if constexpr (!SWEEP_EARLY_XCHG) snapshot();
+                        // every per-word loop below runs stage by stage over the NP words (the
+                        // words are independent: no wait state between dependent VOP3P ops)
                         if constexpr (MODE == 0) {
                             uint32_t out[NP];
 #pragma unroll
-                            for (int i = 0; i < NP; i++) out[i] = pk_add(pk_add(nV[i], nA[0][i]), nB[0][i]);
+                            for (int i = 0; i < NP; i++) out[i] = pk_add(nV[i], nA[0][i]);
+#pragma unroll
+                            for (int i = 0; i < NP; i++) out[i] = pk_add(out[i], nB[0][i]);
                             bstore_n<uint32_t, NP, SWEEP_STREAM_AUX>(rp, boff(e, 2), out);
                         } else {
-                            uint32_t Sp[NP];
-                            uint32_t key = 0xFFFFFFFFu;
+                            uint32_t Sp[NP], ew[NP];
                             // a padded cost volume (u16 costs only): its pad planes d >= Dv take
                             // S = 0xFFFF, above every real S <= 32767 (never the minimum, never
                             // below the uniqueness threshold)
                             const bool pad = SAT && a.Dv < D;  // wave-uniform
+                            if constexpr (SAT) {
 #pragma unroll
-                            for (int i = 0; i < NP; i++) {
-                                uint32_t t;
-                                if constexpr (SAT) {
-                                    uint32_t ew = pk_adds(Ein[i], Win[i]);
-                                    if constexpr (MODE == 2) ew = pk_adds(ew, Pin[i]);
-                                    t = pk_adds(pk_adds(nV[i], nA[0][i]), pk_adds(nB[0][i], ew));
-                                    t = pk_min(t, 0x7FFF7FFFu);  // min(sum, 32767)
-                                    if (pad) {
-                                        const int d0 = g * DPL + 2 * i;
-                                        t |= (d0 >= a.Dv ? 0x0000FFFFu : 0u) | (d0 + 1 >= a.Dv ? 0xFFFF0000u : 0u);
-                                    }
-                                } else {
-                                    uint32_t ew = pk_add(Ein[i], Win[i]);
-                                    if constexpr (MODE == 2) ew = pk_add(ew, Pin[i]);
-                                    t = pk_add(pk_add(nV[i], nA[0][i]), pk_add(nB[0][i], ew));
+                                for (int i = 0; i < NP; i++) ew[i] = pk_adds(Ein[i], Win[i]);
+                                if constexpr (MODE == 2) {
+#pragma unroll
+                                    for (int i = 0; i < NP; i++) ew[i] = pk_adds(ew[i], Pin[i]);
                                 }
-                                Sp[i] = t;
-                                key = min(key, min((t << 16) | wta_rank(g * DPL + 2 * i, MODE == 1),
-                                                   (t & 0xFFFF0000u) | wta_rank(g * DPL + 2 * i + 1, MODE == 1)));
+#pragma unroll
+                                for (int i = 0; i < NP; i++) Sp[i] = pk_adds(nV[i], nA[0][i]);
+#pragma unroll
+                                for (int i = 0; i < NP; i++) ew[i] = pk_adds(nB[0][i], ew[i]);
+#pragma unroll
+                                for (int i = 0; i < NP; i++) Sp[i] = pk_adds(Sp[i], ew[i]);
+#pragma unroll
+                                for (int i = 0; i < NP; i++) Sp[i] = pk_min(Sp[i], 0x7FFF7FFFu);  // min(sum, 32767)
+                                if (pad) {
+#pragma unroll
+                                    for (int i = 0; i < NP; i++) {
+                                        const int d0 = g * DPL + 2 * i;
+                                        Sp[i] |= (d0 >= a.Dv ? 0x0000FFFFu : 0u) | (d0 + 1 >= a.Dv ? 0xFFFF0000u : 0u);
+                                    }
+                                }
+                            } else {
+#pragma unroll
+                                for (int i = 0; i < NP; i++) ew[i] = pk_add(Ein[i], Win[i]);
+                                if constexpr (MODE == 2) {
+#pragma unroll
+                                    for (int i = 0; i < NP; i++) ew[i] = pk_add(ew[i], Pin[i]);
+                                }
+#pragma unroll
+                                for (int i = 0; i < NP; i++) Sp[i] = pk_add(nV[i], nA[0][i]);
+#pragma unroll
+                                for (int i = 0; i < NP; i++) ew[i] = pk_add(nB[0][i], ew[i]);
+#pragma unroll
+                                for (int i = 0; i < NP; i++) Sp[i] = pk_add(Sp[i], ew[i]);
                             }
+                            uint32_t key = 0xFFFFFFFFu;
+#pragma unroll
+                            for (int i = 0; i < NP; i++)
+                                key = min(key, min((Sp[i] << 16) | wta_rank(g * DPL + 2 * i, MODE == 1),
+                                                   (Sp[i] & 0xFFFF0000u) | wta_rank(g * DPL + 2 * i + 1, MODE == 1)));
                             lds_put_pk<NP>(&srow[(wave - 1) % (NCW - 2)][kl][g * DPL], Sp);
                             key = group_min<VL>(key);
                             const uint32_t minS = key >> 16;
@@ -762,14 +863,18 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
                             // (best-1) in {0, 1, 2} exactly inside it, 3 - t (saturating) > 0 there,
                             // times 0xFFFF = -(3 - t) mod 2^16.
                             const uint32_t bm1p = (uint32_t)best * 0x10001u;  // t = (d + 1) - best = d - (best - 1)
-                            uint32_t m2p = 0xFFFFFFFFu;
+                            uint32_t tw[NP];
 #pragma unroll
-                            for (int i = 0; i < NP; i++) {
-                                const uint32_t t = pk_sub(dpk[i], bm1p);
-                                const uint32_t w = pkw(__builtin_elementwise_sub_sat(pkv(0x00030003u), pkv(t)));
-                                const uint32_t mask = pkw(pkv(w) * pkv(0xFFFFFFFFu));
-                                m2p = pk_min(m2p, pk_adds(Sp[i], mask));
-                            }
+                            for (int i = 0; i < NP; i++) tw[i] = pk_sub(dpk[i], bm1p);
+#pragma unroll
+                            for (int i = 0; i < NP; i++) tw[i] = pkw(__builtin_elementwise_sub_sat(pkv(0x00030003u), pkv(tw[i])));
+#pragma unroll
+                            for (int i = 0; i < NP; i++) tw[i] = pkw(pkv(tw[i]) * pkv(0xFFFFFFFFu));
+#pragma unroll
+                            for (int i = 0; i < NP; i++) tw[i] = pk_adds(Sp[i], tw[i]);
+                            uint32_t m2p = tw[0];
+#pragma unroll
+                            for (int i = 1; i < NP; i++) m2p = pk_min(m2p, tw[i]);
                             const uint32_t m2 = group_min<VL>(min(m2p & 0xFFFFu, m2p >> 16));
                             // (m2 = 0xFFFF: no real far entry, only pad planes of a volume with Dv <= 3)
                             const bool ok = !(__mul24((int)m2, ku) < __mul24((int)minS, 100) && (!pad || m2 <= 32767u)) &&

@@ -607,7 +607,7 @@ struct FgsSolveArgs {
 #endif
 // materialise a loaded value at this point of the program (the read cannot sink below it)
 __device__ __forceinline__ void fgs_pin(float& x) { asm volatile("" : "+v"(x)); }
-template <int NRHS, bool ROWS>
+template <int NRHS, bool ROWS, class M = TileMap<ROWS>>
 __device__ __forceinline__ void fgs_fwd_chunk(const float* RT, float* U0, float* U1, const float* Ct, int lane,
                                               float lam, float& p0, float& p1, float& cp)
 {
@@ -616,7 +616,7 @@ __device__ __forceinline__ void fgs_fwd_chunk(const float* RT, float* U0, float*
     float r[2][SB], u0[2][SB], u1[2][NRHS == 2 ? SB : 1], cc[2][SB];
 #pragma unroll
     for (int k = 0; k < SB; k++) {
-        const int t = TileMap<ROWS>::tix(lane, k);
+        const int t = M::tix(lane, k);
         r[0][k] = RT[t];
         u0[0][k] = U0[t];
         if (NRHS == 2) u1[0][k] = U1[t];
@@ -635,7 +635,7 @@ __device__ __forceinline__ void fgs_fwd_chunk(const float* RT, float* U0, float*
         if (b + 1 < NSB) {
 #pragma unroll
             for (int k = 0; k < SB; k++) {
-                const int t = TileMap<ROWS>::tix(lane, (b + 1) * SB + k);
+                const int t = M::tix(lane, (b + 1) * SB + k);
                 r[nxt][k] = RT[t];
                 u0[nxt][k] = U0[t];
                 if (NRHS == 2) u1[nxt][k] = U1[t];
@@ -664,7 +664,7 @@ __device__ __forceinline__ void fgs_fwd_chunk(const float* RT, float* U0, float*
         }
 #pragma unroll
         for (int k = 0; k < SB; k++) {
-            const int t = TileMap<ROWS>::tix(lane, b * SB + k);
+            const int t = M::tix(lane, b * SB + k);
             U0[t] = u0[cur][k];
             if (NRHS == 2) U1[t] = u1[cur][k];
         }
@@ -672,7 +672,7 @@ __device__ __forceinline__ void fgs_fwd_chunk(const float* RT, float* U0, float*
 }
 
 // backward over a full chunk, positions 63 .. 0 (RT holds c')
-template <int NRHS, bool ROWS>
+template <int NRHS, bool ROWS, class M = TileMap<ROWS>>
 __device__ __forceinline__ void fgs_bwd_chunk(const float* RT, float* U0, float* U1, int lane, float& p0, float& p1)
 {
 #pragma clang fp contract(off)
@@ -680,7 +680,7 @@ __device__ __forceinline__ void fgs_bwd_chunk(const float* RT, float* U0, float*
     float f[2][SB], u0[2][SB], u1[2][NRHS == 2 ? SB : 1];
 #pragma unroll
     for (int k = 0; k < SB; k++) {
-        const int t = TileMap<ROWS>::tix(lane, FT - 1 - k);
+        const int t = M::tix(lane, FT - 1 - k);
         f[0][k] = RT[t];
         u0[0][k] = U0[t];
         if (NRHS == 2) u1[0][k] = U1[t];
@@ -697,7 +697,7 @@ __device__ __forceinline__ void fgs_bwd_chunk(const float* RT, float* U0, float*
         if (b + 1 < NSB) {
 #pragma unroll
             for (int k = 0; k < SB; k++) {
-                const int t = TileMap<ROWS>::tix(lane, FT - 1 - (b + 1) * SB - k);
+                const int t = M::tix(lane, FT - 1 - (b + 1) * SB - k);
                 f[nxt][k] = RT[t];
                 u0[nxt][k] = U0[t];
                 if (NRHS == 2) u1[nxt][k] = U1[t];
@@ -722,7 +722,7 @@ __device__ __forceinline__ void fgs_bwd_chunk(const float* RT, float* U0, float*
         }
 #pragma unroll
         for (int k = 0; k < SB; k++) {
-            const int t = TileMap<ROWS>::tix(lane, FT - 1 - b * SB - k);
+            const int t = M::tix(lane, FT - 1 - b * SB - k);
             U0[t] = u0[cur][k];
             if (NRHS == 2) U1[t] = u1[cur][k];
         }
@@ -871,6 +871,208 @@ __global__ void __launch_bounds__(64 * FGS_WAVES) k_fgs_solve(FgsSolveArgs a)
             tile_to_lds_part<ROWS, NK>(rr, RT, lane, k0);
             tile_to_lds_part<ROWS, NK>(r0, U0, lane, k0);
             if (NRHS == 2) tile_to_lds_part<ROWS, NK>(r1, U1, lane, k0);
+        }
+    }
+}
+
+// ---- narrow tiles (round 4): 16 lines x 64 positions, one wave per workgroup.  The 64-line
+// workgroups above put a pass's whole tile traffic through 6 CUs on the KITTI row pass (375
+// lines): each 64-step chunk moved 96 KB through one CU's LDS between its chain steps, ~3 us
+// per chunk.  With 16 lines per workgroup the same pass spreads over 4x the CUs, a chunk moves
+// 24 KB, and the lane -> chain mapping (and so every chain's float32 operations and their
+// order) is unchanged: lane l runs line l % 16 (lanes with bit 4 set: the second right-hand
+// side), lanes 32..63 repeat lanes 0..31.
+constexpr int FL = 16;       // lines per narrow tile
+constexpr int FPC = FL + 1;  // LDS pitch of a column tile's position rows
+template <bool ROWS>
+struct TileMap16 {
+    // load k (0..3) of lane -> local (line, pos) of the float4's first element; the float4
+    // runs along pos (ROWS: 4 lines of 64 positions per load) or along line (columns: 16
+    // positions of 16 lines per load)
+    __device__ static void at(int k, int lane, int& ll, int& pl)
+    {
+        if (ROWS) {
+            ll = 4 * k + (lane >> 4);
+            pl = (lane & 15) * 4;
+        } else {
+            pl = 16 * k + (lane >> 2);
+            ll = (lane & 3) * 4;
+        }
+    }
+    __device__ static int tix(int ll, int pl) { return ROWS ? ll * FP + pl : pl * FPC + ll; }
+    __device__ static int tix_e(int ll, int pl, int e) { return ROWS ? tix(ll, pl + e) : tix(ll + e, pl); }
+    static constexpr int KSTEP = ROWS ? 16 : 64;  // byte step of load k per element of pitch wp
+    static constexpr int TS = ROWS ? FL * FP : FT * FPC;
+};
+
+template <bool ROWS>
+__device__ inline void tile16_load(float4 (&r)[4], rsrc_t rs, uint32_t voff, int wp)
+{
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, k * TileMap16<ROWS>::KSTEP * wp, 0);
+        r[k] = make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+    }
+}
+
+template <bool ROWS>
+__device__ inline void tile16_to_lds(const float4 (&r)[4], float* T, int lane)
+{
+    using M = TileMap16<ROWS>;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        int ll, pl;
+        M::at(k, lane, ll, pl);
+        T[M::tix_e(ll, pl, 0)] = r[k].x;
+        T[M::tix_e(ll, pl, 1)] = r[k].y;
+        T[M::tix_e(ll, pl, 2)] = r[k].z;
+        T[M::tix_e(ll, pl, 3)] = r[k].w;
+    }
+}
+
+template <bool ROWS>
+__device__ inline void tile16_store(rsrc_t rs, uint32_t voff, const float* T, int wp, int lane)
+{
+    using M = TileMap16<ROWS>;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        int ll, pl;
+        M::at(k, lane, ll, pl);
+        u32x4 v;
+        v[0] = __float_as_uint(T[M::tix_e(ll, pl, 0)]);
+        v[1] = __float_as_uint(T[M::tix_e(ll, pl, 1)]);
+        v[2] = __float_as_uint(T[M::tix_e(ll, pl, 2)]);
+        v[3] = __float_as_uint(T[M::tix_e(ll, pl, 3)]);
+        // offset in the VGPR, soffset the literal 0 (see tile_store: gfx950 store-data hazard)
+        __builtin_amdgcn_raw_buffer_store_b128(v, rs, voff + (uint32_t)(k * M::KSTEP * wp), 0, 0);
+    }
+}
+
+template <int NRHS, bool ROWS>
+__global__ void __launch_bounds__(64) k_fgs_solve16(FgsSolveArgs a)
+{
+#pragma clang fp contract(off)
+    using M = TileMap16<ROWS>;
+    __shared__ float Ct[M::TS], RT[M::TS], U0[M::TS], U1[NRHS == 2 ? M::TS : 1];
+    const int lane = threadIdx.x, pair = blockIdx.y;
+    const int cl = lane % FL;  // the line this lane's chain runs
+    const int n = ROWS ? a.w : a.h;
+    const int l0 = blockIdx.x * FL, wp = a.wp;
+    const uint64_t bytes = a.roi_pair * 4;
+    const rsrc_t u0 = make_rsrc(a.u[0] + pair * a.roi_pair, bytes);
+    const rsrc_t u1 = make_rsrc(a.u[NRHS == 2 ? 1 : 0] + pair * a.roi_pair, bytes);
+    const rsrc_t C = make_rsrc(a.C + pair * a.roi_pair, bytes);
+    const rsrc_t R = make_rsrc(a.R + pair * a.roi_pair, bytes);
+    const rsrc_t I = make_rsrc(a.IT + pair * a.roi_pair, bytes);
+    int ll0, pl0;
+    M::at(0, lane, ll0, pl0);
+    const uint32_t voff0 = (uint32_t)(TileMap<ROWS>::eoff(l0 + ll0, pl0, wp) * 4);
+    const uint32_t cstep = ROWS ? FT * 4 : (uint32_t)FT * wp * 4;
+    const float lam = a.lam;
+    const int nchunks = (n + FT - 1) / FT;
+    float4 rc[4], rr[4], r0[4], r1[4];
+    tile16_load<ROWS>(rc, C, voff0, wp);
+    tile16_load<ROWS>(rr, R, voff0, wp);
+    tile16_load<ROWS>(r0, u0, voff0, wp);
+    if (NRHS == 2) tile16_load<ROWS>(r1, u1, voff0, wp);
+    tile16_to_lds<ROWS>(rc, Ct, lane);
+    tile16_to_lds<ROWS>(rr, RT, lane);
+    tile16_to_lds<ROWS>(r0, U0, lane);
+    if (NRHS == 2) tile16_to_lds<ROWS>(r1, U1, lane);
+    constexpr bool SPLIT = NRHS == 2;  // lanes with bit 4 set take u[1] (scalar chains, as FGS_SPLIT)
+    constexpr int NC = SPLIT ? 1 : NRHS;
+    float* const UA = SPLIT && (lane & 16) ? U1 : U0;
+    float* const UB = U1;
+    float p0 = 0.f, p1 = 0.f, cp = 0.f;
+    for (int c = 0; c < nchunks; c++) {
+        const int j0 = c * FT;
+        const bool next = c + 1 < nchunks;
+        __syncthreads();
+        if (next) {  // prefetch chunk c+1 (consumed after the sweep)
+            const uint32_t vn = voff0 + (c + 1) * cstep;
+            tile16_load<ROWS>(rc, C, vn, wp);
+            tile16_load<ROWS>(rr, R, vn, wp);
+            tile16_load<ROWS>(r0, u0, vn, wp);
+            if (NRHS == 2) tile16_load<ROWS>(r1, u1, vn, wp);
+        }
+        const int m = min(FT, n - j0);
+        if (m == FT) {
+            fgs_fwd_chunk<NC, ROWS, M>(RT, UA, UB, Ct, cl, lam, p0, p1, cp);
+        } else {
+#pragma unroll 8
+            for (int jj = 0; jj < m; jj++) {
+                const int t = M::tix(cl, jj);
+                const float r = RT[t];
+                const float lcp = lam * cp;
+                p0 = (UA[t] - lcp * p0) * r;
+                UA[t] = p0;
+                if (NC == 2) {
+                    p1 = (UB[t] - lcp * p1) * r;
+                    UB[t] = p1;
+                }
+                cp = Ct[t];
+            }
+        }
+        __syncthreads();
+        const uint32_t vc = voff0 + c * cstep;
+        tile16_store<ROWS>(u0, vc, U0, wp, lane);
+        if (NRHS == 2) tile16_store<ROWS>(u1, vc, U1, wp, lane);
+        if (next) {
+            __syncthreads();
+            tile16_to_lds<ROWS>(rc, Ct, lane);
+            tile16_to_lds<ROWS>(rr, RT, lane);
+            tile16_to_lds<ROWS>(r0, U0, lane);
+            if (NRHS == 2) tile16_to_lds<ROWS>(r1, U1, lane);
+        }
+    }
+    // backward substitution; the last chunk's d' is still in LDS (RT takes c')
+    {
+        __syncthreads();
+        tile16_load<ROWS>(rr, I, voff0 + (nchunks - 1) * cstep, wp);
+        tile16_to_lds<ROWS>(rr, RT, lane);
+    }
+    for (int c = nchunks - 1; c >= 0; c--) {
+        const int j0 = c * FT;
+        const bool prev = c > 0;
+        __syncthreads();
+        if (prev) {
+            const uint32_t vp = voff0 + (c - 1) * cstep;
+            tile16_load<ROWS>(rr, I, vp, wp);
+            tile16_load<ROWS>(r0, u0, vp, wp);
+            if (NRHS == 2) tile16_load<ROWS>(r1, u1, vp, wp);
+        }
+        const int m = min(FT, n - j0);
+        int jj = m - 1;
+        if (c == nchunks - 1) {  // x[n-1] = d'[n-1]
+            const int t = M::tix(cl, jj);
+            p0 = UA[t];
+            if (NC == 2) p1 = UB[t];
+            jj--;
+        }
+        if (jj == FT - 1) {
+            fgs_bwd_chunk<NC, ROWS, M>(RT, UA, UB, cl, p0, p1);
+        } else {
+#pragma unroll 8
+            for (; jj >= 0; jj--) {
+                const int t = M::tix(cl, jj);
+                const float f = RT[t];
+                p0 = UA[t] - f * p0;
+                UA[t] = p0;
+                if (NC == 2) {
+                    p1 = UB[t] - f * p1;
+                    UB[t] = p1;
+                }
+            }
+        }
+        __syncthreads();
+        const uint32_t vc = voff0 + c * cstep;
+        tile16_store<ROWS>(u0, vc, U0, wp, lane);
+        if (NRHS == 2) tile16_store<ROWS>(u1, vc, U1, wp, lane);
+        if (prev) {
+            __syncthreads();
+            tile16_to_lds<ROWS>(rr, RT, lane);
+            tile16_to_lds<ROWS>(r0, U0, lane);
+            if (NRHS == 2) tile16_to_lds<ROWS>(r1, U1, lane);
         }
     }
 }
