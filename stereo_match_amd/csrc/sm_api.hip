@@ -388,16 +388,18 @@ const int kVdy[6] = {1, 1, 1, -1, -1, -1};
 // dynamic LDS a row kernel (k_wta, k_wide_wta, k_lr_rows: one image row's disp2 keys and
 // sub-pixel values) may request: HIP's default per-workgroup limit
 constexpr size_t kRowLds = 65536;
-constexpr size_t kSetBudget = size_t(12) << 30;  // bytes of path volumes per buffer set
+// bytes of path volumes per buffer set (MI355X: 288 GB of HBM).  Middlebury (2880 x 1988,
+// D = 256) needs 13.4 GB per pair on the sweep engine (the guarded fallback's 8 direction
+// volumes + the partial): 32 GB lets two pairs share a launch group, which the D = 256 wide
+// sweeps run in one launch
+constexpr size_t kSetBudget = size_t(32) << 30;
 constexpr int kMaxGroup = 16;
 // smallest launch group the fused sweeps run by default: their time per launch is nearly
 // flat until the strips fill the CUs, so few pairs run on the per-direction engine (KITTI
 // D = 128 per pair, sweeps vs per-direction: census8 6 pairs 285 vs 259 us, 8 pairs 217 vs
 // 249; sgbm5 3 pairs 440 vs 395, 4 pairs 348 vs 368; sgbm8 3 pairs 540 vs 537)
-int sweep_min_pairs(const Norm& n)
-{
-    return n.cost == SM_COST_CENSUS ? 7 : 3;
-}
+bool sweep_fit_variant(sm_ctx* ctx, const Norm& n, int mode, int variant, struct SweepFit& f);
+int sweep_min_pairs(sm_ctx* ctx, const Norm& n);
 // u8 cost volumes of a per-direction launch group kept below this (MI355X Infinity Cache:
 // 256 MiB), at no fewer than kMallMinPairs pairs per group
 constexpr size_t kMallBudget = size_t(224) << 20;
@@ -741,6 +743,17 @@ bool sweep_fit_variant(sm_ctx* ctx, const Norm& n, int mode, int variant, SweepF
     return f.nwg <= f.cap;
 }
 
+// census: enough pairs for the wide strips to occupy ~200 of the 256 CUs (KITTI: 31 strips
+// per pair -> 7; Middlebury's 2624 columns: 101 strips of the D = 256 instance -> 2), at most
+// 7; other costs: 3 (measured, see above)
+int sweep_min_pairs(sm_ctx* ctx, const Norm& n)
+{
+    if (n.cost != SM_COST_CENSUS) return 3;
+    SweepFit f;
+    if (!sweep_fit_variant(ctx, n, 2, 0, f) || f.nwg <= 0) return 7;
+    return std::max(2, std::min(7, (200 + f.nwg - 1) / f.nwg));
+}
+
 // modelled time of G pairs on one variant: the sweeps are bound by the instruction issue of
 // the CU that holds the most strips, so (launches) x (strips per CU) x (compute waves per
 // strip).  Wide strips recompute fewer halo columns per own column, narrow strips spread a
@@ -751,7 +764,9 @@ double sweep_model(const SweepFit& f, int G)
     const int per_launch = std::max(1, std::min(G, f.cap / std::max(f.nwg, 1)));
     const int launches = (G + per_launch - 1) / per_launch;
     const int per_cu = (per_launch * f.nwg + f.ncu - 1) / std::max(f.ncu, 1);
-    return (double)launches * per_cu * (f.si.threads / 64 - 1);
+    // a wave's work per row scales with its disparities per lane (the D = 256 wide instance
+    // runs 32-lane lines: half the per-wave work of the 16-lane narrow one)
+    return (double)launches * per_cu * (f.si.threads / 64 - 1) * std::max(f.si.dpl, 1);
 }
 
 // the kernel variant for one pass over G pairs (G = 0: any that fits, wide strips first)
@@ -1490,7 +1505,7 @@ int run_pairs(sm_ctx* ctx, const Src& src, int npairs, int H, int W, int stride,
     int G = group_size(ctx, n, H, npairs, g.sweep, g.hybrid);
     // the sweeps' parallelism is (strips x pairs): below sweep_min_pairs pairs per launch
     // group the per-direction engine is faster; flag 16384 forces them
-    if (g.sweep && std::min(G, npairs) < sweep_min_pairs(n) && !(ctx->dbg_flags & DBG_SWEEP8)) {
+    if (g.sweep && std::min(G, npairs) < sweep_min_pairs(ctx, n) && !(ctx->dbg_flags & DBG_SWEEP8)) {
         g.sweep = false;
         G = group_size(ctx, n, H, npairs, false, false);
     }

@@ -153,6 +153,40 @@ struct Line<4> {
     }
 };
 
+// 32-lane lines (two per wave, each spanning two DPP rows): whole-wave shifts (DPP
+// wave_shr / wave_shl cross the row boundary inside a line) plus a fix-up at the line edge
+// (lane 32 would otherwise read lane 31 of the other line)
+template <>
+struct Line<32> {
+    template <typename T>
+    static __device__ __forceinline__ T prev(T edge, T v)
+    {
+        T r;
+        if constexpr (sizeof(T) == 8) r = dpp64<DPP_WAVE_SHR1>(edge, v);
+        else r = dpp<DPP_WAVE_SHR1>(edge, v);
+        return (threadIdx.x & 31) == 0 ? edge : r;
+    }
+    template <typename T>
+    static __device__ __forceinline__ T next(T edge, T v)
+    {
+        T r;
+        if constexpr (sizeof(T) == 8) r = dpp64<DPP_WAVE_SHL1>(edge, v);
+        else r = dpp<DPP_WAVE_SHL1>(edge, v);
+        return (threadIdx.x & 31) == 31 ? edge : r;
+    }
+    static __device__ __forceinline__ uint32_t min(uint32_t v);
+};
+
+// gfx950 v_permlane16_swap of v with itself: in rows 0 and 1 (2 and 3) the two results hold
+// row 0's and row 1's (row 2's and row 3's) values, one each, in some order, so any
+// symmetric combination of the pair (min, max, or, +) combines the two rows of a 32-lane half
+template <class F>
+__device__ __forceinline__ uint32_t row_pair_combine(uint32_t v, F f)
+{
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return f((uint32_t)r[0], (uint32_t)r[1]);
+}
+
 __device__ __forceinline__ uint32_t row16_or(uint32_t v)
 {
     v |= perm_dpp<DPP_QP_XOR1>(v);
@@ -163,6 +197,11 @@ __device__ __forceinline__ uint32_t row16_or(uint32_t v)
 }
 
 __device__ __forceinline__ uint32_t Line<16>::min(uint32_t v) { return row16_min(v); }
+
+__device__ __forceinline__ uint32_t Line<32>::min(uint32_t v)
+{
+    return row_pair_combine(row16_min(v), [](uint32_t a, uint32_t b) { return ::min(a, b); });
+}
 
 __device__ __forceinline__ uint32_t Line<8>::min(uint32_t v)
 {

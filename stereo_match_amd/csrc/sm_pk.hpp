@@ -12,41 +12,46 @@ __device__ __forceinline__ uint32_t line_or(uint32_t v)
     v |= perm_dpp<DPP_QP_XOR1>(v);
     v |= perm_dpp<DPP_QP_XOR2>(v);
     v |= perm_dpp<DPP_ROW_HALF_MIRROR>(v);
-    if constexpr (VL == 16) v |= perm_dpp<DPP_ROW_MIRROR>(v);
+    if constexpr (VL >= 16) v |= perm_dpp<DPP_ROW_MIRROR>(v);
+    if constexpr (VL == 32) v = row_pair_combine(v, [](uint32_t a, uint32_t b) { return a | b; });
     return v;
 }
 
-// minimum over aligned groups of N lanes (N = 1, 2, 4, 8 or 16)
+// minimum over aligned groups of N lanes (N = 1, 2, 4, 8, 16 or 32: a 32-lane group spans two
+// DPP rows, combined by v_permlane16_swap)
 template <int N>
 __device__ __forceinline__ uint32_t group_min(uint32_t v)
 {
-    static_assert(N == 1 || N == 2 || N == 4 || N == 8 || N == 16, "lane group of 1-16 lanes");
+    static_assert(N == 1 || N == 2 || N == 4 || N == 8 || N == 16 || N == 32, "lane group of 1-32 lanes");
     if constexpr (N >= 2) v = ::min(v, perm_dpp<DPP_QP_XOR1>(v));
     if constexpr (N >= 4) v = ::min(v, perm_dpp<DPP_QP_XOR2>(v));
     if constexpr (N >= 8) v = ::min(v, perm_dpp<DPP_ROW_HALF_MIRROR>(v));
     if constexpr (N >= 16) v = ::min(v, perm_dpp<DPP_ROW_MIRROR>(v));
+    if constexpr (N >= 32) v = row_pair_combine(v, [](uint32_t a, uint32_t b) { return ::min(a, b); });
     return v;
 }
 
 template <int N>
 __device__ __forceinline__ uint32_t group_sum(uint32_t v)
 {
-    static_assert(N == 1 || N == 2 || N == 4 || N == 8 || N == 16, "lane group of 1-16 lanes");
+    static_assert(N == 1 || N == 2 || N == 4 || N == 8 || N == 16 || N == 32, "lane group of 1-32 lanes");
     if constexpr (N >= 2) v += perm_dpp<DPP_QP_XOR1>(v);
     if constexpr (N >= 4) v += perm_dpp<DPP_QP_XOR2>(v);
     if constexpr (N >= 8) v += perm_dpp<DPP_ROW_HALF_MIRROR>(v);
     if constexpr (N >= 16) v += perm_dpp<DPP_ROW_MIRROR>(v);
+    if constexpr (N >= 32) v = row_pair_combine(v, [](uint32_t a, uint32_t b) { return a + b; });
     return v;
 }
 
 template <int N>
 __device__ __forceinline__ uint32_t group_max(uint32_t v)
 {
-    static_assert(N == 1 || N == 2 || N == 4 || N == 8 || N == 16, "lane group of 1-16 lanes");
+    static_assert(N == 1 || N == 2 || N == 4 || N == 8 || N == 16 || N == 32, "lane group of 1-32 lanes");
     if constexpr (N >= 2) v = ::max(v, perm_dpp<DPP_QP_XOR1>(v));
     if constexpr (N >= 4) v = ::max(v, perm_dpp<DPP_QP_XOR2>(v));
     if constexpr (N >= 8) v = ::max(v, perm_dpp<DPP_ROW_HALF_MIRROR>(v));
     if constexpr (N >= 16) v = ::max(v, perm_dpp<DPP_ROW_MIRROR>(v));
+    if constexpr (N >= 32) v = row_pair_combine(v, [](uint32_t a, uint32_t b) { return ::max(a, b); });
     return v;
 }
 
@@ -181,6 +186,10 @@ __device__ __forceinline__ uint32_t sweep_step2(const uint32_t (&Lp)[NP], uint32
         const uint32_t pm = perm_dpp<DPP_ROW_SHR1>(Lp[NP - 1]), pq = perm_dpp<DPP_ROW_SHL1>(Lp[0]);
         lm = eL ? EDGE : pm;
         lq = eR ? EDGE : pq;
+    } else if constexpr (VL == 32) {  // lines across two DPP rows: whole-wave shifts, edge select
+        const uint32_t pm = perm_dpp<DPP_WAVE_SHR1>(Lp[NP - 1]), pq = perm_dpp<DPP_WAVE_SHL1>(Lp[0]);
+        lm = eL ? EDGE : pm;
+        lq = eR ? EDGE : pq;
     } else {
         lm = Line<VL>::prev(EDGE, Lp[NP - 1]);
         lq = Line<VL>::next(EDGE, Lp[0]);
@@ -223,7 +232,7 @@ __device__ __forceinline__ uint32_t sweep_step2(const uint32_t (&Lp)[NP], uint32
 template <int N, int ND>
 __device__ __forceinline__ void group_min_n(uint32_t (&v)[ND])
 {
-    static_assert(N == 1 || N == 2 || N == 4 || N == 8 || N == 16, "lane group of 1-16 lanes");
+    static_assert(N == 1 || N == 2 || N == 4 || N == 8 || N == 16 || N == 32, "lane group of 1-32 lanes");
     if constexpr (N >= 2) {
 #pragma unroll
         for (int n = 0; n < ND; n++) v[n] = ::min(v[n], perm_dpp<DPP_QP_XOR1>(v[n]));
@@ -239,6 +248,10 @@ __device__ __forceinline__ void group_min_n(uint32_t (&v)[ND])
     if constexpr (N >= 16) {
 #pragma unroll
         for (int n = 0; n < ND; n++) v[n] = ::min(v[n], perm_dpp<DPP_ROW_MIRROR>(v[n]));
+    }
+    if constexpr (N >= 32) {
+#pragma unroll
+        for (int n = 0; n < ND; n++) v[n] = row_pair_combine(v[n], [](uint32_t a, uint32_t b) { return ::min(a, b); });
     }
 }
 
@@ -256,6 +269,10 @@ __device__ __forceinline__ void sweep_step2n(const uint32_t (&Lp)[ND][NP], const
             lq[n] = perm_dpp<DPP_ROW_SHL1>(Lp[n][0]) | eR;
         } else if constexpr (VL == 8 || VL == 4) {
             const uint32_t pm = perm_dpp<DPP_ROW_SHR1>(Lp[n][NP - 1]), pq = perm_dpp<DPP_ROW_SHL1>(Lp[n][0]);
+            lm[n] = eL ? EDGE : pm;
+            lq[n] = eR ? EDGE : pq;
+        } else if constexpr (VL == 32) {  // lines across two DPP rows: whole-wave shifts, edge select
+            const uint32_t pm = perm_dpp<DPP_WAVE_SHR1>(Lp[n][NP - 1]), pq = perm_dpp<DPP_WAVE_SHL1>(Lp[n][0]);
             lm[n] = eL ? EDGE : pm;
             lq[n] = eR ? EDGE : pq;
         } else {

@@ -8,6 +8,9 @@
 
 #include "sm_sweep.hpp"
 #include "sm_sweep_host.hpp"
+#ifndef SWEEP_WIDE
+#define SWEEP_WIDE 0
+#endif
 #ifndef SM_ABLATIONS
 #define SM_ABLATIONS 0
 #endif
@@ -44,7 +47,15 @@ hipError_t with_d(int D, F& f)
 #else
         SW16(128)
 #endif
-        SW16(144) SW16(160) SW16(176) SW16(192) SW16(208) SW16(224) SW16(240) SW16(256)
+        SW16(144) SW16(160) SW16(176) SW16(192) SW16(208) SW16(224) SW16(240)
+#if SWEEP_WIDE
+        // the wide D = 256 instance: 32-lane lines for u8 costs (wide_ncw), none for u16
+    case 256:
+        if constexpr (sizeof(CT) == 1) return f.template run<32, 8, CT, MODE>();
+        else return f.template run<16, 16, CT, MODE>();
+#else
+        SW16(256)
+#endif
 #undef SW8
 #undef SW16
     default: return hipErrorInvalidValue;
@@ -52,10 +63,6 @@ hipError_t with_d(int D, F& f)
 }
 
 namespace {
-
-#ifndef SWEEP_WIDE
-#define SWEEP_WIDE 0
-#endif
 
 // compute waves of this unit's instance for (D, CT); 0 = not built here
 template <int D, typename CT>
@@ -93,6 +100,7 @@ struct InfoF {
             out->threads = SG::THREADS;
             out->blocks_per_cu = per_cu;
             out->impl = SWEEP_WIDE ? 1 : 0;
+            out->dpl = DPL;
             return hipSuccess;
         }
     }
@@ -140,6 +148,7 @@ hipError_t sweep2_run(bool info, int device, SweepInfo* out, const SweepArgs* a,
         out->threads = SG::THREADS;
         out->blocks_per_cu = per_cu;
         out->impl = NW;
+        out->dpl = 128 / 64;
         return hipSuccess;
     }
     hipLaunchKernelGGL(kern, dim3(a->nwg, npairs), dim3(SG::THREADS), 0, stream, *a);

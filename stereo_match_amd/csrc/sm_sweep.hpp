@@ -138,7 +138,8 @@ struct SweepGeo {
     static constexpr int SNG = NDAT + HW;           // granules per record
     // rows of inputs in flight per lane (a divisor of HB: the ring slot is the row's index in
     // its block); 2 where the wide strips' register budget needs it (12 waves, <= 168 VGPRs)
-    static constexpr int PF = (DPL >= 10 && NCW_ >= 11) ? 2 : 4;
+    // (32-lane lines: 2, so the 16-wave D = 256 instance stays within 128 VGPRs)
+    static constexpr int PF = ((DPL >= 10 && NCW_ >= 11) || VL == 32) ? 2 : 4;
     static_assert(NCW - 2 >= 2 * HM, "the snapshot's own waves of the two sides are distinct");
     static_assert(HB % PF == 0, "the input ring is indexed by the row within a block");
 };
@@ -150,6 +151,12 @@ struct SweepGeo {
 // occupancy before it picks a wide instance, sm_sweep.hip)
 constexpr int wide_ncw(int D, int ct_bytes)
 {
+    // D = 256 (u8): 32-lane lines (8 disparities per lane, as KITTI's 16-lane D = 128 lines)
+    // in 16-wave workgroups of 13 own waves x 2 columns.  The 16-lane D = 256 instance needs
+    // 183 / 219 VGPRs (modes 0 / 2): two waves per SIMD, one 8-wave strip per CU, and at
+    // Middlebury width (2624 columns, 132 narrow strips) one pair per launch; this one fits
+    // 4 waves per SIMD and 101 strips, i.e. two pairs per launch
+    if (ct_bytes == 1 && D == 256) return 15;
     if (ct_bytes == 1) return (D <= 96 || D == 128 || D == 160 || D == 192) ? 11 : 0;
     if (D == 16 || D == 32 || D == 96) return 13;
     return (D == 48 || D == 80 || D == 128 || D == 160) ? 11 : 0;
@@ -661,10 +668,13 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
                             mB[h] = lmin[rb][1][ch + 2];
                         }
                     }
-                    // the LDS reads leave before the V step (which does not need them), so their
-                    // latency overlaps V instead of adding to the row hand-off chain (the
-                    // scheduler otherwise issued V first)
-                    if constexpr (SWEEP_LDS_FIRST) __builtin_amdgcn_sched_barrier(0);
+                    // 5-path sweep (row barriers): the LDS reads leave before the V step (which
+                    // does not need them), so their latency overlaps V instead of adding to the
+                    // row chain (the scheduler otherwise issued V first).  Measured on one box:
+                    // sgbm5 4991 -> 5041-5068 pairs/s; the counter-synchronised sweeps (modes 0
+                    // and 2) were slower with it (census8 6193 -> 6081-6088), so they keep the
+                    // compiler's order
+                    if constexpr (SWEEP_LDS_FIRST && MODE == 1) __builtin_amdgcn_sched_barrier(0);
                     uint32_t nV[NP], nA[NS][NP], nB[NS][NP], mnV = 0, mnA[NS], mnB[NS];
                     auto step = [&](const uint32_t(&Lp)[NP], uint32_t m, const uint32_t(&Ch)[NP], uint32_t(&Ln)[NP]) {
                         return sweep_step2<VL, NP, H16>(Lp, m, Ch, P1p, P2p, eL, eR, Ln);

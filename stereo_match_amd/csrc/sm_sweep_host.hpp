@@ -41,6 +41,7 @@ struct SweepInfo {
     int threads;        // threads per workgroup
     int blocks_per_cu;  // occupancy API answer for that block size
     int impl;           // kernel: 0 k_sweep narrow strips, 1 k_sweep wide strips, 3 / 6 k_sweep2
+    int dpl;            // disparities per lane (the per-wave work of a row scales with it)
 };
 
 template <typename CT, int MODE, class F>

@@ -122,6 +122,23 @@ def _random_case(eng, c):
     assert np.array_equal(out, expected), f"{np.sum(out != expected)} px differ"
 
 
+@pytest.mark.parametrize("mode", [8, 5])
+@pytest.mark.parametrize("H,W,minD", [(37, 257, 0), (52, 300, 0), (29, 334, -7), (64, 700, 3), (9, 1200, 0)])
+def test_d256_wide_strips_32_lane_lines(eng, H, W, minD, mode):
+    """Census D = 256 on the wide sweep instance (32-lane lines across two DPP rows, 16-wave
+    workgroups of 2-column waves; flags 16384 | 1 << 21): ragged strips, one to several
+    dozen strips, both sweep modes of the census cost (8 paths: modes 0 + 2; 5: mode 1)."""
+    left, right, _ = synthetic.random_dot_pair(H, W, 256, seed=H * 1000 + W)
+    p = dict(synthetic.headline_params(256), minDisparity=minD, mode=mode)
+    eng.set_debug_flags(16384 | (1 << 21))
+    try:
+        out = run(eng, left, right, p)
+    finally:
+        eng.set_debug_flags(0)
+    exp = ref_c.compute(left, right, p)
+    assert np.array_equal(out, exp), f"{np.sum(out != exp)} px differ"
+
+
 @pytest.mark.parametrize("bs,D,minD", [(9, 16, 0), (11, 48, -5), (9, 144, 3), (11, 80, 0), (1, 256, 0), (3, 160, -20)])
 def test_sgbm_cost_block_sizes(eng, bs, D, minD):
     """The streaming SGBM cost kernel at every blockSize radius and odd /

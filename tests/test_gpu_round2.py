@@ -145,13 +145,36 @@ def test_tsukuba_config1(eng, kind, flags):
 
 @pytest.mark.slow
 def test_middlebury_full_frame_bit_exact(eng):
-    """BASELINE config 3 (2880x1988, D=256, census + 8 paths) on the whole frame."""
+    """BASELINE config 3 (2880x1988, D=256, census + 8 paths) on the whole frame: the
+    default engine (one pair: per-direction), the fused sweeps forced (16384: the wide D = 256
+    instance with 32-lane lines, sm_sweep.hpp wide_ncw), and two pairs in one device batch
+    (the default engine there: the sweeps, two pairs per launch)."""
+    import torch
+
     H, W, D = synthetic.CONFIGS["middlebury"]
     left, right, _ = synthetic.random_dot_pair(H, W, D, seed=9)
     p = synthetic.headline_params(D)
-    out = _run(eng, left, right, p)
     exp = ref_c.compute(left, right, p)
-    assert np.array_equal(out, exp), f"{np.sum(out != exp)} px differ"
+    out = _run(eng, left, right, p)
+    assert np.array_equal(out, exp), f"default: {np.sum(out != exp)} px differ"
+    eng.set_debug_flags(16384)
+    try:
+        out = _run(eng, left, right, p)
+    finally:
+        eng.set_debug_flags(0)
+    assert np.array_equal(out, exp), f"sweeps: {np.sum(out != exp)} px differ"
+    # a two-pair batch of the same pair (a second oracle run would cost another full C run)
+    L = torch.tensor(np.stack([left, left]), device="cuda")
+    R = torch.tensor(np.stack([right, right]), device="cuda")
+    o = torch.empty((2, H, W), dtype=torch.int16, device="cuda")
+    eng.set_stream(torch.cuda.current_stream().cuda_stream)
+    try:
+        eng.compute_batch_device(L.data_ptr(), R.data_ptr(), 2, H * W, H, W, W, synthetic.to_sm_params(p),
+                                 o.data_ptr())
+        got = o.cpu().numpy()
+    finally:
+        eng.set_stream(None)
+    assert np.array_equal(got[0], exp) and np.array_equal(got[1], exp)
 
 
 def test_compute_disparity_settings_ini_full_kitti():
