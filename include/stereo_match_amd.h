@@ -320,7 +320,8 @@ long long sm_debug_fetch(sm_ctx* ctx, int what, void* host, size_t bytes);
  *   16384    the fused sweeps wherever their preconditions hold (by default launch
  *            groups below 7 census / 3 other pairs run per-direction);
  *   8192     one pair per fused-sweep launch;  1 << 19 narrow sweep strips only;
- *   1 << 21  wide sweep strips wherever built;  256 the other E/W kernel of the sweeps;
+ *   1 << 21  wide sweep strips wherever built;  256 the sweeps' E/W volumes from the
+ *            per-direction engine's row lines;
  *   1 << 23  flag every sweep group as given up (the guarded fallback recomputes it);
  *   64       WTA + median on a second stream, overlapped with the next launch group;
  *   8, 512   16-lane vertical / 64-lane horizontal lines in the per-direction engine;
@@ -334,6 +335,19 @@ long long sm_debug_fetch(sm_ctx* ctx, int what, void* host, size_t bytes);
  * 1 << 28, 1 << 29, 1 << 31) exist only in the ablation build (make ablation ->
  * libstereo_match_amd_ablate.so); this library returns SM_E_UNSUPPORTED for them. */
 int sm_set_debug_flags(sm_ctx* ctx, int flags);
+
+/* Launch-shape knobs for measurements (every value gives the same disparities):
+ *   SM_TUNE_EW_LANES   lanes per line of the fused-sweep engine's E/W kernel:
+ *                      0 automatic (by pairs per launch group), 8 / 16 / 32 the packed
+ *                      line kernel with that many lanes (where built for D), -1 the
+ *                      per-direction engine's 16-lane row lines;
+ *   SM_TUNE_SWEEP_NCW  compute waves per fused-sweep strip: 0 automatic (modelled per
+ *                      launch), else 5 (latency strips), 7 (narrow) or the wide
+ *                      instance's count where built; unbuilt counts fail the call.
+ * Returns SM_E_ARG for an unknown key or value. */
+#define SM_TUNE_EW_LANES 1
+#define SM_TUNE_SWEEP_NCW 2
+int sm_set_tuning(sm_ctx* ctx, int key, int value);
 
 /* Last error text of ctx (or of the calling thread when ctx == NULL). */
 const char* sm_last_error(sm_ctx* ctx);

@@ -126,6 +126,7 @@ _SIGS = {
                                  _c.POINTER(_c.c_longlong)]),
     "sm_reset_timing": (_c.c_int, [_c.c_void_p]),
     "sm_set_debug_flags": (_c.c_int, [_c.c_void_p, _c.c_int]),
+    "sm_set_tuning": (_c.c_int, [_c.c_void_p, _c.c_int, _c.c_int]),
     "sm_debug_fetch": (_c.c_longlong, [_c.c_void_p, _c.c_int, _c.c_void_p, _c.c_size_t]),
     "sm_last_error": (_c.c_char_p, [_c.c_void_p]),
 }
@@ -458,6 +459,12 @@ class Engine:
     def set_debug_flags(self, flags: int):
         """Timing ablations only (results become wrong); 0 = normal."""
         self._check(self._lib.sm_set_debug_flags(self.ctx, int(flags)))
+
+    TUNE_EW_LANES, TUNE_SWEEP_NCW = 1, 2
+
+    def set_tuning(self, key: int, value: int):
+        """Launch-shape knob (include/stereo_match_amd.h sm_set_tuning); 0 = automatic."""
+        self._check(self._lib.sm_set_tuning(self.ctx, int(key), int(value)))
 
     def debug_fetch(self, what: int) -> bytes:
         n = self._lib.sm_debug_fetch(self.ctx, what, None, 0)

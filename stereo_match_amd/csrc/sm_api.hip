@@ -85,9 +85,8 @@ struct BufSet {
 
 // debug flags (sm_set_debug_flags); 1 skip horizontal, 2 skip vertical and 4 drop stores are read in-kernel
 constexpr int DBG_VL16 = 8, DBG_STORE_W = 16, DBG_ROW = 32, DBG_OVERLAP = 64, DBG_H64 = 512, DBG_NO_C8 = 1024;
-// 256: the sweep engine's E/W volumes from the other E/W kernel (u8 costs: the
-// per-direction engine's row lines instead of the packed k_ew; u16: k_ew instead of the
-// row lines); 128 and 1 << 27: the fused sweeps on k_sweep2 (see sweep_variant)
+// 256: the sweep engine's E/W volumes from the per-direction engine's row lines instead of
+// the packed k_ew (ew_lanes); 128 and 1 << 27: the fused sweeps on k_sweep2 (see sweep_variant)
 constexpr int DBG_OLD_EW = 256, DBG_SWEEP_V2 = 128, DBG_SWEEP2_NW = 1 << 27;
 // WLS smoother timing ablations (results wrong): 1 << 28 skips the FGS sweeps, 1 << 29 its
 // global loads/stores
@@ -151,6 +150,8 @@ struct sm_ctx {
     size_t last_L_pair = 0;
     uint32_t timing = 0;  // stages timed (bit = SM_STAGE_*), sm_set_timing
     int dbg_flags = 0;
+    // sm_set_tuning knobs (0 = automatic)
+    int tune_ew_lanes = 0, tune_sweep_ncw = 0;
     std::vector<TimedEvent> pending;
     std::vector<hipEvent_t> free_events;
     double stage_ms[SM_NUM_STAGES] = {0};
@@ -769,17 +770,35 @@ double sweep_model(const SweepFit& f, int G)
     return (double)launches * per_cu * (f.si.threads / 64 - 1) * std::max(f.si.dpl, 1);
 }
 
-// the kernel variant for one pass over G pairs (G = 0: any that fits, wide strips first)
+// the kernel variant for one pass over G pairs (G = 0: any that fits, wide strips first).
+// Candidates: wide strips (where built), narrow strips (kNarrowNcw compute waves) and the
+// latency strips (kLatNcw: more, narrower strips for launches of one or two pairs); the
+// smallest modelled issue time wins.  SM_TUNE_SWEEP_NCW forces the instance with that many
+// compute waves.
 bool sweep_capacity(sm_ctx* ctx, const Norm& n, int mode, int G, SweepFit& f)
 {
+    if (ctx->tune_sweep_ncw && sweep_variant(ctx) <= 1) {
+        for (int v : {0, 1, 2}) {
+            SweepFit t;
+            if (sweep_fit_variant(ctx, n, mode, v, t) && t.si.threads / 64 - 1 == ctx->tune_sweep_ncw) {
+                f = t;
+                return true;
+            }
+        }
+        return false;
+    }
     const int variant = sweep_variant(ctx);
     if (!sweep_fit_variant(ctx, n, mode, variant, f)) {
         // wide strips that do not fit: the narrow ones may
-        return variant == 0 && f.si.impl == 1 && sweep_fit_variant(ctx, n, mode, 1, f);
+        if (!(variant == 0 && f.si.impl == 1 && sweep_fit_variant(ctx, n, mode, 1, f))) return false;
+    } else if (variant == 0 && f.si.impl == 1 && G > 0 && !(ctx->dbg_flags & DBG_WIDE_SWEEPS)) {
+        SweepFit nf;
+        if (sweep_fit_variant(ctx, n, mode, 1, nf) && sweep_model(nf, G) < sweep_model(f, G)) f = nf;
     }
-    if (variant != 0 || f.si.impl != 1 || G <= 0 || (ctx->dbg_flags & DBG_WIDE_SWEEPS)) return true;
-    SweepFit nf;
-    if (sweep_fit_variant(ctx, n, mode, 1, nf) && sweep_model(nf, G) < sweep_model(f, G)) f = nf;
+    if (variant == 0 && G > 0 && !(ctx->dbg_flags & DBG_WIDE_SWEEPS)) {
+        SweepFit lf;
+        if (sweep_fit_variant(ctx, n, mode, 2, lf) && sweep_model(lf, G) < sweep_model(f, G)) f = lf;
+    }
     return true;
 }
 
@@ -872,15 +891,28 @@ struct StreamSwap {
     ~StreamSwap() { c->stream = old; }
 };
 
+// lanes per line of the sweep engine's E/W kernel (-1: the per-direction engine's row lines,
+// also forced by flag 256).  u8 costs (8 KITTI pairs, beside the down sweep): the packed
+// 8-lane lines, 114 vs 122 us per pair for the row lines (4 and 16 lanes no faster)
+int ew_lanes(const sm_ctx* ctx, const Norm& n)
+{
+    if (ctx->tune_ew_lanes) return ctx->tune_ew_lanes;
+    if (ctx->dbg_flags & DBG_OLD_EW) return -1;  // flag 256: the row lines
+    if (elem_bytes(n) == 1) return 0;
+    // u16 costs (round 4, tools/lr_probe.py): the packed lines with more lanes per line beat
+    // the row lines at every pair count measured: KITTI D = 128, 32 lanes, 1 / 2 / 8 pairs
+    // 168 -> 120 / 262 -> 205 / 708 -> 655 us per launch; D = 160, 16 lanes, 1 / 2 / 4 pairs
+    // 208 -> 204 / 422 -> 408 / 534 -> 520
+    return n.D % 64 == 0 ? 32 : n.D % 32 == 0 ? 16 : -1;
+}
+
 // E and W path volumes of the sweep engine (slots 0, 1 of bs.L): the packed
 // horizontal-line kernel (sm_ew.hpp), or the per-direction engine's row lines
-// (ablation flag 256)
 int launch_ew(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs)
 {
     const size_t et = elem_bytes(n);
-    // measured (8 KITTI pairs): u8 costs 114 vs 122 us per pair beside the down sweep;
-    // u16 costs (alone) 103 vs 92, the row lines stay
-    if ((et == 1) == ((ctx->dbg_flags & DBG_OLD_EW) != 0)) return dispatch(ctx, n, g, bs, DISPATCH_HORIZONTAL);
+    const int vl = ew_lanes(ctx, n);
+    if (vl < 0) return dispatch(ctx, n, g, bs, DISPATCH_HORIZONTAL);
     smk::EwArgs a{};
     a.cost = (const uint8_t*)bs.cost.p;
     a.cost_pair = g.vol * et;
@@ -892,7 +924,7 @@ int launch_ew(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs)
     a.P1 = n.P1;
     a.P2 = n.P2;
     StageTimer t(ctx, ctx->stream, SM_STAGE_HORIZONTAL, g.G);
-    const hipError_t e = smk::ew_launch(n.D, (int)et, 0, a, g.G, ctx->stream);
+    const hipError_t e = smk::ew_launch(n.D, (int)et, vl, a, g.G, ctx->stream);
     if (e == hipErrorInvalidValue) return fail(ctx, SM_E_UNSUPPORTED, "E/W lines: numDisparities %d not built", n.D);
     HIP_TRY(ctx, e);
     return SM_OK;
@@ -1497,6 +1529,9 @@ int run_pairs(sm_ctx* ctx, const Src& src, int npairs, int H, int W, int stride,
     g.slot_bytes = (g.vol * elem_bytes(n) + 255) & ~size_t(255);
     g.hybrid = !n.wide && use_hybrid(ctx, n, H) && sweeps_fit(ctx, n, true);
     g.sweep = !n.wide && !g.hybrid && use_sweep(ctx, n, H) && sweeps_fit(ctx, n, false);
+    if (ctx->tune_sweep_ncw && !n.wide && !g.hybrid && !g.sweep && use_sweep(ctx, n, H))
+        return fail(ctx, SM_E_UNSUPPORTED, "no fused-sweep instance with %d compute waves fits (D %d)",
+                    ctx->tune_sweep_ncw, n.D);
     // sweep engine: E and W volumes in slots 0/1 plus room for every direction's volume
     // (written only by the guarded fallback); hybrid: E, W (+ NE, N, NW at 8 paths)
     g.L_pair = g.slot_bytes * (g.hybrid ? hybrid_slots(n) : n.ndirs);
@@ -2327,6 +2362,8 @@ int sm_compute_disparity_batch_device(sm_ctx* ctx, const uint8_t* dL, const uint
         if ((rc = sm_create(ctx->device, &ctx->twin)) != SM_OK) return fail(ctx, rc, "%s", g_thread_error.c_str());
         ctx->twin->timing = ctx->timing;
         ctx->twin->dbg_flags = ctx->dbg_flags;
+        ctx->twin->tune_ew_lanes = ctx->tune_ew_lanes;
+        ctx->twin->tune_sweep_ncw = ctx->tune_sweep_ncw;
         if (!ctx->cu_mask.empty() &&
             (rc = sm_set_cu_mask(ctx->twin, ctx->cu_mask.data(), (int)ctx->cu_mask.size())) != SM_OK)
             return fail(ctx, rc, "%s", ctx->twin->err.c_str());
@@ -2721,6 +2758,25 @@ int sm_set_debug_flags(sm_ctx* ctx, int flags)
                     (unsigned)(flags & kAblationFlags));
     if (ctx->twin) sm_set_debug_flags(ctx->twin, flags);
     ctx->dbg_flags = flags;
+    return SM_OK;
+}
+
+int sm_set_tuning(sm_ctx* ctx, int key, int value)
+{
+    if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
+    switch (key) {
+    case SM_TUNE_EW_LANES:
+        if (value != 0 && value != -1 && value != 8 && value != 16 && value != 32)
+            return fail(ctx, SM_E_ARG, "E/W lanes %d: 0, -1, 8, 16 or 32", value);
+        ctx->tune_ew_lanes = value;
+        break;
+    case SM_TUNE_SWEEP_NCW:
+        if (value < 0) return fail(ctx, SM_E_ARG, "sweep compute waves %d < 0", value);
+        ctx->tune_sweep_ncw = value;
+        break;
+    default: return fail(ctx, SM_E_ARG, "unknown tuning key %d", key);
+    }
+    if (ctx->twin) sm_set_tuning(ctx->twin, key, value);
     return SM_OK;
 }
 

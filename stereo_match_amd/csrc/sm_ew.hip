@@ -21,7 +21,26 @@ template <typename CT>
 hipError_t ew_d(int D, int vl, const EwArgs& a, int npairs, hipStream_t stream)
 {
     if (D == 128 && vl == 4) return run_ew<4, 16, CT>(a, npairs, stream);
-    if (D == 128 && vl == 16) return run_ew<16, 4, CT>(a, npairs, stream);
+    // latency forms for a few pairs per launch (more lanes per line: less work per lane and
+    // step on the serial chain): 16-lane lines for D % 32 == 0, 32-lane lines for D % 64 == 0
+    if (vl == 16) {
+        switch (D) {
+#define EW16(d) \
+    case d: return run_ew<16, d / 32, CT>(a, npairs, stream);
+            EW16(32) EW16(64) EW16(96) EW16(128) EW16(160) EW16(192) EW16(224) EW16(256)
+#undef EW16
+        default: return hipErrorInvalidValue;
+        }
+    }
+    if (vl == 32) {
+        switch (D) {
+        case 64: return run_ew<32, 1, CT>(a, npairs, stream);
+        case 128: return run_ew<32, 2, CT>(a, npairs, stream);
+        case 192: return run_ew<32, 3, CT>(a, npairs, stream);
+        case 256: return run_ew<32, 4, CT>(a, npairs, stream);
+        default: return hipErrorInvalidValue;
+        }
+    }
     if (vl != 0 && vl != 8) return hipErrorInvalidValue;
     switch (D) {  // 8-lane lines, D / 16 u16 pairs per lane
 #define EW8(d) \

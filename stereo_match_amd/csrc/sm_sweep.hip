@@ -48,7 +48,7 @@ hipError_t with_d(int D, F& f)
         SW16(128)
 #endif
         SW16(144) SW16(160) SW16(176) SW16(192) SW16(208) SW16(224) SW16(240)
-#if SWEEP_WIDE
+#if SWEEP_WIDE == 1
         // the wide D = 256 instance: 32-lane lines for u8 costs (wide_ncw), none for u16
     case 256:
         if constexpr (sizeof(CT) == 1) return f.template run<32, 8, CT, MODE>();
@@ -68,6 +68,7 @@ namespace {
 template <int D, typename CT>
 constexpr int unit_ncw()
 {
+    if constexpr (SWEEP_WIDE == 2) return lat_built(D) ? kLatNcw : 0;
     return SWEEP_WIDE ? wide_ncw(D, (int)sizeof(CT)) : kNarrowNcw;
 }
 
@@ -99,7 +100,7 @@ struct InfoF {
             out->ngr = SG::SNG;
             out->threads = SG::THREADS;
             out->blocks_per_cu = per_cu;
-            out->impl = SWEEP_WIDE ? 1 : 0;
+            out->impl = SWEEP_WIDE == 2 ? 2 : SWEEP_WIDE ? 1 : 0;
             out->dpl = DPL;
             return hipSuccess;
         }
@@ -181,7 +182,20 @@ hipError_t sweep2(int D, int ct_bytes, int variant, bool info, int device, Sweep
 #define SW_CAT2(a, b) a##b
 #define SW_CAT(a, b) SW_CAT2(a, b)
 
-#if SWEEP_WIDE
+#if SWEEP_WIDE == 2
+hipError_t SW_CAT(sweep_info_lat_m, SWEEP_MODE)(int D, int ct_bytes, int device, SweepInfo* out)
+{
+    InfoF f{device, out};
+    return with_sweep(D, ct_bytes, f);
+}
+
+hipError_t SW_CAT(sweep_launch_lat_m, SWEEP_MODE)(int D, int ct_bytes, const SweepArgs& a, int npairs,
+                                                  hipStream_t stream)
+{
+    LaunchF f{&a, dim3(a.nwg, npairs), stream};
+    return with_sweep(D, ct_bytes, f);
+}
+#elif SWEEP_WIDE
 hipError_t SW_CAT(sweep_info_wide_m, SWEEP_MODE)(int D, int ct_bytes, int device, SweepInfo* out)
 {
     InfoF f{device, out};

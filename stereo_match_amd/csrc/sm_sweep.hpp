@@ -110,6 +110,13 @@ constexpr uint32_t SW_SPIN_LIMIT = 1u << 19;
 // census8 sweeps 244 -> 217 us per pair at NCW 7 -> 11, sgbm5 247 -> 235, sgbm8 321 -> 287
 // at NCW 13 (u16 costs); 9, 12, 14 and 15 are slower (the strip count against 256 CUs).
 constexpr int kNarrowNcw = 7;
+// latency instances (a launch of one or two pairs, or a pair on half the CUs: DESIGN.md §4.3):
+// 3 own waves and single-set halos, so a KITTI pair's strips spread over ~90 CUs at D = 160
+#ifndef SWEEP_LAT_NCW
+#define SWEEP_LAT_NCW 5
+#endif
+constexpr int kLatNcw = SWEEP_LAT_NCW;
+constexpr bool lat_built(int D) { return D % 32 == 0 && D >= 64 && D <= 224; }  // D = 256 spills
 // HM: column sets per halo wave in the packed row loops.  A halo of HM*LPW columns stays
 // exact for HM*LPW rows after a snapshot, so the strips hand off once per HM*LPW rows; the
 // hand-off latency (us under the sweeps' streaming traffic, SWEEP_STATS) is paid half as
@@ -120,7 +127,9 @@ constexpr int kNarrowNcw = 7;
 template <int VL, int DPL, int NCW_ = kNarrowNcw>
 struct SweepGeo {
     static constexpr int LPW = 64 / VL;             // columns per wave (per column set)
-    static constexpr int HM = (DPL % 2 == 0 && !SWEEP_U32) ? SWEEP_HM : 1;  // column sets per halo wave
+    // column sets per halo wave (1 where fewer than 2 * SWEEP_HM own waves would publish the two
+    // sides' snapshots: the latency instances' 2-3 own waves)
+    static constexpr int HM = (DPL % 2 == 0 && !SWEEP_U32 && NCW_ >= 2 + 2 * SWEEP_HM) ? SWEEP_HM : 1;
     static constexpr int NCW = NCW_;                // compute waves: left halo, NCW-2 own, right halo
     static constexpr int THREADS = (NCW + 1) * 64;  // + the poller wave
     static constexpr int HW = HM * LPW;             // halo columns per side

@@ -40,7 +40,7 @@ struct SweepInfo {
     int ngr;            // halo granules per (strip, direction, block)
     int threads;        // threads per workgroup
     int blocks_per_cu;  // occupancy API answer for that block size
-    int impl;           // kernel: 0 k_sweep narrow strips, 1 k_sweep wide strips, 3 / 6 k_sweep2
+    int impl;           // kernel: 0 k_sweep narrow strips, 1 wide strips, 2 latency strips, 3 / 6 k_sweep2
     int dpl;            // disparities per lane (the per-wave work of a row scales with it)
 };
 
@@ -58,6 +58,12 @@ hipError_t sweep_info_m2(int D, int ct_bytes, int variant, int device, SweepInfo
 hipError_t sweep_info_wide_m0(int D, int ct_bytes, int device, SweepInfo* out);
 hipError_t sweep_info_wide_m1(int D, int ct_bytes, int device, SweepInfo* out);
 hipError_t sweep_info_wide_m2(int D, int ct_bytes, int device, SweepInfo* out);
+hipError_t sweep_info_lat_m0(int D, int ct_bytes, int device, SweepInfo* out);
+hipError_t sweep_info_lat_m1(int D, int ct_bytes, int device, SweepInfo* out);
+hipError_t sweep_info_lat_m2(int D, int ct_bytes, int device, SweepInfo* out);
+hipError_t sweep_launch_lat_m0(int D, int ct_bytes, const SweepArgs& a, int npairs, hipStream_t stream);
+hipError_t sweep_launch_lat_m1(int D, int ct_bytes, const SweepArgs& a, int npairs, hipStream_t stream);
+hipError_t sweep_launch_lat_m2(int D, int ct_bytes, const SweepArgs& a, int npairs, hipStream_t stream);
 // grid (a.nwg, npairs), SweepInfo::threads threads
 hipError_t sweep_launch_m0(int D, int ct_bytes, int variant, const SweepArgs& a, int npairs, hipStream_t stream);
 hipError_t sweep_launch_m1(int D, int ct_bytes, int variant, const SweepArgs& a, int npairs, hipStream_t stream);
@@ -68,6 +74,10 @@ hipError_t sweep_launch_wide_m2(int D, int ct_bytes, const SweepArgs& a, int npa
 
 inline hipError_t sweep_info(int D, int ct_bytes, int mode, int variant, int device, SweepInfo* out)
 {
+    if (variant == 2)  // latency instances (kLatNcw compute waves)
+        return mode == 0 ? sweep_info_lat_m0(D, ct_bytes, device, out)
+             : mode == 1 ? sweep_info_lat_m1(D, ct_bytes, device, out)
+                         : sweep_info_lat_m2(D, ct_bytes, device, out);
     if (variant == 0) {
         const hipError_t e = mode == 0 ? sweep_info_wide_m0(D, ct_bytes, device, out)
                            : mode == 1 ? sweep_info_wide_m1(D, ct_bytes, device, out)
@@ -82,6 +92,10 @@ inline hipError_t sweep_info(int D, int ct_bytes, int mode, int variant, int dev
 inline hipError_t sweep_launch(int D, int ct_bytes, int mode, int impl, const SweepArgs& a, int npairs,
                                hipStream_t stream)
 {
+    if (impl == 2)
+        return mode == 0 ? sweep_launch_lat_m0(D, ct_bytes, a, npairs, stream)
+             : mode == 1 ? sweep_launch_lat_m1(D, ct_bytes, a, npairs, stream)
+                         : sweep_launch_lat_m2(D, ct_bytes, a, npairs, stream);
     if (impl == 1)
         return mode == 0 ? sweep_launch_wide_m0(D, ct_bytes, a, npairs, stream)
              : mode == 1 ? sweep_launch_wide_m1(D, ct_bytes, a, npairs, stream)

@@ -1,7 +1,9 @@
 """Single-pair latency of the reference surface (one pair per call, as
 stereo_vision.py:178-182 runs it): stage breakdown of sm_compute_disparity at
 settings.ini values (D=160) for each engine flag set.
-    python tools/single_pair.py [--flags 0,4096] [--calls 20]"""
+    python tools/single_pair.py [--flags 0,4096] [--calls 20] [--runs "0/ew=16;16384/ncw=5"]
+A run is debug flags, then /knob=value items (ew: SM_TUNE_EW_LANES, ncw: SM_TUNE_SWEEP_NCW);
+--runs replaces --flags."""
 import argparse
 import json
 import os
@@ -18,6 +20,7 @@ def main():
     ap.add_argument("--flags", default="0,4096")
     ap.add_argument("--calls", type=int, default=20)
     ap.add_argument("--D", type=int, default=160)
+    ap.add_argument("--runs", default="")
     args = ap.parse_args()
     import stereo_match_amd as sm
     from stereo_match_amd import _lib, synthetic, wls
@@ -34,8 +37,15 @@ def main():
     wp = wf.params(H, W)
     e = _lib.Engine(0)
     ref = None
-    for f in [int(x) for x in args.flags.split(",")]:
+    knobs = {"ew": e.TUNE_EW_LANES, "ncw": e.TUNE_SWEEP_NCW}
+    runs = args.runs.split(";") if args.runs else args.flags.split(",")
+    for run in runs:
+        parts = run.split("/")
+        f = int(parts[0])
+        tune = {k: int(v) for k, v in (p.split("=") for p in parts[1:])}
         e.set_debug_flags(f)
+        for k in knobs:
+            e.set_tuning(knobs[k], tune.get(k, 0))
         d, fl = e.compute_disparity(gl, gr, prm, wp)
         if ref is None:
             ref = (d, fl)
@@ -49,7 +59,7 @@ def main():
             ts.append(time.perf_counter() - t0)
         st = e.timing()
         e.set_timing(False)
-        print(json.dumps({"flags": f, "same_as_first": same, "ms_per_call": round(float(np.median(ts)) * 1e3, 3),
+        print(json.dumps({"run": run, "same_as_first": same, "ms_per_call": round(float(np.median(ts)) * 1e3, 3),
                           "stage_us_per_call": {k: round(v[0] * 1e3 / args.calls, 1) for k, v in st.items() if v[0] > 0}}))
 
 
