@@ -76,6 +76,9 @@ def parse():
     ap.add_argument("--engine", default="auto", choices=["auto", "perdir", "sweep"],
                     help="auto: the library's default per configuration; perdir / sweep force one engine "
                          "(DESIGN.md §4)")
+    ap.add_argument("--tune", default="",
+                    help="launch-shape knobs for A/B measurements, e.g. ew_waves=1,ew_lanes=16 "
+                         "(sm_set_tuning; every value gives the same disparities)")
     ap.add_argument("--cpu-baseline-pairs", type=int, default=8,
                     help="pairs timed on the host C port per thread (rank 0, N=1 only); 0 = skip")
     ap.add_argument("--cpu-threads", type=int, default=16,
@@ -246,6 +249,9 @@ class GpuWorkload:
         flags = {"auto": 0, "perdir": 4096, "sweep": 16384}[self.args.engine]
         if flags:
             self.eng.set_debug_flags(flags)
+        for kv in filter(None, self.args.tune.split(",")):
+            k, v = kv.split("=")
+            self.eng.set_tuning(getattr(self.eng, "TUNE_" + k.upper()), int(v))
 
     def step(self, out=None):
         """One engine call over the block into ``out`` ([P, H, W] int16 on this GPU; default
@@ -360,6 +366,7 @@ class GpuWorkload:
                                "volume8": "f32 cost volume (mc-cnn) + 8-path SGM",
                                "disparity5": "compute_disparity: left+right OpenCV-SGBM 5-path + WLS",
                                "bm": "OpenCV StereoBM blockSize 21 (X-Sobel prefilter)"}[args.mode],
+                **({"tune": args.tune} if args.tune else {}),
             },
             "mpix_disp_per_s": gpairs * K / elapsed * cells / 1e6,
             "roofline": {

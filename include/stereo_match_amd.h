@@ -344,9 +344,11 @@ int sm_set_debug_flags(sm_ctx* ctx, int flags);
  *   SM_TUNE_SWEEP_NCW  compute waves per fused-sweep strip: 0 automatic (modelled per
  *                      launch), else 5 (latency strips), 7 (narrow) or the wide
  *                      instance's count where built; unbuilt counts fail the call.
+ *   SM_TUNE_EW_WAVES   waves per workgroup of the packed E/W lines: 0 automatic, 1..4.
  * Returns SM_E_ARG for an unknown key or value. */
 #define SM_TUNE_EW_LANES 1
 #define SM_TUNE_SWEEP_NCW 2
+#define SM_TUNE_EW_WAVES 3
 int sm_set_tuning(sm_ctx* ctx, int key, int value);
 
 /* Last error text of ctx (or of the calling thread when ctx == NULL). */

@@ -151,7 +151,7 @@ struct sm_ctx {
     uint32_t timing = 0;  // stages timed (bit = SM_STAGE_*), sm_set_timing
     int dbg_flags = 0;
     // sm_set_tuning knobs (0 = automatic)
-    int tune_ew_lanes = 0, tune_sweep_ncw = 0;
+    int tune_ew_lanes = 0, tune_sweep_ncw = 0, tune_ew_waves = 0;
     std::vector<TimedEvent> pending;
     std::vector<hipEvent_t> free_events;
     double stage_ms[SM_NUM_STAGES] = {0};
@@ -898,12 +898,15 @@ int ew_lanes(const sm_ctx* ctx, const Norm& n)
 {
     if (ctx->tune_ew_lanes) return ctx->tune_ew_lanes;
     if (ctx->dbg_flags & DBG_OLD_EW) return -1;  // flag 256: the row lines
-    if (elem_bytes(n) == 1) return 0;
-    // u16 costs (round 4, tools/lr_probe.py): the packed lines with more lanes per line beat
-    // the row lines at every pair count measured: KITTI D = 128, 32 lanes, 1 / 2 / 8 pairs
-    // 168 -> 120 / 262 -> 205 / 708 -> 655 us per launch; D = 160, 16 lanes, 1 / 2 / 4 pairs
-    // 208 -> 204 / 422 -> 408 / 534 -> 520
-    return n.D % 64 == 0 ? 32 : n.D % 32 == 0 ? 16 : -1;
+    // round 4 (tools/lr_probe.py, bench.py --tune): more lanes per line.  u16 costs beat the
+    // row lines at every pair count measured: KITTI D = 128, 32 lanes, 1 / 2 / 8 pairs 168 ->
+    // 120 / 262 -> 205 / 708 -> 655 us per launch; D = 160, 16 lanes, 1 / 2 / 4 pairs 208 ->
+    // 204 / 422 -> 408 / 534 -> 520.  u8 costs beside the census down sweep (8 KITTI pairs, one
+    // box): 8 lanes 5978, 16 lanes 6126, 32 lanes 6163 pairs/s: the lines themselves take a
+    // little longer (74 vs 67 us per pair) but stretch the down sweep less (72 vs 78)
+    if (n.D % 64 == 0) return 32;
+    if (n.D % 32 == 0) return 16;
+    return elem_bytes(n) == 1 ? 0 : -1;
 }
 
 // E and W path volumes of the sweep engine (slots 0, 1 of bs.L): the packed
@@ -923,6 +926,7 @@ int launch_ew(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs)
     a.W1 = n.width1;
     a.P1 = n.P1;
     a.P2 = n.P2;
+    a.wpb = ctx->tune_ew_waves;
     StageTimer t(ctx, ctx->stream, SM_STAGE_HORIZONTAL, g.G);
     const hipError_t e = smk::ew_launch(n.D, (int)et, vl, a, g.G, ctx->stream);
     if (e == hipErrorInvalidValue) return fail(ctx, SM_E_UNSUPPORTED, "E/W lines: numDisparities %d not built", n.D);
@@ -2364,6 +2368,7 @@ int sm_compute_disparity_batch_device(sm_ctx* ctx, const uint8_t* dL, const uint
         ctx->twin->dbg_flags = ctx->dbg_flags;
         ctx->twin->tune_ew_lanes = ctx->tune_ew_lanes;
         ctx->twin->tune_sweep_ncw = ctx->tune_sweep_ncw;
+        ctx->twin->tune_ew_waves = ctx->tune_ew_waves;
         if (!ctx->cu_mask.empty() &&
             (rc = sm_set_cu_mask(ctx->twin, ctx->cu_mask.data(), (int)ctx->cu_mask.size())) != SM_OK)
             return fail(ctx, rc, "%s", ctx->twin->err.c_str());
@@ -2769,6 +2774,10 @@ int sm_set_tuning(sm_ctx* ctx, int key, int value)
         if (value != 0 && value != -1 && value != 8 && value != 16 && value != 32)
             return fail(ctx, SM_E_ARG, "E/W lanes %d: 0, -1, 8, 16 or 32", value);
         ctx->tune_ew_lanes = value;
+        break;
+    case SM_TUNE_EW_WAVES:
+        if (value < 0 || value > 4) return fail(ctx, SM_E_ARG, "E/W waves per workgroup %d: 0..4", value);
+        ctx->tune_ew_waves = value;
         break;
     case SM_TUNE_SWEEP_NCW:
         if (value < 0) return fail(ctx, SM_E_ARG, "sweep compute waves %d < 0", value);

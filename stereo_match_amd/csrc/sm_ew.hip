@@ -5,15 +5,20 @@ namespace smk {
 
 namespace {
 
-constexpr int ew_pf(int words) { return words >= 16 ? 4 : words >= 8 ? 8 : 16; }  // ring: <= 64 VGPRs
+// ring depth: <= 64 VGPRs.  u16 slices of <= 2 words take 32 slots (sgbm5, 8 KITTI pairs, 32-lane
+// lines: 5016 -> 5066 pairs/s); the u8 lines keep 16 (beside the census down sweep a deeper
+// ring made the lines slower and the total worse: 6185 -> 5670)
+template <typename CT>
+constexpr int ew_pf(int words) { return words >= 16 ? 4 : words >= 8 ? 8 : (sizeof(CT) == 2 && words <= 2) ? 32 : 16; }
 
 template <int VL, int NP, typename CT>
 hipError_t run_ew(EwArgs a, int npairs, hipStream_t stream)
 {
     constexpr int WORDS = RawBytes<2 * NP * (int)sizeof(CT)>::WORDS;
     constexpr int LPW = 64 / VL;
-    a.nrb = (a.H + 4 * LPW - 1) / (4 * LPW);
-    hipLaunchKernelGGL((k_ew<VL, NP, CT, CT, ew_pf(WORDS)>), dim3(2 * a.nrb, npairs), dim3(256), 0, stream, a);
+    if (a.wpb < 1 || a.wpb > 4) a.wpb = 4;
+    a.nrb = (a.H + a.wpb * LPW - 1) / (a.wpb * LPW);
+    hipLaunchKernelGGL((k_ew<VL, NP, CT, CT, ew_pf<CT>(WORDS)>), dim3(2 * a.nrb, npairs), dim3(64 * a.wpb), 0, stream, a);
     return hipGetLastError();
 }
 

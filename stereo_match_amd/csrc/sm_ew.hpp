@@ -50,7 +50,7 @@ __device__ __forceinline__ void store_pk(rsrc_t r, uint32_t off, const uint32_t 
     }
 }
 
-// grid (2 * a.nrb, pairs), 256 threads: workgroup b < nrb runs E lines, the rest W;
+// grid (2 * a.nrb, pairs), 64 * a.wpb threads: workgroup b < nrb runs E lines, the rest W;
 // each wave owns LPW = 64 / VL consecutive rows.
 template <int VL, int NP, typename CT, typename LT, int PF>
 __global__ void __launch_bounds__(256) k_ew(EwArgs a)
@@ -61,7 +61,7 @@ __global__ void __launch_bounds__(256) k_ew(EwArgs a)
     const int g = lane % VL, kl = lane / VL;
     const int dir = (int)blockIdx.x >= a.nrb ? 1 : 0;
     const int H = a.H, W1 = a.W1;
-    const int y0 = (((int)blockIdx.x - dir * a.nrb) * 4 + wave) * LPW;
+    const int y0 = (((int)blockIdx.x - dir * a.nrb) * a.wpb + wave) * LPW;
     if (y0 >= H) return;  // wave-uniform
     const bool line_ok = y0 + kl < H;
     const int y = min(y0 + kl, H - 1);

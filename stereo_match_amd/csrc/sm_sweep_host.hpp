@@ -117,6 +117,7 @@ struct EwArgs {
     size_t out_pair, out_slot;
     int H, W1, P1, P2;
     int nrb;  // workgroups per direction (filled by ew_launch)
+    int wpb;  // waves per workgroup, 1..4 (0: 4)
 };
 // lanes per line: vl = 4, 8 or 16 (0 = the default for D); hipErrorInvalidValue when
 // (D, ct_bytes, vl) is not built.  LT = CT (u8 census costs -> u8 volumes, u16 -> u16).
