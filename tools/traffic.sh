@@ -10,7 +10,7 @@ OUT=gpurun_out/traffic; mkdir -p $OUT
 CONFIG=${1:-kitti}; MODE=${2:-census8}
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc $C -d $OUT/$C -o run --output-format csv -- \
-      python bench.py --steps 3 --warmup 1 --cpu-baseline-pairs 0 --host-surface-calls 0 --config $CONFIG --mode $MODE > $OUT/$C.log 2>&1
+      python bench.py --steps 3 --warmup 1 --cpu-baseline-pairs 0 --host-surface-calls 0 --config $CONFIG --mode $MODE ${BENCH_EXTRA:-} > $OUT/$C.log 2>&1
   rc=$?; echo "$C rc=$rc"; if [ $rc -ne 0 ]; then tail -5 $OUT/$C.log; exit $rc; fi
 done
 python3 tools/traffic_summary.py $OUT $CONFIG $MODE
