@@ -345,10 +345,12 @@ int sm_set_debug_flags(sm_ctx* ctx, int flags);
  *                      launch), else 5 (latency strips), 7 (narrow) or the wide
  *                      instance's count where built; unbuilt counts fail the call.
  *   SM_TUNE_EW_WAVES   waves per workgroup of the packed E/W lines: 0 automatic, 1..4.
+ *   SM_TUNE_EW_PRIO    issue priority (s_setprio 0..3) of the packed E/W lines' waves.
  * Returns SM_E_ARG for an unknown key or value. */
 #define SM_TUNE_EW_LANES 1
 #define SM_TUNE_SWEEP_NCW 2
 #define SM_TUNE_EW_WAVES 3
+#define SM_TUNE_EW_PRIO 4
 int sm_set_tuning(sm_ctx* ctx, int key, int value);
 
 /* Last error text of ctx (or of the calling thread when ctx == NULL). */

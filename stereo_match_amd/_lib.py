@@ -460,7 +460,7 @@ class Engine:
         """Timing ablations only (results become wrong); 0 = normal."""
         self._check(self._lib.sm_set_debug_flags(self.ctx, int(flags)))
 
-    TUNE_EW_LANES, TUNE_SWEEP_NCW, TUNE_EW_WAVES = 1, 2, 3
+    TUNE_EW_LANES, TUNE_SWEEP_NCW, TUNE_EW_WAVES, TUNE_EW_PRIO = 1, 2, 3, 4
 
     def set_tuning(self, key: int, value: int):
         """Launch-shape knob (include/stereo_match_amd.h sm_set_tuning); 0 = automatic."""

@@ -139,6 +139,7 @@ struct sm_ctx {
     std::vector<uint32_t> cu_mask;  // sm_set_cu_mask words (applied to the twin too)
     uint32_t hop_epoch = 0;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;  // sweep engine: E/W kernel on the side stream
+    hipEvent_t ev_fb_fork = nullptr, ev_fb_join = nullptr;  // sweep engine: fallback beside the LR pass
     const uint32_t* fb_guard = nullptr;  // set while enqueuing a group's guarded per-direction fallback
     hipStream_t wta_override = nullptr;  // stream of the WTA launch when it is not stream_b()
     int16_t* wta_dst = nullptr;  // integer WTA index of the current launch group (sm_compute_wta_*), or null
@@ -151,7 +152,7 @@ struct sm_ctx {
     uint32_t timing = 0;  // stages timed (bit = SM_STAGE_*), sm_set_timing
     int dbg_flags = 0;
     // sm_set_tuning knobs (0 = automatic)
-    int tune_ew_lanes = 0, tune_sweep_ncw = 0, tune_ew_waves = 0;
+    int tune_ew_lanes = 0, tune_sweep_ncw = 0, tune_ew_waves = 0, tune_ew_prio = 0;
     std::vector<TimedEvent> pending;
     std::vector<hipEvent_t> free_events;
     double stage_ms[SM_NUM_STAGES] = {0};
@@ -927,6 +928,7 @@ int launch_ew(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs)
     a.P1 = n.P1;
     a.P2 = n.P2;
     a.wpb = ctx->tune_ew_waves;
+    a.prio = ctx->tune_ew_prio;
     StageTimer t(ctx, ctx->stream, SM_STAGE_HORIZONTAL, g.G);
     const hipError_t e = smk::ew_launch(n.D, (int)et, vl, a, g.G, ctx->stream);
     if (e == hipErrorInvalidValue) return fail(ctx, SM_E_UNSUPPORTED, "E/W lines: numDisparities %d not built", n.D);
@@ -990,12 +992,40 @@ int run_sweep(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs, hipStream_t 
     }
     StreamSwap sw(ctx, wta_stream);
     StageTimer t(ctx, ctx->stream, SM_STAGE_WTA, G);
-    {
-        StageTimer ts(ctx, ctx->stream, SM_STAGE_SWEEP_WTA, G);
-        if ((rc = sweep_pass(ctx, n, g, j, n.ndirs == 8 ? 2 : 1)) != SM_OK) return rc;
+    StageTimer ts(ctx, ctx->stream, SM_STAGE_SWEEP_WTA, G);
+    return sweep_pass(ctx, n, g, j, n.ndirs == 8 ? 2 : 1);
+}
+
+// after the WTA sweep (on stream ws): the LR pass into bs.raw and, unless flag 1 << 31, the
+// guarded per-direction fallback of the group.  The fallback (two launches that exit at once
+// while the group flag is clear) runs on a second stream beside the LR pass, which writes
+// nothing when the flag is set, so neither waits for the other's launch latency; ws joins
+// the second stream before the median reads bs.raw.
+int sweep_finish(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs, hipStream_t ws, uint32_t* gflag)
+{
+    const bool fb = !(ctx->dbg_flags & DBG_NO_FALLBACK);
+    int rc;
+    hipStream_t fs = ws == ctx->side ? ctx->stream : ctx->side;  // the stream the fallback runs on
+    if (fb) {
+        if (ctx->dbg_flags & DBG_FORCE_FALLBACK) HIP_TRY(ctx, hipMemsetAsync(gflag, 1, 1, ws));
+        if ((rc = ensure_event(ctx, ctx->ev_fb_fork)) != SM_OK) return rc;
+        if ((rc = ensure_event(ctx, ctx->ev_fb_join)) != SM_OK) return rc;
+        HIP_TRY(ctx, hipEventRecord(ctx->ev_fb_fork, ws));
+        HIP_TRY(ctx, hipStreamWaitEvent(fs, ctx->ev_fb_fork, 0));
+        StreamSwap sw(ctx, fs);
+        ctx->wta_override = fs;
+        ctx->fb_guard = gflag;
+        rc = dispatch(ctx, n, g, bs, DISPATCH_PATHS);
+        if (rc == SM_OK) rc = dispatch(ctx, n, g, bs, DISPATCH_WTA);
+        ctx->fb_guard = nullptr;
+        ctx->wta_override = nullptr;
+        if (rc != SM_OK) return rc;
+        HIP_TRY(ctx, hipEventRecord(ctx->ev_fb_join, fs));
     }
     HIP_TRY(ctx, smk::lr_rows_launch((const uint32_t*)bs.key2.p, (const uint32_t*)bs.pre.p, (int16_t*)bs.raw.p,
-                                     ctx->wta_dst, G, g.H, g.W, n.Dv, n.minD, n.minX1, n.maxX1, n.disp12, ctx->stream));
+                                     ctx->wta_dst, g.G, g.H, g.W, n.Dv, n.minD, n.minX1, n.maxX1, n.disp12,
+                                     fb ? gflag : nullptr, ws));
+    if (fb) HIP_TRY(ctx, hipStreamWaitEvent(ws, ctx->ev_fb_join, 0));
     return SM_OK;
 }
 
@@ -1487,19 +1517,9 @@ int run_group(sm_ctx* ctx, const Src& src, const Geo& g, const Norm& n, int16_t*
         // Strips of a sweep wait on their neighbours, so all of a launch's strips must be
         // resident together; the grid is sized for that (sweep_pass), but work on other
         // streams or processes can take the slots.  A strip that gives up raises the
-        // group flag, and this guarded per-direction launch pair (a small grid that exits
+        // group flag, and the guarded per-direction launch pair (a small grid that exits
         // at once while the flag is clear) then recomputes the whole group into bs.raw.
-        if (!(ctx->dbg_flags & DBG_NO_FALLBACK)) {
-            if (ctx->dbg_flags & DBG_FORCE_FALLBACK) HIP_TRY(ctx, hipMemsetAsync(gflag, 1, 1, ws));
-            StreamSwap sw(ctx, ws);
-            ctx->wta_override = ws;
-            ctx->fb_guard = gflag;
-            rc = dispatch(ctx, n, g, bs, DISPATCH_PATHS);
-            if (rc == SM_OK) rc = dispatch(ctx, n, g, bs, DISPATCH_WTA);
-            ctx->fb_guard = nullptr;
-            ctx->wta_override = nullptr;
-            if (rc != SM_OK) return rc;
-        }
+        if ((rc = sweep_finish(ctx, n, g, bs, ws, gflag)) != SM_OK) return rc;
     } else if (g.hybrid) {
         if ((rc = run_hybrid(ctx, n, g, bs)) != SM_OK) return rc;
     } else if ((rc = dispatch(ctx, n, g, bs, DISPATCH_PATHS)) != SM_OK) {
@@ -2088,6 +2108,8 @@ void sm_destroy(sm_ctx* ctx)
     if (ctx->ev_wls_ready) (void)hipEventDestroy(ctx->ev_wls_ready);
     if (ctx->wls_stream) (void)hipStreamDestroy(ctx->wls_stream);
     if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
+    if (ctx->ev_fb_fork) (void)hipEventDestroy(ctx->ev_fb_fork);
+    if (ctx->ev_fb_join) (void)hipEventDestroy(ctx->ev_fb_join);
     if (ctx->side) (void)hipStreamDestroy(ctx->side);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
     delete ctx;
@@ -2369,6 +2391,7 @@ int sm_compute_disparity_batch_device(sm_ctx* ctx, const uint8_t* dL, const uint
         ctx->twin->tune_ew_lanes = ctx->tune_ew_lanes;
         ctx->twin->tune_sweep_ncw = ctx->tune_sweep_ncw;
         ctx->twin->tune_ew_waves = ctx->tune_ew_waves;
+        ctx->twin->tune_ew_prio = ctx->tune_ew_prio;
         if (!ctx->cu_mask.empty() &&
             (rc = sm_set_cu_mask(ctx->twin, ctx->cu_mask.data(), (int)ctx->cu_mask.size())) != SM_OK)
             return fail(ctx, rc, "%s", ctx->twin->err.c_str());
@@ -2778,6 +2801,10 @@ int sm_set_tuning(sm_ctx* ctx, int key, int value)
     case SM_TUNE_EW_WAVES:
         if (value < 0 || value > 4) return fail(ctx, SM_E_ARG, "E/W waves per workgroup %d: 0..4", value);
         ctx->tune_ew_waves = value;
+        break;
+    case SM_TUNE_EW_PRIO:
+        if (value < 0 || value > 3) return fail(ctx, SM_E_ARG, "E/W issue priority %d: 0..3", value);
+        ctx->tune_ew_prio = value;
         break;
     case SM_TUNE_SWEEP_NCW:
         if (value < 0) return fail(ctx, SM_E_ARG, "sweep compute waves %d < 0", value);

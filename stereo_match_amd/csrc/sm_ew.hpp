@@ -57,6 +57,14 @@ __global__ void __launch_bounds__(256) k_ew(EwArgs a)
 {
     constexpr int LPW = 64 / VL, DPL = 2 * NP, D = VL * DPL;
     constexpr int CB = DPL * (int)sizeof(CT);  // cost bytes per lane and step
+    // issue priority against the down sweep's waves sharing the SIMDs (SM_TUNE_EW_PRIO; the
+    // sweep's hand-off chain runs at 3, its other work at 2)
+    switch (a.prio) {
+    case 1: __builtin_amdgcn_s_setprio(1); break;
+    case 2: __builtin_amdgcn_s_setprio(2); break;
+    case 3: __builtin_amdgcn_s_setprio(3); break;
+    default: break;
+    }
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int g = lane % VL, kl = lane / VL;
     const int dir = (int)blockIdx.x >= a.nrb ? 1 : 0;

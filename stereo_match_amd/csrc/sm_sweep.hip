@@ -239,10 +239,10 @@ hipError_t SW_CAT(sweep_launch_m, SWEEP_MODE)(int D, int ct_bytes, int variant, 
 
 #if SWEEP_MODE == 0 && !SWEEP_WIDE
 hipError_t lr_rows_launch(const uint32_t* rec, const uint32_t* nb, int16_t* out, int16_t* wta, int G, int H, int W,
-                          int D, int minD, int minX1, int maxX1, int disp12, hipStream_t stream)
+                          int D, int minD, int minX1, int maxX1, int disp12, const uint32_t* guard, hipStream_t stream)
 {
     hipLaunchKernelGGL(k_lr_rows, dim3(H, G), dim3(256), (size_t)W * 6 + 16, stream, rec, nb, out, wta, H, W, D, minD,
-                       minX1, maxX1, disp12);
+                       minX1, maxX1, disp12, guard);
     return hipGetLastError();
 }
 #endif

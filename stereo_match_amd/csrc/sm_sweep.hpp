@@ -1088,8 +1088,12 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
 // [minX1, maxX1)), before the sub-pixel step, the LR check and the median.
 __global__ void __launch_bounds__(256) k_lr_rows(const uint32_t* __restrict__ rec, const uint32_t* __restrict__ nbs,
                                                  int16_t* __restrict__ out, int16_t* __restrict__ wta, int H, int W,
-                                                 int D, int minD, int minX1, int maxX1, int disp12)
+                                                 int D, int minD, int minX1, int maxX1, int disp12,
+                                                 const uint32_t* guard)
 {
+    // a strip of the group gave up: the guarded per-direction fallback (running beside this
+    // kernel on another stream) writes the maps instead
+    if (guard && __hip_atomic_load(guard, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;
     extern __shared__ uint32_t key2[];
     int16_t* drow = reinterpret_cast<int16_t*>(key2 + W);
     const int y = blockIdx.x;

@@ -105,9 +105,10 @@ inline hipError_t sweep_launch(int D, int ct_bytes, int mode, int impl, const Sw
                      : sweep_launch_m2(D, ct_bytes, impl, a, npairs, stream);
 }
 // sub-pixel + disp2 + disp12MaxDiff check from the WTA sweep's records, one row per workgroup;
-// wta (may be null): the integer WTA index [pair][H][W] (-1: rejected / outside the domain)
+// wta (may be null): the integer WTA index [pair][H][W] (-1: rejected / outside the domain);
+// guard (may be null): the group's give-up flag, the kernel writes nothing when it is set
 hipError_t lr_rows_launch(const uint32_t* rec, const uint32_t* nb, int16_t* out, int16_t* wta, int G, int H, int W,
-                          int D, int minD, int minX1, int maxX1, int disp12, hipStream_t stream);
+                          int D, int minD, int minX1, int maxX1, int disp12, const uint32_t* guard, hipStream_t stream);
 
 // horizontal (E, W) path volumes, packed recurrence (sm_ew.hpp / sm_ew.hip)
 struct EwArgs {
@@ -118,6 +119,7 @@ struct EwArgs {
     int H, W1, P1, P2;
     int nrb;  // workgroups per direction (filled by ew_launch)
     int wpb;  // waves per workgroup, 1..4 (0: 4)
+    int prio;  // wave issue priority 0..3
 };
 // lanes per line: vl = 4, 8 or 16 (0 = the default for D); hipErrorInvalidValue when
 // (D, ct_bytes, vl) is not built.  LT = CT (u8 census costs -> u8 volumes, u16 -> u16).
