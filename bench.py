@@ -629,7 +629,11 @@ def design_kernels(args, stages, H, W, D, p, P_dirs, sweep, bm):
                 "wta": ("k_bm_sad (column sums in LDS + WTA)", H * W * (2 + 2 + 4))}, ("wta",)
     if sweep:
         rec_b = 8 * H * width1  # WTA winner record + sub-pixel inputs per pixel
-        kern = {"horizontal": ("k_ew (packed E/W lines)" if eb == 1 else "k_sgm_paths (E/W lines only)", 4 * vol * eb),
+        # E/W kernel (sm_api.hip ew_lanes): packed lines of 32 / 16 lanes where D % 64 / D % 32 == 0,
+        # else 8-lane packed lines (u8 costs) or the per-direction row lines (u16)
+        ew_lanes = 32 if D % 64 == 0 else 16 if D % 32 == 0 else 8 if eb == 1 else 0
+        ew = f"k_ew ({ew_lanes}-lane packed E/W lines)" if ew_lanes else "k_sgm_paths (E/W row lines only)"
+        kern = {"horizontal": (ew, 4 * vol * eb),
                 "sweep": ("k_sweep down (S+SE+SW -> u16 partial)", vol * eb + 2 * vol),
                 "sweep_wta": ("k_sweep " + ("up (N+NE+NW" if P_dirs == 8 else "down (S+SE+SW")
                               + " + E + W" + (" + partial" if P_dirs == 8 else "") + " + WTA)",
