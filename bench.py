@@ -76,6 +76,9 @@ def parse():
     ap.add_argument("--engine", default="auto", choices=["auto", "perdir", "sweep"],
                     help="auto: the library's default per configuration; perdir / sweep force one engine "
                          "(DESIGN.md §4)")
+    ap.add_argument("--debug-flags", type=int, default=0,
+                    help="sm_set_debug_flags value OR-ed into the engine flags (engine selection for A/B runs; "
+                         "ablation-only flags need STEREO_MATCH_AMD_LIB=.../libstereo_match_amd_ablate.so)")
     ap.add_argument("--tune", default="",
                     help="launch-shape knobs for A/B measurements, e.g. ew_waves=1,ew_lanes=16 "
                          "(sm_set_tuning; every value gives the same disparities)")
@@ -246,7 +249,7 @@ class GpuWorkload:
         self.eng = _lib.Engine(self.local_rank)
         self.stream = torch.cuda.current_stream(dev)
         self.eng.set_stream(self.stream.cuda_stream)
-        flags = {"auto": 0, "perdir": 4096, "sweep": 16384}[self.args.engine]
+        flags = {"auto": 0, "perdir": 4096, "sweep": 16384}[self.args.engine] | self.args.debug_flags
         if flags:
             self.eng.set_debug_flags(flags)
         for kv in filter(None, self.args.tune.split(",")):
