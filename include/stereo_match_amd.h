@@ -338,9 +338,9 @@ int sm_set_debug_flags(sm_ctx* ctx, int flags);
 
 /* Launch-shape knobs for measurements (every value gives the same disparities):
  *   SM_TUNE_EW_LANES   lanes per line of the fused-sweep engine's E/W kernel:
- *                      0 automatic (by pairs per launch group), 8 / 16 / 32 the packed
- *                      line kernel with that many lanes (where built for D), -1 the
- *                      per-direction engine's 16-lane row lines;
+ *                      0 automatic (32 where D % 64 == 0, 16 where D % 32 == 0), 8 / 16 /
+ *                      32 / 64 the packed line kernel with that many lanes (where built
+ *                      for D), -1 the per-direction engine's 16-lane row lines;
  *   SM_TUNE_SWEEP_NCW  compute waves per fused-sweep strip: 0 automatic (modelled per
  *                      launch), else 5 (latency strips), 7 (narrow) or the wide
  *                      instance's count where built; unbuilt counts fail the call.

@@ -2794,8 +2794,8 @@ int sm_set_tuning(sm_ctx* ctx, int key, int value)
     if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
     switch (key) {
     case SM_TUNE_EW_LANES:
-        if (value != 0 && value != -1 && value != 8 && value != 16 && value != 32)
-            return fail(ctx, SM_E_ARG, "E/W lanes %d: 0, -1, 8, 16 or 32", value);
+        if (value != 0 && value != -1 && value != 8 && value != 16 && value != 32 && value != 64)
+            return fail(ctx, SM_E_ARG, "E/W lanes %d: 0, -1, 8, 16, 32 or 64", value);
         ctx->tune_ew_lanes = value;
         break;
     case SM_TUNE_EW_WAVES:

@@ -37,6 +37,13 @@ hipError_t ew_d(int D, int vl, const EwArgs& a, int npairs, hipStream_t stream)
         default: return hipErrorInvalidValue;
         }
     }
+    if (vl == 64) {  // one line per wave (measurement instances, SM_TUNE_EW_LANES 64)
+        switch (D) {
+        case 128: return run_ew<64, 1, CT>(a, npairs, stream);
+        case 256: return run_ew<64, 2, CT>(a, npairs, stream);
+        default: return hipErrorInvalidValue;
+        }
+    }
     if (vl == 32) {
         switch (D) {
         case 64: return run_ew<32, 1, CT>(a, npairs, stream);

@@ -232,7 +232,7 @@ __device__ __forceinline__ uint32_t sweep_step2(const uint32_t (&Lp)[NP], uint32
 template <int N, int ND>
 __device__ __forceinline__ void group_min_n(uint32_t (&v)[ND])
 {
-    static_assert(N == 1 || N == 2 || N == 4 || N == 8 || N == 16 || N == 32, "lane group of 1-32 lanes");
+    static_assert(N == 1 || N == 2 || N == 4 || N == 8 || N == 16 || N == 32 || N == 64, "lane group of 1-64 lanes");
     if constexpr (N >= 2) {
 #pragma unroll
         for (int n = 0; n < ND; n++) v[n] = ::min(v[n], perm_dpp<DPP_QP_XOR1>(v[n]));
@@ -252,6 +252,13 @@ __device__ __forceinline__ void group_min_n(uint32_t (&v)[ND])
     if constexpr (N >= 32) {
 #pragma unroll
         for (int n = 0; n < ND; n++) v[n] = row_pair_combine(v[n], [](uint32_t a, uint32_t b) { return ::min(a, b); });
+    }
+    if constexpr (N >= 64) {  // the two wave halves: v_permlane32_swap
+#pragma unroll
+        for (int n = 0; n < ND; n++) {
+            const auto r = __builtin_amdgcn_permlane32_swap(v[n], v[n], false, false);
+            v[n] = ::min((uint32_t)r[0], (uint32_t)r[1]);
+        }
     }
 }
 

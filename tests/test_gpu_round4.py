@@ -71,14 +71,15 @@ def test_latency_strips_full_kitti(eng, cost, mode, D):
     assert np.array_equal(out, exp), f"{np.sum(out != exp)} px differ"
 
 
-@pytest.mark.parametrize("lanes", [-1, 8, 16, 32])
+@pytest.mark.parametrize("lanes", [-1, 8, 16, 32, 64])
 @pytest.mark.parametrize("cost,mode,D", [(0, 5, 128), (0, 8, 128), (0, 5, 160), (1, 8, 128), (0, 5, 64), (1, 8, 96)])
 def test_ew_lanes_bit_exact(eng, lanes, cost, mode, D):
     """Every E/W line width built for D gives the oracle's maps (row lines -1; packed lines
-    of 8, 16 or 32 lanes); unbuilt widths are refused, not silently replaced."""
+    of 8, 16, 32 or 64 lanes); unbuilt widths are refused, not silently replaced."""
     left, right, _ = synthetic.random_dot_pair(61, 2 * D + 150, D, seed=lanes * 7 + D)
     p = _params(cost, D, mode)
-    built = lanes in (-1, 8) or (lanes == 16 and D % 32 == 0) or (lanes == 32 and D % 64 == 0)
+    built = (lanes in (-1, 8) or (lanes == 16 and D % 32 == 0) or (lanes == 32 and D % 64 == 0)
+             or (lanes == 64 and D in (128, 256)))
     if not built:
         with pytest.raises(_lib.SmError):
             _run(eng, left, right, p, ew_lanes=lanes)
