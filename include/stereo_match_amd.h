@@ -259,6 +259,21 @@ int sm_synchronize(sm_ctx* ctx);
  * guarded per-direction fallback.  Synchronises the context stream. */
 int sm_get_counters(sm_ctx* ctx, long long* sweep_fallbacks);
 
+/* One counter since sm_create (synchronises the context's streams):
+ *   SM_COUNTER_SWEEP_FALLBACKS  launch groups the guarded per-direction fallback recomputed;
+ *   SM_COUNTER_EW_REPAIRS       E/W strip segments of the in-sweep lines whose speculative
+ *                               start state differed from the true one and that the patch
+ *                               pass recomputed (results stay exact; a measure of the
+ *                               speculation);
+ *   SM_COUNTER_VOLUME_CLAMPED   external cost-volume cells (sm_aggregate_cost_f32*) whose
+ *                               quantised value fell outside [0, 4095] and was clamped;
+ *   SM_COUNTER_VOLUME_NAN       external cost-volume cells that were NaN (cost 4095). */
+#define SM_COUNTER_SWEEP_FALLBACKS 0
+#define SM_COUNTER_EW_REPAIRS 1
+#define SM_COUNTER_VOLUME_CLAMPED 2
+#define SM_COUNTER_VOLUME_NAN 3
+int sm_get_counter(sm_ctx* ctx, int which, long long* value);
+
 /* Restrict the context's own streams (the default stream and its internal
  * second stream) to a CU subset: mask = nwords 32-bit words, bit i = CU i
  * (hipExtStreamCreateWithCUMask); nwords = 0 restores unmasked streams.  The
@@ -346,11 +361,20 @@ int sm_set_debug_flags(sm_ctx* ctx, int flags);
  *                      instance's count where built; unbuilt counts fail the call.
  *   SM_TUNE_EW_WAVES   waves per workgroup of the packed E/W lines: 0 automatic, 1..4.
  *   SM_TUNE_EW_PRIO    issue priority (s_setprio 0..3) of the packed E/W lines' waves.
+ *   SM_TUNE_EW_WARMUP  columns each in-sweep E/W strip segment runs before its strip
+ *                      (0 automatic: 16 census, 24 u16 costs; 1..4096).  Any value is
+ *                      exact (the patch pass repairs segments that started wrong); small
+ *                      values force repairs (tests), large ones cost line work.
+ *   SM_TUNE_SWEEP_LINES the fused-sweep engine's horizontal paths: 0 automatic (inside the
+ *                      down sweep wherever that instance is built), 1 the same, -1 the E/W
+ *                      volume kernel (k_ew) before / beside the sweeps.
  * Returns SM_E_ARG for an unknown key or value. */
 #define SM_TUNE_EW_LANES 1
 #define SM_TUNE_SWEEP_NCW 2
 #define SM_TUNE_EW_WAVES 3
 #define SM_TUNE_EW_PRIO 4
+#define SM_TUNE_EW_WARMUP 5
+#define SM_TUNE_SWEEP_LINES 6
 int sm_set_tuning(sm_ctx* ctx, int key, int value);
 
 /* Last error text of ctx (or of the calling thread when ctx == NULL). */

@@ -120,6 +120,7 @@ _SIGS = {
     "sm_right_matcher_params": (_c.c_int, [_c.POINTER(SmParams), _c.POINTER(SmParams)]),
     "sm_synchronize": (_c.c_int, [_c.c_void_p]),
     "sm_get_counters": (_c.c_int, [_c.c_void_p, _c.POINTER(_c.c_longlong)]),
+    "sm_get_counter": (_c.c_int, [_c.c_void_p, _c.c_int, _c.POINTER(_c.c_longlong)]),
     "sm_set_cu_mask": (_c.c_int, [_c.c_void_p, _c.POINTER(_c.c_uint32), _c.c_int]),
     "sm_set_timing": (_c.c_int, [_c.c_void_p, _c.c_int]),
     "sm_get_timing": (_c.c_int, [_c.c_void_p, _c.c_int, _c.POINTER(_c.c_double), _c.POINTER(_c.c_longlong),
@@ -182,14 +183,24 @@ def load():
                 "There is no CPU fallback.")
         _init_torch_hip_first()
         lib = ctypes.CDLL(LIB_PATH)
-        for name, (res, args) in _SIGS.items():
-            fn = getattr(lib, name)
-            fn.restype = res
-            fn.argtypes = args
+        # the version check comes before any other symbol is bound: a library built for an
+        # older ABI may lack symbols this binding declares (AttributeError otherwise)
+        if not hasattr(lib, "sm_abi_version"):
+            raise ImportError(f"{LIB_PATH} predates the versioned C-ABI (no sm_abi_version), this binding needs "
+                              f"version {ABI_VERSION}: rebuild it with `make -C stereo_match_amd/csrc`")
+        lib.sm_abi_version.restype = ctypes.c_int
+        lib.sm_abi_version.argtypes = []
         abi = lib.sm_abi_version()
         if abi != ABI_VERSION:
             raise ImportError(f"{LIB_PATH} has C-ABI version {abi}, this binding needs {ABI_VERSION}: rebuild it "
                               "with `make -C stereo_match_amd/csrc`")
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(lib, name, None)
+            if fn is None:
+                raise ImportError(f"{LIB_PATH} (C-ABI {abi}) does not export {name}: rebuild it with "
+                                  "`make -C stereo_match_amd/csrc`")
+            fn.restype = res
+            fn.argtypes = args
         _lib = lib
         return lib
 
@@ -413,11 +424,19 @@ class Engine:
     def synchronize(self):
         self._check(self._lib.sm_synchronize(self.ctx))
 
+    COUNTERS = ("sweep_fallbacks", "ew_repairs", "volume_clamped", "volume_nan")  # SM_COUNTER_* order
+
     def counters(self) -> dict:
-        """{"sweep_fallbacks": launch groups recomputed by the guarded fallback}"""
+        """Counters since the engine was created (include/stereo_match_amd.h SM_COUNTER_*):
+        sweep_fallbacks (launch groups the guarded fallback recomputed), ew_repairs (in-sweep
+        E/W strip segments the patch pass recomputed), volume_clamped / volume_nan (external
+        cost-volume cells clamped by the quantisation window / NaN)."""
+        out = {}
         n = ctypes.c_longlong()
-        self._check(self._lib.sm_get_counters(self.ctx, ctypes.byref(n)))
-        return {"sweep_fallbacks": n.value}
+        for i, name in enumerate(self.COUNTERS):
+            self._check(self._lib.sm_get_counter(self.ctx, i, ctypes.byref(n)))
+            out[name] = n.value
+        return out
 
     def set_cu_mask(self, cus):
         """Restrict the context's streams to the CU indices in ``cus`` (None: all)."""
@@ -460,7 +479,7 @@ class Engine:
         """Timing ablations only (results become wrong); 0 = normal."""
         self._check(self._lib.sm_set_debug_flags(self.ctx, int(flags)))
 
-    TUNE_EW_LANES, TUNE_SWEEP_NCW, TUNE_EW_WAVES, TUNE_EW_PRIO = 1, 2, 3, 4
+    TUNE_EW_LANES, TUNE_SWEEP_NCW, TUNE_EW_WAVES, TUNE_EW_PRIO, TUNE_EW_WARMUP, TUNE_SWEEP_LINES = 1, 2, 3, 4, 5, 6
 
     def set_tuning(self, key: int, value: int):
         """Launch-shape knob (include/stereo_match_amd.h sm_set_tuning); 0 = automatic."""

@@ -79,6 +79,7 @@ struct TimedEvent {
 struct BufSet {
     DevBuf census[2], cost, L, raw;
     DevBuf part, key2, pre;  // sweep engine: u16 partial sums, WTA winner records, sub-pixel inputs
+    DevBuf st;               // in-sweep E/W lines (MODE 3): the strip segments' boundary states
     hipEvent_t paths_done = nullptr, wta_done = nullptr;
     bool pending = false;  // wta_done recorded and not yet waited for by stream A
 };
@@ -109,6 +110,9 @@ constexpr int DBG_FORCE_FALLBACK = 1 << 23;
 // up waiting; cleared by the host before each group), the sticky error of the
 // (unguarded) hybrid engine, and the count of fallback recomputations
 constexpr int ERR_GROUP0 = 0, ERR_STICKY = 32, ERR_FALLBACKS = 48;
+// E/W strip segments the patch pass recomputed (u32), and (u64 words at 52, 54) the external
+// cost-volume cells clamped by the quantisation window / NaN cells
+constexpr int ERR_EW_REPAIRS = 49, ERR_VOL_CLAMPED = 52, ERR_VOL_NAN = 54;
 // timing ablation: no guarded fallback launches after the sweeps
 constexpr int DBG_NO_FALLBACK = (int)0x80000000u;
 // flags only the ablation build (SM_ABLATIONS) accepts: timing switches whose results are
@@ -153,6 +157,7 @@ struct sm_ctx {
     int dbg_flags = 0;
     // sm_set_tuning knobs (0 = automatic)
     int tune_ew_lanes = 0, tune_sweep_ncw = 0, tune_ew_waves = 0, tune_ew_prio = 0;
+    int tune_ew_warmup = 0, tune_sweep_lines = 0;  // in-sweep E/W lines: warmup columns, -1 off / 1 on
     std::vector<TimedEvent> pending;
     std::vector<hipEvent_t> free_events;
     double stage_ms[SM_NUM_STAGES] = {0};
@@ -430,6 +435,7 @@ struct Geo {  // per-group geometry shared by the launches
     int H, W, stride, G;
     size_t vol, slot_bytes, L_pair, census_pair, cost_pair;
     bool sweep;   // fused-sweep engine (sm_sweep.hpp) instead of per-direction volumes
+    bool lines;   // ... with the E/W lines inside the down sweep (MODE 3 + patch pass) instead of k_ew volumes
     bool hybrid;  // 8 paths: down sweep (u16 partial) beside a per-direction launch of E, W, NE, N, NW
 };
 
@@ -570,8 +576,11 @@ int launch_wta_t(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs)
     wa.L = (const uint8_t*)bs.L.p;
     wa.slot_bytes = g.slot_bytes;
     wa.L_pair_bytes = g.L_pair;
-    wa.nslots = g.hybrid ? hybrid_slots(n) : n.ndirs;
-    wa.part = g.hybrid ? (const uint16_t*)bs.part.p : nullptr;  // hybrid: S + SE + SW partial
+    // in-sweep E/W lines (5 paths): S = the patched partial alone; the guarded fallback reads
+    // every direction's volume
+    const bool part_only = g.lines && !ctx->fb_guard;
+    wa.nslots = part_only ? 0 : g.hybrid ? hybrid_slots(n) : n.ndirs;
+    wa.part = (g.hybrid || part_only) ? (const uint16_t*)bs.part.p : nullptr;  // hybrid: S + SE + SW partial
     wa.part_pair = g.vol;
     wa.H = g.H;
     wa.W = g.W;
@@ -691,6 +700,9 @@ struct SweepJob {
     uint32_t* pre;  // sub-pixel inputs (SweepArgs::nb)
     uint32_t* err;  // word a strip sets when it gives up waiting for a neighbour
     int G;
+    uint8_t* st = nullptr;  // MODE 3: boundary states of the E/W strip segments
+    size_t st_pair = 0;     // bytes
+    int ewarm = 0;          // MODE 3: warmup columns of the E/W segments
 };
 
 // CUs the stream may run on: its CU mask (sm_set_cu_mask), the whole device when unmasked
@@ -781,7 +793,7 @@ bool sweep_capacity(sm_ctx* ctx, const Norm& n, int mode, int G, SweepFit& f)
     if (ctx->tune_sweep_ncw && sweep_variant(ctx) <= 1) {
         for (int v : {0, 1, 2}) {
             SweepFit t;
-            if (sweep_fit_variant(ctx, n, mode, v, t) && t.si.threads / 64 - 1 == ctx->tune_sweep_ncw) {
+            if (sweep_fit_variant(ctx, n, mode, v, t) && t.si.ncw == ctx->tune_sweep_ncw) {
                 f = t;
                 return true;
             }
@@ -805,11 +817,12 @@ bool sweep_capacity(sm_ctx* ctx, const Norm& n, int mode, int G, SweepFit& f)
 
 // every sweep pass of the configuration can make all strips of a pair co-resident (wide
 // images on few CUs cannot: those run on the per-direction engine)
-bool sweeps_fit(sm_ctx* ctx, const Norm& n, bool hybrid)
+bool sweeps_fit(sm_ctx* ctx, const Norm& n, bool hybrid, bool lines = false)
 {
-    // passes: hybrid = the down sweep; 8 paths = down + up/WTA; 5 paths = down/WTA
-    const int m8[2] = {0, 2}, m5[1] = {1}, mh[1] = {0};
-    const int* modes = hybrid ? mh : n.ndirs == 8 ? m8 : m5;
+    // passes: hybrid = the down sweep; 8 paths = down + up/WTA; 5 paths = down/WTA; with the
+    // in-sweep E/W lines: the down sweep with lines (+ the up/WTA sweep over its partial)
+    const int m8[2] = {0, 2}, m5[1] = {1}, mh[1] = {0}, l8[2] = {3, 4}, l5[1] = {3};
+    const int* modes = hybrid ? mh : lines ? (n.ndirs == 8 ? l8 : l5) : n.ndirs == 8 ? m8 : m5;
     const int count = !hybrid && n.ndirs == 8 ? 2 : 1;
     for (int k = 0; k < count; k++) {
         SweepFit f;
@@ -859,6 +872,9 @@ int sweep_pass(sm_ctx* ctx, const Norm& n, const Geo& g, const SweepJob& j, int 
         a.part_pair = j.part_pair;
         a.hop = (unsigned long long*)ctx->hop.p;
         a.hop_pair = hop_pair;
+        a.st = j.st ? j.st + (size_t)p0 * j.st_pair : nullptr;
+        a.st_pair = j.st_pair;
+        a.ewarm = j.ewarm;
         a.rec = j.key2 ? j.key2 + (size_t)p0 * g.H * g.W : nullptr;
         a.nb = j.pre ? j.pre + (size_t)p0 * g.H * g.W : nullptr;
         a.err = j.err;
@@ -1005,7 +1021,24 @@ int sweep_finish(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs, hipStream
 {
     const bool fb = !(ctx->dbg_flags & DBG_NO_FALLBACK);
     int rc;
-    hipStream_t fs = ws == ctx->side ? ctx->stream : ctx->side;  // the stream the fallback runs on
+    if (fb && ws != ctx->stream) {
+        // the WTA sweep runs on the second stream beside the next group (flag 64): a fallback
+        // on ctx->stream would make that group wait for this group's WTA sweep, so it follows
+        // the LR pass on ws instead (in order; the LR pass writes nothing when the flag is set)
+        if (ctx->dbg_flags & DBG_FORCE_FALLBACK) HIP_TRY(ctx, hipMemsetAsync(gflag, 1, 1, ws));
+        HIP_TRY(ctx, smk::lr_rows_launch((const uint32_t*)bs.key2.p, (const uint32_t*)bs.pre.p, (int16_t*)bs.raw.p,
+                                         ctx->wta_dst, g.G, g.H, g.W, n.Dv, n.minD, n.minX1, n.maxX1, n.disp12,
+                                         gflag, ws));
+        StreamSwap sw(ctx, ws);
+        ctx->wta_override = ws;
+        ctx->fb_guard = gflag;
+        rc = dispatch(ctx, n, g, bs, DISPATCH_PATHS);
+        if (rc == SM_OK) rc = dispatch(ctx, n, g, bs, DISPATCH_WTA);
+        ctx->fb_guard = nullptr;
+        ctx->wta_override = nullptr;
+        return rc;
+    }
+    hipStream_t fs = ctx->side;  // the stream the fallback runs on (ws == ctx->stream here)
     if (fb) {
         if (ctx->dbg_flags & DBG_FORCE_FALLBACK) HIP_TRY(ctx, hipMemsetAsync(gflag, 1, 1, ws));
         if ((rc = ensure_event(ctx, ctx->ev_fb_fork)) != SM_OK) return rc;
@@ -1027,6 +1060,108 @@ int sweep_finish(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs, hipStream
                                      fb ? gflag : nullptr, ws));
     if (fb) HIP_TRY(ctx, hipStreamWaitEvent(ws, ctx->ev_fb_join, 0));
     return SM_OK;
+}
+
+// ---- in-sweep E/W lines: MODE 3 down sweep with line waves -> patch pass ->
+// (8 paths) MODE 4 up/WTA sweep + LR pass, (5 paths) k_wta over the partial.  No E/W volumes:
+// census 8 paths 7 instead of 13 B per cell, u16 5 paths 6 instead of 16.
+// By default wherever the MODE 3 instance (and MODE 4 at 8 paths) fits; SM_TUNE_SWEEP_LINES -1,
+// any SM_TUNE_EW_LANES value or flag 256 keep the E/W volumes (k_ew / row lines).
+bool use_lines(sm_ctx* ctx, const Norm& n)
+{
+    if (ctx->tune_sweep_lines < 0 || ctx->tune_ew_lanes || (ctx->dbg_flags & DBG_OLD_EW)) return false;
+    return sweeps_fit(ctx, n, false, true);
+}
+
+// warmup columns of the E/W strip segments: the speculative state meets the true one within
+// 16 columns on ~98 % of KITTI census segments, 24 on ~97 % of u16 (settings.ini) ones
+// (measured on the synthetic pairs with the numpy oracle); SM_TUNE_EW_WARMUP overrides
+int ew_warmup(const sm_ctx* ctx, const Norm& n)
+{
+    if (ctx->tune_ew_warmup > 0) return ctx->tune_ew_warmup;
+    return elem_bytes(n) == 1 ? 16 : 24;
+}
+
+int run_lines(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs, hipStream_t ws, uint32_t* gflag)
+{
+    const int G = g.G;
+    const size_t et = elem_bytes(n);
+    int rc;
+    SweepJob j{};
+    j.cost = (const uint8_t*)bs.cost.p;
+    j.cost_pair = g.vol * et;
+    j.G = G;
+    j.err = gflag;
+    if ((rc = ensure(ctx, bs.part, (size_t)G * g.vol * 2)) != SM_OK) return rc;
+    j.part = (uint16_t*)bs.part.p;
+    j.part_pair = g.vol * 2;
+    SweepFit f;
+    if (!sweep_capacity(ctx, n, 3, G, f)) return fail(ctx, SM_E_UNSUPPORTED, "sweep lines: no instance fits");
+    j.st_pair = ((size_t)g.H * f.nwg * 4 * n.D * et + 255) & ~size_t(255);
+    if ((rc = ensure(ctx, bs.st, j.st_pair * G)) != SM_OK) return rc;
+    j.st = (uint8_t*)bs.st.p;
+    j.ewarm = ew_warmup(ctx, n);
+    {
+        StageTimer t(ctx, ctx->stream, SM_STAGE_PATHS, G);
+        {
+            StageTimer ts(ctx, ctx->stream, SM_STAGE_SWEEP, G);
+            if ((rc = sweep_pass(ctx, n, g, j, 3)) != SM_OK) return rc;
+        }
+        StageTimer th(ctx, ctx->stream, SM_STAGE_HORIZONTAL, G);
+        smk::EwPatchArgs pa{};
+        pa.cost = j.cost;
+        pa.cost_pair = j.cost_pair;
+        pa.part = j.part;
+        pa.part_pair = j.part_pair * 1;
+        pa.st = j.st;
+        pa.st_pair = j.st_pair;
+        pa.H = g.H;
+        pa.W1 = n.width1;
+        pa.nwg = f.nwg;
+        pa.cw = f.si.cw;
+        pa.P1 = n.P1;
+        pa.P2 = n.P2;
+        pa.guard = gflag;
+        pa.fixes = (uint32_t*)ctx->sweep_err.p + ERR_EW_REPAIRS;
+        const hipError_t e = smk::ew_patch_launch(n.D, (int)et, pa, G, ctx->stream);
+        if (e == hipErrorInvalidValue) return fail(ctx, SM_E_UNSUPPORTED, "E/W patch: numDisparities %d not built", n.D);
+        HIP_TRY(ctx, e);
+    }
+    if (ws != ctx->stream) {
+        HIP_TRY(ctx, hipEventRecord(bs.paths_done, ctx->stream));
+        HIP_TRY(ctx, hipStreamWaitEvent(ws, bs.paths_done, 0));
+    }
+    if (n.ndirs == 8) {
+        if ((rc = ensure(ctx, bs.key2, (size_t)G * g.H * g.W * 4)) != SM_OK) return rc;
+        if ((rc = ensure(ctx, bs.pre, (size_t)G * g.H * g.W * 4)) != SM_OK) return rc;
+        j.key2 = (uint32_t*)bs.key2.p;
+        j.pre = (uint32_t*)bs.pre.p;
+        {
+            StreamSwap sw(ctx, ws);
+            StageTimer t(ctx, ctx->stream, SM_STAGE_WTA, G);
+            StageTimer ts(ctx, ctx->stream, SM_STAGE_SWEEP_WTA, G);
+            if ((rc = sweep_pass(ctx, n, g, j, 4)) != SM_OK) return rc;
+        }
+        return sweep_finish(ctx, n, g, bs, ws, gflag);
+    }
+    // 5 paths: the WTA row kernel over the patched partial (k_wta: uniqueness, sub-pixel, LR)
+    // into bs.raw, then the guarded per-direction fallback of the group (it exits at once
+    // unless a strip gave up, and then overwrites bs.raw)
+    StreamSwap sw(ctx, ws);
+    ctx->wta_override = ws;
+    {
+        StageTimer ts(ctx, ws, SM_STAGE_SWEEP_WTA, G);
+        rc = dispatch(ctx, n, g, bs, DISPATCH_WTA);
+    }
+    if (rc == SM_OK && !(ctx->dbg_flags & DBG_NO_FALLBACK)) {
+        if (ctx->dbg_flags & DBG_FORCE_FALLBACK) HIP_TRY(ctx, hipMemsetAsync(gflag, 1, 1, ws));
+        ctx->fb_guard = gflag;
+        rc = dispatch(ctx, n, g, bs, DISPATCH_PATHS);
+        if (rc == SM_OK) rc = dispatch(ctx, n, g, bs, DISPATCH_WTA);
+        ctx->fb_guard = nullptr;
+    }
+    ctx->wta_override = nullptr;
+    return rc;
 }
 
 // hybrid 8-path aggregation (see use_hybrid); leaves per-direction slots 0..4 and bs.part for k_wta
@@ -1513,13 +1648,18 @@ int run_group(sm_ctx* ctx, const Src& src, const Geo& g, const Norm& n, int16_t*
         // 5 paths: the WTA sweep of this group overlaps the next group's cost + E/W
         // (the 8-path sweeps keep the second stream for their E/W fork)
         const hipStream_t ws = n.ndirs == 5 ? stream_b(ctx) : ctx->stream;
-        if ((rc = run_sweep(ctx, n, g, bs, ws, gflag)) != SM_OK) return rc;
+        if (g.lines) {
+            if ((rc = run_lines(ctx, n, g, bs, ws, gflag)) != SM_OK) return rc;
+        } else if ((rc = run_sweep(ctx, n, g, bs, ws, gflag)) != SM_OK) {
+            return rc;
+        }
         // Strips of a sweep wait on their neighbours, so all of a launch's strips must be
         // resident together; the grid is sized for that (sweep_pass), but work on other
         // streams or processes can take the slots.  A strip that gives up raises the
         // group flag, and the guarded per-direction launch pair (a small grid that exits
-        // at once while the flag is clear) then recomputes the whole group into bs.raw.
-        if ((rc = sweep_finish(ctx, n, g, bs, ws, gflag)) != SM_OK) return rc;
+        // at once while the flag is clear) then recomputes the whole group into bs.raw
+        // (run_lines enqueues its own).
+        if (!g.lines && (rc = sweep_finish(ctx, n, g, bs, ws, gflag)) != SM_OK) return rc;
     } else if (g.hybrid) {
         if ((rc = run_hybrid(ctx, n, g, bs)) != SM_OK) return rc;
     } else if ((rc = dispatch(ctx, n, g, bs, DISPATCH_PATHS)) != SM_OK) {
@@ -1552,7 +1692,9 @@ int run_pairs(sm_ctx* ctx, const Src& src, int npairs, int H, int W, int stride,
     g.vol = (size_t)H * std::max(n.width1, 0) * n.D;
     g.slot_bytes = (g.vol * elem_bytes(n) + 255) & ~size_t(255);
     g.hybrid = !n.wide && use_hybrid(ctx, n, H) && sweeps_fit(ctx, n, true);
-    g.sweep = !n.wide && !g.hybrid && use_sweep(ctx, n, H) && sweeps_fit(ctx, n, false);
+    const bool sweep_ok = !n.wide && !g.hybrid && use_sweep(ctx, n, H);
+    g.lines = sweep_ok && use_lines(ctx, n);
+    g.sweep = g.lines || (sweep_ok && sweeps_fit(ctx, n, false));
     if (ctx->tune_sweep_ncw && !n.wide && !g.hybrid && !g.sweep && use_sweep(ctx, n, H))
         return fail(ctx, SM_E_UNSUPPORTED, "no fused-sweep instance with %d compute waves fits (D %d)",
                     ctx->tune_sweep_ncw, n.D);
@@ -1563,12 +1705,15 @@ int run_pairs(sm_ctx* ctx, const Src& src, int npairs, int H, int W, int stride,
     g.cost_pair = n.cost == SM_COST_CENSUS ? 0 : g.vol;
     int G = group_size(ctx, n, H, npairs, g.sweep, g.hybrid);
     // the sweeps' parallelism is (strips x pairs): below sweep_min_pairs pairs per launch
-    // group the per-direction engine is faster; flag 16384 forces them
-    if (g.sweep && std::min(G, npairs) < sweep_min_pairs(ctx, n) && !(ctx->dbg_flags & DBG_SWEEP8)) {
-        g.sweep = false;
+    // group the per-direction engine is faster; flag 16384 forces them, and so
+    // does SM_TUNE_SWEEP_NCW (a forced instance is measured, never silently replaced)
+    if (g.sweep && std::min(G, npairs) < sweep_min_pairs(ctx, n) && !(ctx->dbg_flags & DBG_SWEEP8) &&
+        !ctx->tune_sweep_ncw) {
+        g.sweep = g.lines = false;
         G = group_size(ctx, n, H, npairs, false, false);
     }
-    ctx->last_ndirs = g.sweep ? 2 : g.hybrid ? hybrid_slots(n) : n.ndirs;
+    // sm_debug_fetch(1): the sweep engine's E/W volumes (none with the in-sweep lines)
+    ctx->last_ndirs = g.lines ? 0 : g.sweep ? 2 : g.hybrid ? hybrid_slots(n) : n.ndirs;
     int rc = SM_OK;
     {
         StageTimer total(ctx, ctx->stream, SM_STAGE_TOTAL, npairs);
@@ -2392,6 +2537,8 @@ int sm_compute_disparity_batch_device(sm_ctx* ctx, const uint8_t* dL, const uint
         ctx->twin->tune_sweep_ncw = ctx->tune_sweep_ncw;
         ctx->twin->tune_ew_waves = ctx->tune_ew_waves;
         ctx->twin->tune_ew_prio = ctx->tune_ew_prio;
+        ctx->twin->tune_ew_warmup = ctx->tune_ew_warmup;
+        ctx->twin->tune_sweep_lines = ctx->tune_sweep_lines;
         if (!ctx->cu_mask.empty() &&
             (rc = sm_set_cu_mask(ctx->twin, ctx->cu_mask.data(), (int)ctx->cu_mask.size())) != SM_OK)
             return fail(ctx, rc, "%s", ctx->twin->err.c_str());
@@ -2721,6 +2868,38 @@ int sm_get_counters(sm_ctx* ctx, long long* sweep_fallbacks)
     return SM_OK;
 }
 
+int sm_get_counter(sm_ctx* ctx, int which, long long* value)
+{
+    if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
+    if (!value) return fail(ctx, SM_E_ARG, "value is NULL");
+    if (which < SM_COUNTER_SWEEP_FALLBACKS || which > SM_COUNTER_VOLUME_NAN)
+        return fail(ctx, SM_E_ARG, "unknown counter %d", which);
+    long long v = 0;
+    if (ctx->sweep_err.p) {
+        HIP_TRY(ctx, hipSetDevice(ctx->device));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->side));
+        if (which == SM_COUNTER_VOLUME_CLAMPED || which == SM_COUNTER_VOLUME_NAN) {
+            unsigned long long u = 0;
+            const int word = which == SM_COUNTER_VOLUME_CLAMPED ? ERR_VOL_CLAMPED : ERR_VOL_NAN;
+            HIP_TRY(ctx, hipMemcpy(&u, (uint32_t*)ctx->sweep_err.p + word, 8, hipMemcpyDeviceToHost));
+            v = (long long)u;
+        } else {
+            uint32_t u = 0;
+            const int word = which == SM_COUNTER_SWEEP_FALLBACKS ? ERR_FALLBACKS : ERR_EW_REPAIRS;
+            HIP_TRY(ctx, hipMemcpy(&u, (uint32_t*)ctx->sweep_err.p + word, 4, hipMemcpyDeviceToHost));
+            v = u;
+        }
+    }
+    long long t = 0;
+    if (ctx->twin) {
+        int rc = sm_get_counter(ctx->twin, which, &t);
+        if (rc != SM_OK) return rc;
+    }
+    *value = v + t;
+    return SM_OK;
+}
+
 int sm_set_cu_mask(sm_ctx* ctx, const uint32_t* mask, int nwords)
 {
     if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
@@ -2809,6 +2988,14 @@ int sm_set_tuning(sm_ctx* ctx, int key, int value)
     case SM_TUNE_SWEEP_NCW:
         if (value < 0) return fail(ctx, SM_E_ARG, "sweep compute waves %d < 0", value);
         ctx->tune_sweep_ncw = value;
+        break;
+    case SM_TUNE_EW_WARMUP:
+        if (value < 0 || value > 4096) return fail(ctx, SM_E_ARG, "E/W segment warmup %d: 0..4096", value);
+        ctx->tune_ew_warmup = value;
+        break;
+    case SM_TUNE_SWEEP_LINES:
+        if (value < -1 || value > 1) return fail(ctx, SM_E_ARG, "sweep lines %d: -1, 0 or 1", value);
+        ctx->tune_sweep_lines = value;
         break;
     default: return fail(ctx, SM_E_ARG, "unknown tuning key %d", key);
     }

@@ -66,6 +66,39 @@ hipError_t ew_d(int D, int vl, const EwArgs& a, int npairs, hipStream_t stream)
 
 }  // namespace
 
+namespace {
+
+template <int VL, int NP, typename CT>
+hipError_t run_patch(const EwPatchArgs& a, int npairs, hipStream_t stream)
+{
+    constexpr int LPW = 64 / VL;
+    hipLaunchKernelGGL((k_ew_patch<VL, NP, CT>), dim3((a.H + 4 * LPW - 1) / (4 * LPW), npairs), dim3(256), 0, stream, a);
+    return hipGetLastError();
+}
+
+template <typename CT>
+hipError_t patch_d(int D, const EwPatchArgs& a, int npairs, hipStream_t stream)
+{
+    switch (D) {  // 16-lane lines where D % 32 == 0, else 8-lane lines (every D % 16 == 0)
+#define P16(d) \
+    case d: return run_patch<16, d / 32, CT>(a, npairs, stream);
+#define P8(d) \
+    case d: return run_patch<8, d / 16, CT>(a, npairs, stream);
+        P8(16) P16(32) P8(48) P16(64) P8(80) P16(96) P8(112) P16(128)
+        P8(144) P16(160) P8(176) P16(192) P8(208) P16(224) P8(240) P16(256)
+#undef P16
+#undef P8
+    default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace
+
+hipError_t ew_patch_launch(int D, int ct_bytes, const EwPatchArgs& a, int npairs, hipStream_t stream)
+{
+    return ct_bytes == 1 ? patch_d<uint8_t>(D, a, npairs, stream) : patch_d<uint16_t>(D, a, npairs, stream);
+}
+
 hipError_t ew_launch(int D, int ct_bytes, int vl, EwArgs a, int npairs, hipStream_t stream)
 {
     return ct_bytes == 1 ? ew_d<uint8_t>(D, vl, a, npairs, stream) : ew_d<uint16_t>(D, vl, a, npairs, stream);

@@ -30,26 +30,6 @@ namespace smk {
 #define EW_STEPN 1  // the step's words stage by stage (no wait states between dependent VOP3P ops)
 #endif
 
-// NP packed u16 pairs -> LT bytes at byte offset off (u8: truncating pack; u16: as is)
-template <typename LT, int NP, int AUX = 0>
-__device__ __forceinline__ void store_pk(rsrc_t r, uint32_t off, const uint32_t (&w)[NP])
-{
-    if constexpr (sizeof(LT) == 2) {
-        bstore_n<uint32_t, NP, AUX>(r, off, w);
-    } else {
-        constexpr int NW = NP / 2;
-        if constexpr (NW > 0) {
-            uint32_t b[NW];
-#pragma unroll
-            for (int j = 0; j < NW; j++) b[j] = __builtin_amdgcn_perm(w[2 * j + 1], w[2 * j], 0x06040200u);
-            bstore_n<uint32_t, NW, AUX>(r, off, b);
-        }
-        if constexpr (NP % 2)
-            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)((w[NP - 1] & 0xFFu) | ((w[NP - 1] >> 8) & 0xFF00u)), r,
-                                                  off + 4 * NW, 0, AUX);
-    }
-}
-
 // grid (2 * a.nrb, pairs), 64 * a.wpb threads: workgroup b < nrb runs E lines, the rest W;
 // each wave owns LPW = 64 / VL consecutive rows.
 template <int VL, int NP, typename CT, typename LT, int PF>
@@ -133,6 +113,157 @@ __global__ void __launch_bounds__(256) k_ew(EwArgs a)
             minLp = mn;
         }
     }
+}
+
+// ---------------------------------------------------------------------------
+// Patch pass after a MODE 3 sweep (sm_sweep.hpp line waves).  Strip k's E line
+// started from the zero state `ewarm` columns before the strip, so its values are exact from
+// the column where its state met the true one.  Walking one row's strips in path order, the
+// trusted state entering strip k is strip k-1's stored end state as long as every earlier
+// strip was exact (or was repaired up to the meeting point); where the stored entering state
+// of strip k differs from it, the segment is recomputed from the trusted state beside the
+// speculative one (from k's stored entering state) and the partial gets (true - speculative)
+// column by column until the two trajectories are equal, after which every later value is
+// equal.  A segment that never meets hands its true end state to the next strip.  One line of
+// VL lanes per image row walks E, then W, so no two lines touch one partial cell.
+// u16 costs: the MODE 3 partial saturates at 0xFFFF; a cell below that holds the exact sum
+// (every term >= 0), one at 0xFFFF stays there (the true five-path sum is then still
+// >= 65535 - 2 * 16383 > 32767, so the WTA's 32767 clamp sees the same value).
+template <int VL, int NP, typename CT>
+__global__ void __launch_bounds__(256) k_ew_patch(EwPatchArgs a)
+{
+    constexpr int LPW = 64 / VL, DPL = 2 * NP, D = VL * DPL;
+    constexpr int CB = DPL * (int)sizeof(CT);
+    constexpr bool H16 = sizeof(CT) == 1 && EW_H16;
+    constexpr bool SAT = sizeof(CT) == 2;
+    constexpr uint32_t EDGE = H16 ? 0x7BFF7BFFu : (kBig | (kBig << 16));
+    constexpr int KB = 8;  // strips whose boundary states are loaded together
+    if (a.guard && __hip_atomic_load(a.guard, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int g = lane % VL, kl = lane / VL;
+    const int y = ((int)blockIdx.x * 4 + wave) * LPW + kl;
+    const size_t pair = blockIdx.y;
+    const int H = a.H, W1 = a.W1, nwg = a.nwg, CW = a.cw;
+    if (y >= H) return;  // line-uniform; the remaining lines' DPL steps stay inside their lanes
+    const uint64_t cells = (uint64_t)H * W1 * D;
+    const rsrc_t rc = make_rsrc(a.cost + pair * a.cost_pair, cells * sizeof(CT));
+    const rsrc_t rp = make_rsrc((const uint8_t*)a.part + pair * a.part_pair, cells * 2);
+    const rsrc_t rs = make_rsrc(a.st + pair * a.st_pair, a.st_pair);
+    const uint32_t P1p = (uint32_t)a.P1 * 0x10001u, P2p = (uint32_t)a.P2 * 0x10001u;
+    const uint32_t eL = g == 0 ? EDGE : 0u, eR = g == VL - 1 ? EDGE : 0u;
+    auto soff = [&](int k, int dir, int which) -> uint32_t {
+        return (((((uint32_t)y * (uint32_t)nwg + (uint32_t)k) * 2u + (uint32_t)dir) * 2u + (uint32_t)which) *
+                    (uint32_t)D + (uint32_t)(g * DPL)) * (uint32_t)sizeof(CT);
+    };
+    auto cell = [&](int c) -> uint32_t { return ((uint32_t)y * (uint32_t)W1 + (uint32_t)c) * (uint32_t)D + (uint32_t)(g * DPL); };
+    auto line_all = [&](bool ok) -> bool { return group_min<VL>(ok ? 1u : 0u) != 0u; };
+    auto same_state = [&](const uint32_t (&x)[NP], const uint32_t (&z)[NP]) -> bool {
+        bool ok = true;
+#pragma unroll
+        for (int i = 0; i < NP; i++) ok &= x[i] == z[i];
+        return line_all(ok);
+    };
+    // the recurrence's replicated minimum (m | m << 16) of a stored state
+    auto state_min = [&](const uint32_t (&x)[NP]) -> uint32_t {
+        uint32_t m = x[0];
+#pragma unroll
+        for (int i = 1; i < NP; i++) m = pk_min(m, x[i]);
+        m = ::min(m & 0xFFFFu, m >> 16);
+        return group_min<VL>(m) * 0x10001u;
+    };
+    uint32_t nfix = 0;
+    for (int dir = 0; dir < 2; dir++) {  // 0 = E (strips in x order), 1 = W (reverse)
+        bool same = true;  // the trusted state entering the next strip = the previous strip's stored end
+        uint32_t T[NP];
+#pragma unroll
+        for (int i = 0; i < NP; i++) T[i] = 0;
+        for (int i0 = 1; i0 < nwg; i0 += KB) {
+            RawBytes<CB> sb[KB], eb[KB];
+#pragma unroll
+            for (int kk = 0; kk < KB; kk++) {
+                const int i = i0 + kk;
+                const int k = dir ? nwg - 1 - i : i, kp = dir ? k + 1 : k - 1;
+                sb[kk].load(rs, i < nwg ? soff(k, dir, 0) : kOOB);
+                eb[kk].load(rs, i < nwg ? soff(kp, dir, 1) : kOOB);
+            }
+#pragma unroll
+            for (int kk = 0; kk < KB; kk++) {
+                const int i = i0 + kk;
+                if (i >= nwg) break;
+                const int k = dir ? nwg - 1 - i : i;
+                uint32_t S[NP], E[NP];
+                unpack_ct_pk<CT, DPL>(sb[kk], S);
+                unpack_ct_pk<CT, DPL>(eb[kk], E);
+                if (same) {
+#pragma unroll
+                    for (int q = 0; q < NP; q++) T[q] = E[q];
+                }
+                if (same_state(S, T)) {  // the speculative segment started from the true state
+                    same = true;
+                    continue;
+                }
+                // recompute strip k from T beside its speculative trajectory
+                uint32_t Lq[2][NP], mq[2];
+#pragma unroll
+                for (int q = 0; q < NP; q++) {
+                    Lq[0][q] = S[q];
+                    Lq[1][q] = T[q];
+                }
+                mq[0] = state_min(Lq[0]);
+                mq[1] = state_min(Lq[1]);
+                const int x0 = k * CW, ncol = ::min(CW, W1 - x0);  // W: every repaired strip is full
+                bool met = false;
+                for (int o = 0; o < ncol; o++) {
+                    const int c = dir ? x0 + CW - 1 - o : x0 + o;
+                    RawBytes<CB> cc;
+                    cc.load(rc, cell(c) * (uint32_t)sizeof(CT));
+                    uint32_t C2[2][NP], Ln[2][NP], mn[2];
+                    unpack_ct_pk<CT, DPL>(cc, C2[0]);
+#pragma unroll
+                    for (int q = 0; q < NP; q++) C2[1][q] = C2[0][q];
+                    sweep_step2n<VL, NP, H16, 2>(Lq, mq, C2, P1p, P2p, eL, eR, Ln, mn);
+                    if (same_state(Ln[0], Ln[1])) {
+                        met = true;
+                        break;
+                    }
+                    RawBytes<DPL * 2> pb;
+                    pb.load(rp, cell(c) * 2u);
+                    uint32_t P[NP];
+#pragma unroll
+                    for (int q = 0; q < NP; q++) {
+                        if constexpr (SAT) {
+                            uint32_t h[2];
+#pragma unroll
+                            for (int e = 0; e < 2; e++) {
+                                const uint32_t pv = (pb.w[q] >> (16 * e)) & 0xFFFFu;
+                                const uint32_t sv = (Ln[0][q] >> (16 * e)) & 0xFFFFu;
+                                const uint32_t tv = (Ln[1][q] >> (16 * e)) & 0xFFFFu;
+                                h[e] = pv == 0xFFFFu ? pv : ::min(pv - sv + tv, 0xFFFFu);
+                            }
+                            P[q] = h[0] | (h[1] << 16);
+                        } else {  // census: every sum < 2^11, the u16 wrap is exact
+                            P[q] = pk_add(pk_sub(pb.w[q], Ln[0][q]), Ln[1][q]);
+                        }
+                    }
+                    bstore_n<uint32_t, NP>(rp, cell(c) * 2u, P);
+#pragma unroll
+                    for (int q = 0; q < NP; q++) {
+                        Lq[0][q] = Ln[0][q];
+                        Lq[1][q] = Ln[1][q];
+                    }
+                    mq[0] = mn[0];
+                    mq[1] = mn[1];
+                }
+                nfix++;
+                same = met;
+                if (!met) {  // the true end state of strip k enters strip k + 1
+#pragma unroll
+                    for (int q = 0; q < NP; q++) T[q] = Lq[1][q];
+                }
+            }
+        }
+    }
+    if (a.fixes && g == 0 && nfix) atomicAdd(a.fixes, nfix);
 }
 
 }  // namespace smk

@@ -372,6 +372,26 @@ __device__ __forceinline__ void sweep_step2n(const uint32_t (&Lp)[ND][NP], const
     group_min_n<VL, ND>(mn);  // replicated halves: u32 minima are exact
 }
 
+// NP packed u16 pairs -> LT bytes at byte offset off (u8: truncating pack; u16: as is)
+template <typename LT, int NP, int AUX = 0>
+__device__ __forceinline__ void store_pk(rsrc_t r, uint32_t off, const uint32_t (&w)[NP])
+{
+    if constexpr (sizeof(LT) == 2) {
+        bstore_n<uint32_t, NP, AUX>(r, off, w);
+    } else {
+        constexpr int NW = NP / 2;
+        if constexpr (NW > 0) {
+            uint32_t b[NW];
+#pragma unroll
+            for (int j = 0; j < NW; j++) b[j] = __builtin_amdgcn_perm(w[2 * j + 1], w[2 * j], 0x06040200u);
+            bstore_n<uint32_t, NW, AUX>(r, off, b);
+        }
+        if constexpr (NP % 2)
+            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)((w[NP - 1] & 0xFFu) | ((w[NP - 1] >> 8) & 0xFF00u)), r,
+                                                  off + 4 * NW, 0, AUX);
+    }
+}
+
 // raw cost / E / W bytes of one lane -> NP packed pairs (u16 already pairs; u8 widened)
 template <typename CT, int DPL>
 __device__ __forceinline__ void unpack_ct_pk(const RawBytes<DPL * (int)sizeof(CT)>& r, uint32_t (&C)[DPL / 2])

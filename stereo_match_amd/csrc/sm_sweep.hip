@@ -72,6 +72,19 @@ constexpr int unit_ncw()
     return SWEEP_WIDE ? wide_ncw(D, (int)sizeof(CT)) : kNarrowNcw;
 }
 
+// MODES 3 and 4 (in-kernel E/W lines, then the WTA sweep over their partial) exist only for the
+// packed row loops (even DPL), MODE 3 where its line waves and LDS ring fit the workgroup
+template <int VL, int DPL, typename CT, int MODE>
+constexpr bool unit_built()
+{
+    constexpr int NCW = unit_ncw<VL * DPL, CT>();
+    if constexpr (NCW == 0) return false;
+    else if constexpr (MODE < 3) return true;
+    else if constexpr (DPL % 2 != 0 || SWEEP_U32) return false;
+    else if constexpr (MODE == 3) return LineGeo<VL, DPL, NCW, 3>::BUILT;
+    else return true;
+}
+
 struct InfoF {
     int device;
     SweepInfo* out;
@@ -79,15 +92,16 @@ struct InfoF {
     hipError_t run()
     {
         constexpr int NCW = unit_ncw<VL * DPL, CT>();
-        if constexpr (NCW == 0) {
+        if constexpr (!unit_built<VL, DPL, CT, MODE>()) {
             return hipErrorInvalidValue;
         } else {
             using SG = SweepGeo<VL, DPL, NCW>;
+            constexpr int THREADS = sweep_threads<VL, DPL, NCW, MODE>();
             auto kern = k_sweep<VL, DPL, CT, MODE, NCW>;
             static int per_cu = -1;  // per instance (one device type per process)
             if (per_cu < 0) {
                 int nb = 0;
-                if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, SG::THREADS, 0) != hipSuccess) nb = 0;
+                if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, THREADS, 0) != hipSuccess) nb = 0;
                 // a wide instance is used only if it runs without scratch and fits a CU
                 hipFuncAttributes fa{};
                 if (SWEEP_WIDE && (hipFuncGetAttributes(&fa, (const void*)kern) != hipSuccess || fa.localSizeBytes > 0))
@@ -98,10 +112,11 @@ struct InfoF {
             out->cw = SG::CW;
             out->hb = SG::HB;
             out->ngr = SG::SNG;
-            out->threads = SG::THREADS;
+            out->threads = THREADS;
             out->blocks_per_cu = per_cu;
             out->impl = SWEEP_WIDE == 2 ? 2 : SWEEP_WIDE ? 1 : 0;
             out->dpl = DPL;
+            out->ncw = NCW;
             return hipSuccess;
         }
     }
@@ -115,17 +130,17 @@ struct LaunchF {
     hipError_t run()
     {
         constexpr int NCW = unit_ncw<VL * DPL, CT>();
-        if constexpr (NCW == 0) {
+        if constexpr (!unit_built<VL, DPL, CT, MODE>()) {
             return hipErrorInvalidValue;
         } else {
-            hipLaunchKernelGGL((k_sweep<VL, DPL, CT, MODE, NCW>), grid, dim3(SweepGeo<VL, DPL, NCW>::THREADS), 0,
+            hipLaunchKernelGGL((k_sweep<VL, DPL, CT, MODE, NCW>), grid, dim3(sweep_threads<VL, DPL, NCW, MODE>()), 0,
                                stream, *a);
             return hipGetLastError();
         }
     }
 };
 
-#if !SWEEP_WIDE && SM_ABLATIONS
+#if !SWEEP_WIDE && SM_ABLATIONS && SWEEP_MODE <= 2
 
 // column-per-lane sweeps (sm_sweep2.hpp, a measured ablation): built for u8 (census) costs
 // at D = 128; variant = compute waves per workgroup: 3 (16 columns per wave), 6 (8 columns)
@@ -150,6 +165,7 @@ hipError_t sweep2_run(bool info, int device, SweepInfo* out, const SweepArgs* a,
         out->blocks_per_cu = per_cu;
         out->impl = NW;
         out->dpl = 128 / 64;
+        out->ncw = NW;
         return hipSuccess;
     }
     hipLaunchKernelGGL(kern, dim3(a->nwg, npairs), dim3(SG::THREADS), 0, stream, *a);
@@ -175,7 +191,7 @@ hipError_t sweep2(int D, int ct_bytes, int variant, bool info, int device, Sweep
     }
 }
 
-#endif  // !SWEEP_WIDE && SM_ABLATIONS
+#endif  // !SWEEP_WIDE && SM_ABLATIONS && SWEEP_MODE <= 2
 
 }  // namespace
 
@@ -211,7 +227,7 @@ hipError_t SW_CAT(sweep_launch_wide_m, SWEEP_MODE)(int D, int ct_bytes, const Sw
 #else
 hipError_t SW_CAT(sweep_info_m, SWEEP_MODE)(int D, int ct_bytes, int variant, int device, SweepInfo* out)
 {
-#if SM_ABLATIONS
+#if SM_ABLATIONS && SWEEP_MODE <= 2
     if (variant && sweep2(D, ct_bytes, variant, true, device, out, nullptr, 0, nullptr) == hipSuccess)
         return hipSuccess;
 #else
@@ -224,7 +240,7 @@ hipError_t SW_CAT(sweep_info_m, SWEEP_MODE)(int D, int ct_bytes, int variant, in
 hipError_t SW_CAT(sweep_launch_m, SWEEP_MODE)(int D, int ct_bytes, int variant, const SweepArgs& a, int npairs,
                                               hipStream_t stream)
 {
-#if SM_ABLATIONS
+#if SM_ABLATIONS && SWEEP_MODE <= 2
     if (variant) {
         const hipError_t e = sweep2(D, ct_bytes, variant, false, 0, nullptr, &a, npairs, stream);
         if (e != hipErrorInvalidValue) return e;

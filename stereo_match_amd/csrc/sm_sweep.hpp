@@ -171,6 +171,43 @@ constexpr int wide_ncw(int D, int ct_bytes)
     return (D == 48 || D == 80 || D == 128 || D == 160) ? 11 : 0;
 }
 
+// ---- MODE 3: the horizontal paths inside the down sweep.  NLW extra
+// waves per workgroup run each row's E and W lines over the strip's own columns, starting
+// `ewarm` columns outside the strip from the zero state (a speculation: exact once the line's
+// state has met the true one), and leave E + W per own column in an LDS ring of LR rows that
+// the own waves add into the partial.  A line wave's batch t covers RPW rows (an E and a W
+// line each); the waves take part in the compute waves' two barriers per block of HB rows,
+// running at most LEAD rows ahead of the block those waves are in.  Deadlock-free for
+// LR >= LEAD + RPW: before a line wave's barrier pair b it has produced every row below
+// (b + 1) * HB + LEAD, for which it needed rows up to (b + 1) * HB + LEAD + RPW - 1 - LR <=
+// (b + 1) * HB - 2 consumed, all of which the compute waves consume before that barrier.
+#ifndef SWEEP_NLW
+#define SWEEP_NLW 4  // line waves per workgroup (one per SIMD)
+#endif
+#ifndef SWEEP_LINE_PRIO
+#define SWEEP_LINE_PRIO 2  // issue priority of the line waves (compute waves: 3 on the hand-off chain, else 1)
+#endif
+constexpr int kMaxLds = 163840;  // gfx950: LDS one workgroup may declare
+template <int VL, int DPL, int NCW_, int MODE>
+struct LineGeo {
+    using G = SweepGeo<VL, DPL, NCW_>;
+    static constexpr bool ON = MODE == 3;
+    // at most 16 waves per workgroup (1024 threads): compute waves + poller + lines
+    static constexpr int NLW = !ON ? 0 : (SWEEP_NLW < 15 - NCW_ ? SWEEP_NLW : 15 - NCW_);
+    static constexpr int RPW = G::LPW / 2;  // rows per line wave and batch
+    // LDS besides the ring: lv, lmin, the counters, a margin
+    static constexpr int BASE = 8 * G::COLS * G::D + 16 * G::COLS + 4 * NCW_ + 4 * 16 + 512;
+    static constexpr int ROWB = G::CW * G::D * 2;  // ring row: u16 E + W sums of the own columns
+    static constexpr int FIT = (kMaxLds - BASE) / ROWB;
+    static constexpr int LEAD0 = RPW * (G::HB / 2 / RPW > 0 ? G::HB / 2 / RPW : 1);
+    static constexpr int LEAD = LEAD0 + RPW <= FIT ? LEAD0 : (FIT > RPW ? (FIT - RPW) / RPW * RPW : 0);
+    static constexpr int LR = LEAD + 2 * RPW <= FIT ? LEAD + 2 * RPW : LEAD + RPW;
+    static constexpr bool BUILT = ON && NLW >= 1 && DPL % 2 == 0 && !SWEEP_U32 && LEAD + RPW <= FIT &&
+                                  G::CW % 2 == 0 && G::HB % RPW == 0 && RPW >= 1;
+};
+template <int VL, int DPL, int NCW_, int MODE>
+constexpr int sweep_threads() { return SweepGeo<VL, DPL, NCW_>::THREADS + 64 * LineGeo<VL, DPL, NCW_, MODE>::NLW; }
+
 // NP packed words of one lane <-> LDS (widest aligned chunks)
 template <int NP>
 __device__ __forceinline__ void lds_get_pk(const uint16_t* p, uint32_t (&v)[NP])
@@ -339,11 +376,18 @@ __device__ __forceinline__ void poll_granules(const gu64* src, bool need, uint32
 }
 
 template <int VL, int DPL, typename CT, int MODE, int NCW_ = kNarrowNcw>
-__global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(SweepArgs a)
+__global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_sweep(SweepArgs a)
 {
     using G = SweepGeo<VL, DPL, NCW_>;
-    constexpr bool UP = MODE == 2;
-    constexpr bool WTA = MODE != 0;
+    using LG = LineGeo<VL, DPL, NCW_, MODE>;
+    constexpr bool UP = MODE == 2 || MODE == 4;
+    constexpr bool WTA = MODE == 1 || MODE == 2 || MODE == 4;
+    constexpr bool EWIN = MODE == 1 || MODE == 2;   // E / W path volumes read (k_ew)
+    constexpr bool PARTR = MODE == 2 || MODE == 4;  // the down sweep's partial read
+    constexpr bool LINES = MODE == 3;               // E / W lines in the kernel (line waves)
+    static_assert(!LINES || LG::BUILT, "MODE 3 instance not built for this geometry");
+    static_assert(MODE < 3 || (DPL % 2 == 0 && !SWEEP_U32), "MODES 3 / 4 run the packed row loops only");
+    constexpr int NTH = sweep_threads<VL, DPL, NCW_, MODE>();
     // the down sweep shares its SIMDs with the E/W kernel (8 paths): its waves take issue
     // priority, the E/W waves fill the cycles it leaves (SWEEP_PRIO 0 = default priority)
 #ifndef SWEEP_PRIO
@@ -365,6 +409,7 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
 #define SWEEP_ROWSYNC_M1 0
 #endif
     constexpr bool ROWSYNC = SWEEP_ROW_SYNC && (MODE != 1 || SWEEP_ROWSYNC_M1);
+    static_assert(!LINES || ROWSYNC, "the line waves mirror the row-synchronised barrier pattern");
     constexpr int LPW = G::LPW, NCW = G::NCW, HB = G::HB, NCOL = G::NCOL, COLS = G::COLS, CW = G::CW, D = G::D;
     constexpr int NG = G::NG, SNG = G::SNG, PF = G::PF, HM = G::HM, HW = G::HW;
     constexpr int CB = DPL * (int)sizeof(CT);  // cost / E / W bytes per lane and cell
@@ -376,11 +421,17 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
     // rows whose LDS state each compute wave has published (inside a block of HB rows the
     // waves synchronise with their two neighbours only; SWEEP_ROW_SYNC)
     __shared__ uint32_t rowcnt[NCW];
+    // MODE 3: E + W of the own columns for LR rows; batches each line wave has completed;
+    // rows each own wave has consumed from the ring
+    __shared__ __attribute__((aligned(16))) uint16_t ring[LINES ? LG::LR : 1][LINES ? CW : 1][LINES ? D : 2];
+    __shared__ uint32_t linecnt[LINES ? LG::NLW : 1], conscnt[NCW];
 
-    for (int i = threadIdx.x; i < 2 * 2 * COLS * D / 2; i += G::THREADS)
+    for (int i = threadIdx.x; i < 2 * 2 * COLS * D / 2; i += NTH)
         reinterpret_cast<uint32_t*>(&lv[0][0][0][0])[i] = 0;
-    for (int i = threadIdx.x; i < 2 * 2 * COLS; i += G::THREADS) (&lmin[0][0][0])[i] = 0;
-    for (int i = threadIdx.x; i < NCW; i += G::THREADS) rowcnt[i] = 0;
+    for (int i = threadIdx.x; i < 2 * 2 * COLS; i += NTH) (&lmin[0][0][0])[i] = 0;
+    for (int i = threadIdx.x; i < NCW; i += NTH) rowcnt[i] = conscnt[i] = 0;
+    if constexpr (LINES)
+        for (int i = threadIdx.x; i < LG::NLW; i += NTH) linecnt[i] = 0;
     __syncthreads();
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -485,6 +536,137 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
         return;
     }
 
+    if constexpr (LINES) {
+        if (wave > NCW) {
+            // ---- line waves (MODE 3): line kl of the wave (VL lanes, DPL disparities per lane)
+            // runs direction kl & 1 (0 = E, x ascending; 1 = W) of row y0 + (kl >> 1), over the
+            // strip's own columns plus `ewarm` columns before them in its direction, from the
+            // zero state.  Own column o gets E + W in ring[y % LR][o]; the state entering the
+            // strip and the state at its far end go to the boundary-state buffer (k_ew_patch
+            // checks them against the neighbours' and repairs the partial where they differ).
+            constexpr int NLW = LG::NLW, RPW = LG::RPW, LR = LG::LR, LEAD = LG::LEAD;
+            constexpr int NP = DPL / 2;
+            constexpr int CB = DPL * (int)sizeof(CT);
+            constexpr bool H16 = sizeof(CT) == 1 && SWEEP_H16;
+            constexpr uint32_t EDGE2 = H16 ? 0x7BFF7BFFu : (kBig | (kBig << 16));
+            constexpr int LPF = 8;  // cost loads in flight per lane
+            const int li = wave - NCW - 1;
+            const int kl = lane / VL, g = lane % VL;
+            const int dir = kl & 1, r = kl >> 1;
+            const int H = a.H, W1 = a.W1, x0 = wg * CW;
+            const int w = a.ewarm, nsteps = w + CW;
+            const uint32_t P1p = (uint32_t)a.P1 * 0x10001u, P2p = (uint32_t)a.P2 * 0x10001u;
+            const uint32_t eL = g == 0 ? EDGE2 : 0u, eR = g == VL - 1 ? EDGE2 : 0u;
+            const uint64_t cells = (uint64_t)H * W1 * D;
+            const rsrc_t rc = make_rsrc(a.cost + (size_t)pair * a.cost_pair, cells * sizeof(CT));
+            const rsrc_t rs = make_rsrc(a.st + (size_t)pair * a.st_pair, a.st_pair);
+            const int c0 = dir ? x0 + CW - 1 + w : x0 - w, cs = dir ? -1 : 1;  // column of step j: c0 + cs * j
+            __builtin_amdgcn_s_setprio(SWEEP_LINE_PRIO);
+            int bn = 0;  // barrier pairs passed (the compute waves' two per block of HB rows)
+            auto barriers_to = [&](int y0) {
+                while (bn < nblk && (bn + 1) * HB + LEAD <= y0) {
+                    if (!(a.dbg & 4)) lds_barrier();
+                    if (bn + 1 < nblk) lds_barrier();
+                    bn++;
+                }
+            };
+            // every own wave has consumed the rows below `need` from the ring
+            auto wait_cons = [&](int need) {
+                if (need <= 0) return;
+                for (uint32_t spins = 0;; spins++) {
+                    uint32_t m = 0xFFFFFFFFu;
+#pragma unroll
+                    for (int w2 = 1; w2 <= NCW - 2; w2++)
+                        m = min(m, __hip_atomic_load(&conscnt[w2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+                    m = __builtin_amdgcn_readfirstlane(m);
+                    if (m >= (uint32_t)need) {
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+                        return;
+                    }
+                    if (spins >= SW_SPIN_LIMIT) {  // never expected: report; the guarded fallback recomputes
+                        if (lane == 0) atomicOr(a.err, 1u);
+                        return;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            };
+            for (int t = 0;; t++) {
+                const int y0 = (t * NLW + li) * RPW;
+                if (y0 >= H) break;
+                barriers_to(y0);
+                wait_cons(y0 + RPW - LR);
+                const int y = y0 + r;
+                const bool yl = y < H;
+                uint16_t* rrow = &ring[yl ? y % LR : 0][0][g * DPL];
+                auto coff = [&](int j) -> uint32_t {
+                    const int c = c0 + cs * j;
+                    return yl && j < nsteps && c >= 0 && c < W1
+                               ? (((uint32_t)y * (uint32_t)W1 + (uint32_t)c) * (uint32_t)D + (uint32_t)(g * DPL)) *
+                                     (uint32_t)sizeof(CT)
+                               : kOOB;
+                };
+                // boundary states of (y, strip, dir): [0] entering the strip, [1] at its far end
+                const uint32_t so = yl ? ((((uint32_t)y * (uint32_t)a.nwg + (uint32_t)wg) * 2u + (uint32_t)dir) * 2u *
+                                              (uint32_t)D + (uint32_t)(g * DPL)) * (uint32_t)sizeof(CT)
+                                       : kOOB;
+                RawBytes<CB> cr[LPF];
+#pragma unroll
+                for (int k = 0; k < LPF; k++) {
+                    cr[k].load(rc, coff(k));
+                    asm volatile("" ::: "memory");  // issue order = slot order
+                }
+                uint32_t Lp[NP], mm = 0;
+#pragma unroll
+                for (int i = 0; i < NP; i++) Lp[i] = 0;
+                for (int j0 = 0; j0 < nsteps; j0 += LPF) {
+#pragma unroll
+                    for (int k = 0; k < LPF; k++) {
+                        const int j = j0 + k;
+                        if (j >= nsteps) break;
+                        // the slot is read after the previous step and unpacked before its refill
+                        // is issued (sm_ew.hpp k_ew)
+#pragma unroll
+                        for (int q = 0; q < RawBytes<CB>::WORDS; q++) asm volatile("" : "+v"(cr[k].w[q]) : "v"(mm));
+                        uint32_t C[1][NP];
+                        unpack_ct_pk<CT, DPL>(cr[k], C[0]);
+#pragma unroll
+                        for (int i = 0; i < NP; i++) asm volatile("" : "+v"(C[0][i])::"memory");
+                        cr[k].load(rc, coff(j + LPF));
+                        uint32_t Lq[1][NP], mq[1] = {mm}, Ln[1][NP], mn[1];
+#pragma unroll
+                        for (int i = 0; i < NP; i++) Lq[0][i] = Lp[i];
+                        sweep_step2n<VL, NP, H16, 1>(Lq, mq, C, P1p, P2p, eL, eR, Ln, mn);
+                        if (j == w - 1) store_pk<CT, NP>(rs, so, Ln[0]);  // the state entering the strip
+                        if (j >= w && yl) {
+                            const int h = j - w;
+                            const int o = dir ? CW - 1 - h : h;
+                            uint32_t v[NP];
+                            if (2 * h >= CW) {  // the other direction's line wrote this column first
+                                uint32_t old[NP];
+                                lds_get_pk<NP>(rrow + o * D, old);
+#pragma unroll
+                                for (int i = 0; i < NP; i++) v[i] = pk_add(old[i], Ln[0][i]);
+                            } else {
+#pragma unroll
+                                for (int i = 0; i < NP; i++) v[i] = Ln[0][i];
+                            }
+                            lds_put_pk<NP>(rrow + o * D, v);
+                        }
+                        if (j == nsteps - 1) store_pk<CT, NP>(rs, yl ? so + (uint32_t)(D * sizeof(CT)) : kOOB, Ln[0]);
+#pragma unroll
+                        for (int i = 0; i < NP; i++) Lp[i] = Ln[0][i];
+                        mm = mn[0];
+                    }
+                }
+                // the batch's ring rows are complete (LDS only: the state stores need no ordering)
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+                __hip_atomic_store(&linecnt[li], (uint32_t)(t + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            barriers_to(0x7FFFFFFF);
+            return;
+        }
+    }
+
     // ---- compute waves
     const int kl = lane / VL, g = lane % VL;
     // column slot among the compute waves (halo waves: of their first column set)
@@ -532,6 +714,28 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
         wait_row_spin(s);
         SW_ACC(st_wait, tw);
     };
+    // MODE 3: row s of the ring is complete (its line wave has finished the batch holding it)
+    auto wait_lines = [&](int s) {
+        if constexpr (LINES) {
+            const int li = (s / LG::RPW) % LG::NLW;
+            const uint32_t need = (uint32_t)(s / (LG::RPW * LG::NLW) + 1);
+            for (uint32_t spins = 0;; spins++) {
+                const uint32_t nd = __builtin_amdgcn_readfirstlane(
+                    __hip_atomic_load(&linecnt[li], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+                if (nd >= need) {
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+                    return;
+                }
+                if (spins >= SW_SPIN_LIMIT) {  // never expected: report, the guarded fallback recomputes
+                    if (lane == 0) atomicOr(a.err, 1u);
+                    return;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        } else {
+            (void)s;
+        }
+    };
     auto end_row = [&](int j, int s) {
         if (!ROWSYNC || j == HB - 1) {
             if (!(a.dbg & 4)) lds_barrier();
@@ -543,9 +747,11 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
     const uint64_t cells = (uint64_t)H * W1 * D;
     const rsrc_t rc = make_rsrc(a.cost + (size_t)pair * a.cost_pair, cells * sizeof(CT));
     rsrc_t re = make_rsrc(nullptr, 0), rw = re, rp = re, rrec = re, rnb = re;
-    if constexpr (WTA) {
+    if constexpr (EWIN) {
         re = make_rsrc(a.ew + (size_t)pair * a.ew_pair, cells * sizeof(CT));
         rw = make_rsrc(a.ew + (size_t)pair * a.ew_pair + a.ew_slot, cells * sizeof(CT));
+    }
+    if constexpr (WTA) {
         rrec = make_rsrc(a.rec + (size_t)pair * H * a.W, (uint64_t)H * a.W * 4);
         rnb = make_rsrc(a.nb + (size_t)pair * H * a.W, (uint64_t)H * a.W * 4);
     }
@@ -575,11 +781,11 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
         const uint32_t en = s < H ? cell(UP ? H - 1 - s : s) : NONE;
         const uint32_t eo = own ? en : NONE;
         rc_[k].template load<WTA ? SWEEP_COST_AUX : 0>(rc, boff(en, sizeof(CT)));
-        if constexpr (WTA) {
+        if constexpr (EWIN) {
             re_[k].template load<SWEEP_STREAM_AUX>(re, boff(eo, sizeof(CT)));
             rw_[k].template load<SWEEP_STREAM_AUX>(rw, boff(eo, sizeof(CT)));
         }
-        if constexpr (MODE == 2) rp_[k].template load<SWEEP_STREAM_AUX>(rp, boff(eo, 2));
+        if constexpr (PARTR) rp_[k].template load<SWEEP_STREAM_AUX>(rp, boff(eo, 2));
     };
     if constexpr (DPL % 2 == 0 && !SWEEP_U32) {
         // ---- packed u16-pair form (same steps as the u32 loop below), one straight-line
@@ -618,12 +824,12 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
 #pragma unroll
                 for (int h = 0; h < NS; h++)
                     rcs[k][h].template load<WTA ? SWEEP_COST_AUX : 0>(rc, boff(s < H ? cell_h(h, yy) : NONE, sizeof(CT)));
-                if constexpr (OWN && WTA) {
+                if constexpr (OWN && EWIN) {
                     const uint32_t en = s < H ? cell(yy) : NONE;
                     re_[k].template load<SWEEP_STREAM_AUX>(re, boff(en, sizeof(CT)));
                     rw_[k].template load<SWEEP_STREAM_AUX>(rw, boff(en, sizeof(CT)));
                 }
-                if constexpr (OWN && MODE == 2) rp_[k].template load<SWEEP_STREAM_AUX>(rp, boff(s < H ? cell(yy) : NONE, 2));
+                if constexpr (OWN && PARTR) rp_[k].template load<SWEEP_STREAM_AUX>(rp, boff(s < H ? cell(yy) : NONE, 2));
             };
 #pragma unroll
             for (int k = 0; k < PF; k++) issue_r(k, k);
@@ -649,17 +855,17 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
                     uint32_t C[NS][NP], Ein[NP], Win[NP], Pin[NP];
 #pragma unroll
                     for (int h = 0; h < NS; h++) unpack_ct_pk<CT, DPL>(rcs[k][h], C[h]);
-                    if constexpr (OWN && WTA) {
+                    if constexpr (OWN && EWIN) {
                         unpack_ct_pk<CT, DPL>(re_[k], Ein);
                         unpack_ct_pk<CT, DPL>(rw_[k], Win);
                     }
-                    if constexpr (OWN && MODE == 2) unpack_ct_pk<uint16_t, DPL>(rp_[k], Pin);
+                    if constexpr (OWN && PARTR) unpack_ct_pk<uint16_t, DPL>(rp_[k], Pin);
 #pragma unroll
                     for (int i = 0; i < NP; i++) {  // before the refill (see the u32 loop)
 #pragma unroll
                         for (int h = 0; h < NS; h++) asm volatile("" : "+v"(C[h][i])::"memory");
-                        if constexpr (OWN && WTA) asm volatile("" : "+v"(Ein[i]), "+v"(Win[i])::"memory");
-                        if constexpr (OWN && MODE == 2) asm volatile("" : "+v"(Pin[i])::"memory");
+                        if constexpr (OWN && EWIN) asm volatile("" : "+v"(Ein[i]), "+v"(Win[i])::"memory");
+                        if constexpr (OWN && PARTR) asm volatile("" : "+v"(Pin[i])::"memory");
                     }
                     issue_r(k, s + PF);
                     if (ROWSYNC && j > 0) wait_row(s);
@@ -821,6 +1027,23 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
 #pragma unroll
                             for (int i = 0; i < NP; i++) out[i] = pk_add(out[i], nB[0][i]);
                             bstore_n<uint32_t, NP, SWEEP_STREAM_AUX>(rp, boff(e, 2), out);
+                        } else if constexpr (MODE == 3) {
+                            // + E + W of this row from the line waves' ring (u16 costs: saturating,
+                            // the WTA clamps at 32767 anyway; three paths alone stay below 2^16)
+                            uint32_t out[NP], ewl[NP];
+#pragma unroll
+                            for (int i = 0; i < NP; i++) out[i] = pk_add(nV[i], nA[0][i]);
+#pragma unroll
+                            for (int i = 0; i < NP; i++) out[i] = pk_add(out[i], nB[0][i]);
+                            if (live) wait_lines(s);
+                            lds_get_pk<NP>(&ring[s % LG::LR][(wave - 1) * LPW + kl][g * DPL], ewl);
+#pragma unroll
+                            for (int i = 0; i < NP; i++) out[i] = SAT ? pk_adds(out[i], ewl[i]) : pk_add(out[i], ewl[i]);
+                            bstore_n<uint32_t, NP, SWEEP_STREAM_AUX>(rp, boff(e, 2), out);
+                            // the ring row is read (the fence waits for the LDS read): the lines may reuse it
+                            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+                            __hip_atomic_store(&conscnt[wave], (uint32_t)(s + 1), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
                         } else {
                             uint32_t Sp[NP], ew[NP];
                             // a padded cost volume (u16 costs only): its pad planes d >= Dv take
@@ -828,11 +1051,16 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
                             // below the uniqueness threshold)
                             const bool pad = SAT && a.Dv < D;  // wave-uniform
                             if constexpr (SAT) {
+                                if constexpr (EWIN) {
 #pragma unroll
-                                for (int i = 0; i < NP; i++) ew[i] = pk_adds(Ein[i], Win[i]);
-                                if constexpr (MODE == 2) {
+                                    for (int i = 0; i < NP; i++) ew[i] = pk_adds(Ein[i], Win[i]);
+                                    if constexpr (PARTR) {
 #pragma unroll
-                                    for (int i = 0; i < NP; i++) ew[i] = pk_adds(ew[i], Pin[i]);
+                                        for (int i = 0; i < NP; i++) ew[i] = pk_adds(ew[i], Pin[i]);
+                                    }
+                                } else {  // MODE 4: the partial holds E and W already
+#pragma unroll
+                                    for (int i = 0; i < NP; i++) ew[i] = Pin[i];
                                 }
 #pragma unroll
                                 for (int i = 0; i < NP; i++) Sp[i] = pk_adds(nV[i], nA[0][i]);
@@ -850,11 +1078,16 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
                                     }
                                 }
                             } else {
+                                if constexpr (EWIN) {
 #pragma unroll
-                                for (int i = 0; i < NP; i++) ew[i] = pk_add(Ein[i], Win[i]);
-                                if constexpr (MODE == 2) {
+                                    for (int i = 0; i < NP; i++) ew[i] = pk_add(Ein[i], Win[i]);
+                                    if constexpr (PARTR) {
 #pragma unroll
-                                    for (int i = 0; i < NP; i++) ew[i] = pk_add(ew[i], Pin[i]);
+                                        for (int i = 0; i < NP; i++) ew[i] = pk_add(ew[i], Pin[i]);
+                                    }
+                                } else {
+#pragma unroll
+                                    for (int i = 0; i < NP; i++) ew[i] = Pin[i];
                                 }
 #pragma unroll
                                 for (int i = 0; i < NP; i++) Sp[i] = pk_add(nV[i], nA[0][i]);
@@ -942,19 +1175,21 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
             uint32_t C[DPL];
             unpack_ct<CT, DPL>(rc_[k], C);
             uint32_t Ein[DPL], Win[DPL], Pin[DPL];
-            if constexpr (WTA) {
+#pragma unroll
+            for (int i = 0; i < DPL; i++) Ein[i] = Win[i] = Pin[i] = 0;
+            if constexpr (EWIN) {
                 unpack_ct<CT, DPL>(re_[k], Ein);
                 unpack_ct<CT, DPL>(rw_[k], Win);
             }
-            if constexpr (MODE == 2) unpack_ct<uint16_t, DPL>(rp_[k], Pin);
+            if constexpr (PARTR) unpack_ct<uint16_t, DPL>(rp_[k], Pin);
             // materialise the unpacked values before the slot is refilled: if the
             // unpack sinks below the refill, old and new slot values overlap and the
             // ring gets rotated by moves at the back-edge, which wait for the newest loads
 #pragma unroll
             for (int i = 0; i < DPL; i++) {
                 asm volatile("" : "+v"(C[i])::"memory");
-                if constexpr (WTA) asm volatile("" : "+v"(Ein[i]), "+v"(Win[i])::"memory");
-                if constexpr (MODE == 2) asm volatile("" : "+v"(Pin[i])::"memory");
+                if constexpr (EWIN) asm volatile("" : "+v"(Ein[i]), "+v"(Win[i])::"memory");
+                if constexpr (PARTR) asm volatile("" : "+v"(Pin[i])::"memory");
             }
             issue(k, s + PF);
 
@@ -1026,7 +1261,7 @@ __global__ void __launch_bounds__((SweepGeo<VL, DPL, NCW_>::THREADS)) k_sweep(Sw
 #pragma unroll
                     for (int i = 0; i < DPL; i++) {
                         uint32_t t = nV[i] + nA[i] + nB[i] + Ein[i] + Win[i];
-                        if constexpr (MODE == 2) t += Pin[i];
+                        if constexpr (PARTR) t += Pin[i];
                         if constexpr (sizeof(CT) == 2) t = min(t, 32767u);  // census sums stay below 2^11
                         if (pad && g * DPL + i >= a.Dv) t = 0xFFFFu;  // pad plane: never the minimum
                         S[i] = t;

@@ -8,6 +8,9 @@ namespace smk {
 // MODE: 0 = down sweep writing the u16 partial (8 paths, first pass)
 //       1 = down sweep + E/W + WTA (MODE_SGBM: 5 paths)
 //       2 = up sweep + E/W + down partial + WTA (8 paths, second pass)
+//       3 = down sweep + in-kernel E/W lines (speculative strip segments)
+//           writing the u16 partial S + SE + SW + E + W and the segments' boundary states
+//       4 = up sweep + partial + WTA (8 paths, second pass after MODE 3: no E/W volumes)
 #ifndef SWEEP_STATS
 #define SWEEP_STATS 0  // sm_sweep.hpp: wait-cycle counters (variant builds)
 #endif
@@ -31,6 +34,12 @@ struct SweepArgs {
     uint32_t epoch;  // 1..65535, distinct from the previous launches on the same hop buffer
     int dbg;         // timing ablations only: 1 no waiting in the halo polls, 2 no polls, 4 no row barriers
     unsigned long long* stats;  // SWEEP_STATS builds only: per-mode wait-cycle counters (else null)
+    // MODE 3: each strip's E and W line segments start `ewarm` (>= 1) columns outside the strip
+    // from the zero state; their state entering the strip and at its far end go to
+    // st[pair][y][strip][dir][2][D] (CT elements) for the patch pass (k_ew_patch)
+    uint8_t* st;
+    size_t st_pair;  // bytes
+    int ewarm;
 };
 
 
@@ -42,6 +51,7 @@ struct SweepInfo {
     int blocks_per_cu;  // occupancy API answer for that block size
     int impl;           // kernel: 0 k_sweep narrow strips, 1 wide strips, 2 latency strips, 3 / 6 k_sweep2
     int dpl;            // disparities per lane (the per-wave work of a row scales with it)
+    int ncw;            // compute waves (the threads also count the poller and MODE 3's line waves)
 };
 
 template <typename CT, int MODE, class F>
@@ -55,54 +65,67 @@ hipError_t with_d(int D, F& f);
 hipError_t sweep_info_m0(int D, int ct_bytes, int variant, int device, SweepInfo* out);
 hipError_t sweep_info_m1(int D, int ct_bytes, int variant, int device, SweepInfo* out);
 hipError_t sweep_info_m2(int D, int ct_bytes, int variant, int device, SweepInfo* out);
+hipError_t sweep_info_m3(int D, int ct_bytes, int variant, int device, SweepInfo* out);
+hipError_t sweep_info_m4(int D, int ct_bytes, int variant, int device, SweepInfo* out);
 hipError_t sweep_info_wide_m0(int D, int ct_bytes, int device, SweepInfo* out);
 hipError_t sweep_info_wide_m1(int D, int ct_bytes, int device, SweepInfo* out);
 hipError_t sweep_info_wide_m2(int D, int ct_bytes, int device, SweepInfo* out);
+hipError_t sweep_info_wide_m3(int D, int ct_bytes, int device, SweepInfo* out);
+hipError_t sweep_info_wide_m4(int D, int ct_bytes, int device, SweepInfo* out);
 hipError_t sweep_info_lat_m0(int D, int ct_bytes, int device, SweepInfo* out);
 hipError_t sweep_info_lat_m1(int D, int ct_bytes, int device, SweepInfo* out);
 hipError_t sweep_info_lat_m2(int D, int ct_bytes, int device, SweepInfo* out);
+hipError_t sweep_info_lat_m3(int D, int ct_bytes, int device, SweepInfo* out);
+hipError_t sweep_info_lat_m4(int D, int ct_bytes, int device, SweepInfo* out);
 hipError_t sweep_launch_lat_m0(int D, int ct_bytes, const SweepArgs& a, int npairs, hipStream_t stream);
 hipError_t sweep_launch_lat_m1(int D, int ct_bytes, const SweepArgs& a, int npairs, hipStream_t stream);
 hipError_t sweep_launch_lat_m2(int D, int ct_bytes, const SweepArgs& a, int npairs, hipStream_t stream);
+hipError_t sweep_launch_lat_m3(int D, int ct_bytes, const SweepArgs& a, int npairs, hipStream_t stream);
+hipError_t sweep_launch_lat_m4(int D, int ct_bytes, const SweepArgs& a, int npairs, hipStream_t stream);
 // grid (a.nwg, npairs), SweepInfo::threads threads
 hipError_t sweep_launch_m0(int D, int ct_bytes, int variant, const SweepArgs& a, int npairs, hipStream_t stream);
 hipError_t sweep_launch_m1(int D, int ct_bytes, int variant, const SweepArgs& a, int npairs, hipStream_t stream);
 hipError_t sweep_launch_m2(int D, int ct_bytes, int variant, const SweepArgs& a, int npairs, hipStream_t stream);
+hipError_t sweep_launch_m3(int D, int ct_bytes, int variant, const SweepArgs& a, int npairs, hipStream_t stream);
+hipError_t sweep_launch_m4(int D, int ct_bytes, int variant, const SweepArgs& a, int npairs, hipStream_t stream);
 hipError_t sweep_launch_wide_m0(int D, int ct_bytes, const SweepArgs& a, int npairs, hipStream_t stream);
 hipError_t sweep_launch_wide_m1(int D, int ct_bytes, const SweepArgs& a, int npairs, hipStream_t stream);
 hipError_t sweep_launch_wide_m2(int D, int ct_bytes, const SweepArgs& a, int npairs, hipStream_t stream);
+hipError_t sweep_launch_wide_m3(int D, int ct_bytes, const SweepArgs& a, int npairs, hipStream_t stream);
+hipError_t sweep_launch_wide_m4(int D, int ct_bytes, const SweepArgs& a, int npairs, hipStream_t stream);
 
 inline hipError_t sweep_info(int D, int ct_bytes, int mode, int variant, int device, SweepInfo* out)
 {
-    if (variant == 2)  // latency instances (kLatNcw compute waves)
-        return mode == 0 ? sweep_info_lat_m0(D, ct_bytes, device, out)
-             : mode == 1 ? sweep_info_lat_m1(D, ct_bytes, device, out)
-                         : sweep_info_lat_m2(D, ct_bytes, device, out);
+    typedef hipError_t (*InfoW)(int, int, int, SweepInfo*);
+    typedef hipError_t (*InfoV)(int, int, int, int, SweepInfo*);
+    static const InfoW lat[5] = {sweep_info_lat_m0, sweep_info_lat_m1, sweep_info_lat_m2, sweep_info_lat_m3,
+                                 sweep_info_lat_m4};
+    static const InfoW wide[5] = {sweep_info_wide_m0, sweep_info_wide_m1, sweep_info_wide_m2, sweep_info_wide_m3,
+                                  sweep_info_wide_m4};
+    static const InfoV narrow[5] = {sweep_info_m0, sweep_info_m1, sweep_info_m2, sweep_info_m3, sweep_info_m4};
+    if (mode < 0 || mode > 4) return hipErrorInvalidValue;
+    if (variant == 2) return lat[mode](D, ct_bytes, device, out);  // latency instances (kLatNcw compute waves)
     if (variant == 0) {
-        const hipError_t e = mode == 0 ? sweep_info_wide_m0(D, ct_bytes, device, out)
-                           : mode == 1 ? sweep_info_wide_m1(D, ct_bytes, device, out)
-                                       : sweep_info_wide_m2(D, ct_bytes, device, out);
+        const hipError_t e = wide[mode](D, ct_bytes, device, out);
         if (e == hipSuccess) return e;
     }
-    const int v = variant == 1 ? 0 : variant;
-    return mode == 0 ? sweep_info_m0(D, ct_bytes, v, device, out)
-         : mode == 1 ? sweep_info_m1(D, ct_bytes, v, device, out)
-                     : sweep_info_m2(D, ct_bytes, v, device, out);
+    return narrow[mode](D, ct_bytes, variant == 1 ? 0 : variant, device, out);
 }
 inline hipError_t sweep_launch(int D, int ct_bytes, int mode, int impl, const SweepArgs& a, int npairs,
                                hipStream_t stream)
 {
-    if (impl == 2)
-        return mode == 0 ? sweep_launch_lat_m0(D, ct_bytes, a, npairs, stream)
-             : mode == 1 ? sweep_launch_lat_m1(D, ct_bytes, a, npairs, stream)
-                         : sweep_launch_lat_m2(D, ct_bytes, a, npairs, stream);
-    if (impl == 1)
-        return mode == 0 ? sweep_launch_wide_m0(D, ct_bytes, a, npairs, stream)
-             : mode == 1 ? sweep_launch_wide_m1(D, ct_bytes, a, npairs, stream)
-                         : sweep_launch_wide_m2(D, ct_bytes, a, npairs, stream);
-    return mode == 0 ? sweep_launch_m0(D, ct_bytes, impl, a, npairs, stream)
-         : mode == 1 ? sweep_launch_m1(D, ct_bytes, impl, a, npairs, stream)
-                     : sweep_launch_m2(D, ct_bytes, impl, a, npairs, stream);
+    typedef hipError_t (*LaunchW)(int, int, const SweepArgs&, int, hipStream_t);
+    typedef hipError_t (*LaunchV)(int, int, int, const SweepArgs&, int, hipStream_t);
+    static const LaunchW lat[5] = {sweep_launch_lat_m0, sweep_launch_lat_m1, sweep_launch_lat_m2, sweep_launch_lat_m3,
+                                   sweep_launch_lat_m4};
+    static const LaunchW wide[5] = {sweep_launch_wide_m0, sweep_launch_wide_m1, sweep_launch_wide_m2,
+                                    sweep_launch_wide_m3, sweep_launch_wide_m4};
+    static const LaunchV narrow[5] = {sweep_launch_m0, sweep_launch_m1, sweep_launch_m2, sweep_launch_m3,
+                                      sweep_launch_m4};
+    if (mode < 0 || mode > 4) return hipErrorInvalidValue;
+    if (impl == 2) return lat[mode](D, ct_bytes, a, npairs, stream);
+    if (impl == 1) return wide[mode](D, ct_bytes, a, npairs, stream);
+    return narrow[mode](D, ct_bytes, impl, a, npairs, stream);
 }
 // sub-pixel + disp2 + disp12MaxDiff check from the WTA sweep's records, one row per workgroup;
 // wta (may be null): the integer WTA index [pair][H][W] (-1: rejected / outside the domain);
@@ -124,5 +147,22 @@ struct EwArgs {
 // lanes per line: vl = 4, 8 or 16 (0 = the default for D); hipErrorInvalidValue when
 // (D, ct_bytes, vl) is not built.  LT = CT (u8 census costs -> u8 volumes, u16 -> u16).
 hipError_t ew_launch(int D, int ct_bytes, int vl, EwArgs a, int npairs, hipStream_t stream);
+
+// Patch pass after a MODE 3 sweep (sm_ew.hpp k_ew_patch): per image row, every strip's
+// speculative E / W segment is checked against the trusted state its neighbour hands over;
+// where they differ the segment is recomputed from the trusted state and the partial
+// corrected until the two trajectories meet
+struct EwPatchArgs {
+    const uint8_t* cost;  // [pair][H][W1][D] of CT
+    size_t cost_pair;     // bytes
+    uint16_t* part;       // [pair][H][W1][D] u16 partial written by MODE 3
+    size_t part_pair;     // bytes
+    const uint8_t* st;    // MODE 3 boundary states [pair][H][nwg][2][2][D] of CT
+    size_t st_pair;       // bytes
+    int H, W1, nwg, cw, P1, P2;
+    const uint32_t* guard;  // the group's give-up flag: nothing to patch when set (the fallback recomputes)
+    uint32_t* fixes;        // strip segments recomputed (device counter, atomic)
+};
+hipError_t ew_patch_launch(int D, int ct_bytes, const EwPatchArgs& a, int npairs, hipStream_t stream);
 
 }  // namespace smk

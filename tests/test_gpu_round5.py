@@ -1,0 +1,176 @@
+"""Round 5 GPU parity: the horizontal paths inside the fused down sweep (MODE 3 line waves,
+speculative strip segments) and the patch pass that repairs segments whose guessed start
+state was wrong.  Every case is bit-exact against the C oracle
+(oracle/sgm_ref.c); the adversarial cases force repairs (a 1-column warmup, textureless
+bands, smooth costs, tiny D, one-strip images) and check the repair counter moved."""
+import numpy as np
+import pytest
+
+from oracle import ref_c
+from stereo_match_amd import _lib, synthetic
+
+pytestmark = pytest.mark.gpu
+
+SWEEP8 = 16384  # sm_api.hip DBG_SWEEP8: the fused sweeps at any pair count
+
+
+@pytest.fixture(scope="module")
+def eng():
+    e = _lib.Engine(0)
+    yield e
+    e.close()
+
+
+def _params(cost, D, mode, minD=0, bs=5):
+    if cost:
+        return dict(synthetic.headline_params(D), minDisparity=minD, mode=mode)
+    return dict(synthetic.parity_params(D), minDisparity=minD, mode=mode, blockSize=bs, P1=8 * bs * bs,
+                P2=32 * bs * bs)
+
+
+def _run(eng, left, right, p, flags=SWEEP8, **tune):
+    eng.set_debug_flags(flags)
+    for k, v in tune.items():
+        eng.set_tuning(getattr(eng, "TUNE_" + k.upper()), v)
+    try:
+        return eng.compute(left, right, synthetic.to_sm_params(p))
+    finally:
+        eng.set_debug_flags(0)
+        for k in tune:
+            eng.set_tuning(getattr(eng, "TUNE_" + k.upper()), 0)
+
+
+def _check(out, left, right, p):
+    exp = ref_c.compute(left, right, p)
+    assert np.array_equal(out, exp), f"{np.sum(out != exp)} px differ"
+
+
+_rng = np.random.default_rng(505)
+CASES = []
+for _ in range(30):
+    D = int(_rng.choice([16, 32, 48, 64, 96, 128, 160, 192, 256]))
+    H = int(_rng.integers(1, 48))
+    W = int(_rng.integers(D + 1, D + 320)) if _rng.random() < 0.85 else int(_rng.integers(1, D + 3))
+    CASES.append(dict(H=H, W=W, D=D, minD=int(_rng.choice([0, 0, 0, 5, -9, -D + 1])), cost=int(_rng.integers(0, 2)),
+                      mode=int(_rng.choice([5, 8])), warm=int(_rng.choice([0, 0, 1, 2, 5])),
+                      seed=int(_rng.integers(0, 1 << 30))))
+
+
+@pytest.mark.parametrize("c", CASES, ids=lambda c: "H{H}W{W}D{D}m{minD}c{cost}p{mode}w{warm}".format(**c))
+def test_lines_random_shapes(eng, c):
+    """The in-sweep lines on random shapes: ragged last strips, single-strip images, both cost
+    types and path counts, default and tiny warmups (most segments repaired)."""
+    left, right, _ = synthetic.random_dot_pair(c["H"], c["W"], c["D"], seed=c["seed"])
+    p = _params(c["cost"], c["D"], c["mode"], c["minD"])
+    out = _run(eng, left, right, p, ew_warmup=c["warm"])
+    _check(out, left, right, p)
+
+
+@pytest.mark.parametrize("cost,mode,D", [(1, 8, 128), (0, 5, 128), (0, 8, 128), (0, 5, 160), (1, 5, 64)])
+@pytest.mark.parametrize("warm", [0, 1])
+def test_lines_full_kitti(eng, cost, mode, D, warm):
+    """Full KITTI frames, default warmup and a 1-column warmup (nearly every segment starts
+    wrong and is repaired): bit-exact, and the repair counter counts the repairs."""
+    H, W, _ = synthetic.CONFIGS["kitti"]
+    left, right, _ = synthetic.random_dot_pair(H, W, D, seed=D + mode + cost)
+    p = _params(cost, D, mode)
+    before = eng.counters()["ew_repairs"]
+    out = _run(eng, left, right, p, ew_warmup=warm)
+    _check(out, left, right, p)
+    rep = eng.counters()["ew_repairs"] - before
+    if warm == 1:
+        assert rep > H, rep  # (at least one per row on random texture)
+
+
+def _bands(H, W, period=40, seed=0):
+    """Textureless vertical bands alternating with random texture: states cannot meet inside
+    a flat band, so the segments that start there are repaired across it."""
+    rng = np.random.default_rng(seed)
+    img = rng.integers(0, 256, (H, W)).astype(np.uint8)
+    flat = (np.arange(W) // period) % 2 == 0
+    img[:, flat] = 90
+    return img
+
+
+ADV = [
+    ("const", lambda H, W: (np.full((H, W), 77, np.uint8), np.full((H, W), 77, np.uint8))),
+    ("const_lr_differ", lambda H, W: (np.full((H, W), 40, np.uint8), np.full((H, W), 200, np.uint8))),
+    ("bands", lambda H, W: (_bands(H, W, 40, 1), np.roll(_bands(H, W, 40, 1), -7, axis=1))),
+    ("wide_bands", lambda H, W: (_bands(H, W, 150, 2), np.roll(_bands(H, W, 150, 2), -3, axis=1))),
+    ("hgradient", lambda H, W: (np.tile(np.arange(W, dtype=np.int64) % 256, (H, 1)).astype(np.uint8),
+                                np.tile((np.arange(W, dtype=np.int64) + 5) % 256, (H, 1)).astype(np.uint8))),
+    ("noise_lr_indep", lambda H, W: (np.random.default_rng(3).integers(0, 256, (H, W)).astype(np.uint8),
+                                     np.random.default_rng(4).integers(0, 256, (H, W)).astype(np.uint8))),
+]
+
+
+@pytest.mark.parametrize("name,make", ADV, ids=[a[0] for a in ADV])
+@pytest.mark.parametrize("cost,mode,D,P1,P2", [(1, 8, 64, 10, 120), (1, 8, 32, 60, 61), (0, 5, 64, 200, 201),
+                                               (0, 8, 16, 8, 32), (1, 5, 128, 1, 193)])
+@pytest.mark.parametrize("warm", [0, 3])
+def test_lines_adversarial(eng, name, make, cost, mode, D, P1, P2, warm):
+    """Inputs chosen against the speculation: flat images, flat bands, smooth horizontal
+    gradients, uncorrelated noise; P2 = P1 + 1 (the smallest P2 the matcher keeps) and a
+    large P2; tiny D."""
+    H, W = 23, 3 * D + 257
+    left, right = make(H, W)
+    p = dict(_params(cost, D, mode), P1=P1, P2=P2)
+    out = _run(eng, left, right, p, ew_warmup=warm)
+    _check(out, left, right, p)
+
+
+def test_lines_match_classic_engine_kitti_batch(eng):
+    """8 KITTI census pairs through one launch group: the in-sweep lines and the E/W volume
+    kernel (SM_TUNE_SWEEP_LINES -1) give identical maps, and both equal the oracle."""
+    import torch
+
+    H, W, D = synthetic.CONFIGS["kitti"]
+    ls, rs = [], []
+    for i in range(8):
+        left, right, _ = synthetic.random_dot_pair(H, W, D, seed=5000 + i)
+        ls.append(left)
+        rs.append(right)
+    dl = torch.from_numpy(np.stack(ls)).cuda()
+    dr = torch.from_numpy(np.stack(rs)).cuda()
+    p = synthetic.headline_params(D)
+    outs = []
+    for lines in (0, -1):
+        out = torch.empty((8, H, W), dtype=torch.int16, device="cuda")
+        eng.set_tuning(eng.TUNE_SWEEP_LINES, lines)
+        try:
+            eng.compute_batch_device(dl.data_ptr(), dr.data_ptr(), 8, H * W, H, W, W, synthetic.to_sm_params(p),
+                                     out.data_ptr())
+            eng.synchronize()
+        finally:
+            eng.set_tuning(eng.TUNE_SWEEP_LINES, 0)
+        outs.append(out.cpu().numpy())
+    assert np.array_equal(outs[0], outs[1])
+    for i in (0, 5):
+        _check(outs[0][i], ls[i], rs[i], p)
+
+
+@pytest.mark.parametrize("D,warm", [(192, 0), (192, 2), (64, 0)])
+def test_lines_cost_volume(eng, D, warm):
+    """mc-cnn style f32 volumes (u16 costs, 8 paths) through the in-sweep lines."""
+    H, W = 40, D + 300
+    left, right, _ = synthetic.random_dot_pair(H, W, D, seed=D + warm)
+    vol = synthetic.absdiff_volume(left, right, D)
+    p = synthetic.cost_volume_params(D)
+    eng.set_debug_flags(SWEEP8)
+    eng.set_tuning(eng.TUNE_EW_WARMUP, warm)
+    try:
+        out = eng.aggregate_cost_f32(vol, synthetic.to_sm_params(p), 0.0, synthetic.VOLUME_SCALE)
+    finally:
+        eng.set_debug_flags(0)
+        eng.set_tuning(eng.TUNE_EW_WARMUP, 0)
+    exp = ref_c.compute_volume(vol[0], p, 0.0, synthetic.VOLUME_SCALE)
+    assert np.array_equal(out, exp), f"{np.sum(out != exp)} px differ"
+
+
+def test_lines_tuning_arguments(eng):
+    with pytest.raises(ValueError):
+        eng.set_tuning(eng.TUNE_EW_WARMUP, -1)
+    with pytest.raises(ValueError):
+        eng.set_tuning(eng.TUNE_SWEEP_LINES, 2)
+    c = eng.counters()
+    assert set(c) == {"sweep_fallbacks", "ew_repairs", "volume_clamped", "volume_nan"}

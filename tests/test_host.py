@@ -20,6 +20,26 @@ def test_library_exports_every_header_symbol():
     assert lib.sm_version().startswith(b"stereo_match_amd")
 
 
+def test_soname_names_a_loadable_file():
+    """A C program linked with -lstereo_match_amd records DT_NEEDED = the soname: that file
+    must exist beside the library (the Makefile's symlink) and be the same library."""
+    import subprocess
+
+    path = _lib.LIB_PATH
+    dyn = subprocess.run(["readelf", "-d", path], capture_output=True, text=True, check=True).stdout
+    import re
+    m = re.search(r"Library soname: \[([^\]]+)\]", dyn)
+    assert m, dyn
+    soname = m.group(1)
+    assert soname.endswith(".so.%d" % _lib.ABI_VERSION)
+    target = os.path.join(os.path.dirname(path), soname)
+    assert os.path.exists(target), target
+    assert os.path.samefile(os.path.realpath(target), os.path.realpath(path))
+    lib = ctypes.CDLL(target)
+    lib.sm_abi_version.restype = ctypes.c_int
+    assert lib.sm_abi_version() == _lib.ABI_VERSION
+
+
 def test_c_abi_struct_matches_header():
     text = open(_lib.HEADER_PATH).read()
     body = text[text.index("typedef struct sm_params"):text.index("} sm_params;")]
