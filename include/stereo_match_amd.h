@@ -267,11 +267,14 @@ int sm_get_counters(sm_ctx* ctx, long long* sweep_fallbacks);
  *                               speculation);
  *   SM_COUNTER_VOLUME_CLAMPED   external cost-volume cells (sm_aggregate_cost_f32*) whose
  *                               quantised value fell outside [0, 4095] and was clamped;
- *   SM_COUNTER_VOLUME_NAN       external cost-volume cells that were NaN (cost 4095). */
+ *   SM_COUNTER_VOLUME_NAN       external cost-volume cells that were NaN (cost 4095);
+ *   SM_COUNTER_LINE_GROUPS      launch groups whose horizontal paths ran inside the down
+ *                               sweep (host-side count of the engine's choice). */
 #define SM_COUNTER_SWEEP_FALLBACKS 0
 #define SM_COUNTER_EW_REPAIRS 1
 #define SM_COUNTER_VOLUME_CLAMPED 2
 #define SM_COUNTER_VOLUME_NAN 3
+#define SM_COUNTER_LINE_GROUPS 4
 int sm_get_counter(sm_ctx* ctx, int which, long long* value);
 
 /* Restrict the context's own streams (the default stream and its internal

@@ -158,6 +158,7 @@ struct sm_ctx {
     // sm_set_tuning knobs (0 = automatic)
     int tune_ew_lanes = 0, tune_sweep_ncw = 0, tune_ew_waves = 0, tune_ew_prio = 0;
     int tune_ew_warmup = 0, tune_sweep_lines = 0;  // in-sweep E/W lines: warmup columns, -1 off / 1 on
+    long long line_groups = 0;  // launch groups run with the in-sweep E/W lines (SM_COUNTER_LINE_GROUPS)
     std::vector<TimedEvent> pending;
     std::vector<hipEvent_t> free_events;
     double stage_ms[SM_NUM_STAGES] = {0};
@@ -1101,6 +1102,7 @@ int run_lines(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs, hipStream_t 
     if ((rc = ensure(ctx, bs.st, j.st_pair * G)) != SM_OK) return rc;
     j.st = (uint8_t*)bs.st.p;
     j.ewarm = ew_warmup(ctx, n);
+    ctx->line_groups++;
     {
         StageTimer t(ctx, ctx->stream, SM_STAGE_PATHS, G);
         {
@@ -2872,10 +2874,12 @@ int sm_get_counter(sm_ctx* ctx, int which, long long* value)
 {
     if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
     if (!value) return fail(ctx, SM_E_ARG, "value is NULL");
-    if (which < SM_COUNTER_SWEEP_FALLBACKS || which > SM_COUNTER_VOLUME_NAN)
+    if (which < SM_COUNTER_SWEEP_FALLBACKS || which > SM_COUNTER_LINE_GROUPS)
         return fail(ctx, SM_E_ARG, "unknown counter %d", which);
     long long v = 0;
-    if (ctx->sweep_err.p) {
+    if (which == SM_COUNTER_LINE_GROUPS) {
+        v = ctx->line_groups;
+    } else if (ctx->sweep_err.p) {
         HIP_TRY(ctx, hipSetDevice(ctx->device));
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
         HIP_TRY(ctx, hipStreamSynchronize(ctx->side));

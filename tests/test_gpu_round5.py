@@ -173,4 +173,4 @@ def test_lines_tuning_arguments(eng):
     with pytest.raises(ValueError):
         eng.set_tuning(eng.TUNE_SWEEP_LINES, 2)
     c = eng.counters()
-    assert set(c) == {"sweep_fallbacks", "ew_repairs", "volume_clamped", "volume_nan"}
+    assert set(c) == {"sweep_fallbacks", "ew_repairs", "volume_clamped", "volume_nan", "line_groups"}
