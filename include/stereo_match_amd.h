@@ -365,9 +365,11 @@ int sm_set_debug_flags(sm_ctx* ctx, int flags);
  *   SM_TUNE_EW_WAVES   waves per workgroup of the packed E/W lines: 0 automatic, 1..4.
  *   SM_TUNE_EW_PRIO    issue priority (s_setprio 0..3) of the packed E/W lines' waves.
  *   SM_TUNE_EW_WARMUP  columns each in-sweep E/W strip segment runs before its strip
- *                      (0 automatic: 16 census, 24 u16 costs; 1..4096).  Any value is
- *                      exact (the patch pass repairs segments that started wrong); small
- *                      values force repairs (tests), large ones cost line work.
+ *                      (0 automatic: 16 census, 24 u16 costs; 1..4096; rounded up to the
+ *                      line loop's load chunk).  Any value is exact (the patch pass repairs
+ *                      segments that started wrong); large values cost line work.
+ *   SM_TUNE_EW_GUESS   0 the segments start from the zero state; 1 (tests) from a
+ *                      deliberately wrong state, so that nearly every segment is repaired.
  *   SM_TUNE_SWEEP_LINES the fused-sweep engine's horizontal paths: 0 automatic (inside the
  *                      down sweep wherever that instance is built), 1 the same, -1 the E/W
  *                      volume kernel (k_ew) before / beside the sweeps.
@@ -378,6 +380,7 @@ int sm_set_debug_flags(sm_ctx* ctx, int flags);
 #define SM_TUNE_EW_PRIO 4
 #define SM_TUNE_EW_WARMUP 5
 #define SM_TUNE_SWEEP_LINES 6
+#define SM_TUNE_EW_GUESS 7
 int sm_set_tuning(sm_ctx* ctx, int key, int value);
 
 /* Last error text of ctx (or of the calling thread when ctx == NULL). */

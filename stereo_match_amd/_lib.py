@@ -481,6 +481,7 @@ class Engine:
         self._check(self._lib.sm_set_debug_flags(self.ctx, int(flags)))
 
     TUNE_EW_LANES, TUNE_SWEEP_NCW, TUNE_EW_WAVES, TUNE_EW_PRIO, TUNE_EW_WARMUP, TUNE_SWEEP_LINES = 1, 2, 3, 4, 5, 6
+    TUNE_EW_GUESS = 7
 
     def set_tuning(self, key: int, value: int):
         """Launch-shape knob (include/stereo_match_amd.h sm_set_tuning); 0 = automatic."""

@@ -158,6 +158,7 @@ struct sm_ctx {
     // sm_set_tuning knobs (0 = automatic)
     int tune_ew_lanes = 0, tune_sweep_ncw = 0, tune_ew_waves = 0, tune_ew_prio = 0;
     int tune_ew_warmup = 0, tune_sweep_lines = 0;  // in-sweep E/W lines: warmup columns, -1 off / 1 on
+    int tune_ew_guess = 0;                         // 1: the lines start from a wrong state (tests)
     long long line_groups = 0;  // launch groups run with the in-sweep E/W lines (SM_COUNTER_LINE_GROUPS)
     std::vector<TimedEvent> pending;
     std::vector<hipEvent_t> free_events;
@@ -704,6 +705,7 @@ struct SweepJob {
     uint8_t* st = nullptr;  // MODE 3: boundary states of the E/W strip segments
     size_t st_pair = 0;     // bytes
     int ewarm = 0;          // MODE 3: warmup columns of the E/W segments
+    int ewguess = 0;        // MODE 3: 1 = a deliberately wrong start state (tests)
 };
 
 // CUs the stream may run on: its CU mask (sm_set_cu_mask), the whole device when unmasked
@@ -876,6 +878,7 @@ int sweep_pass(sm_ctx* ctx, const Norm& n, const Geo& g, const SweepJob& j, int 
         a.st = j.st ? j.st + (size_t)p0 * j.st_pair : nullptr;
         a.st_pair = j.st_pair;
         a.ewarm = j.ewarm;
+        a.ewguess = j.ewguess;
         a.rec = j.key2 ? j.key2 + (size_t)p0 * g.H * g.W : nullptr;
         a.nb = j.pre ? j.pre + (size_t)p0 * g.H * g.W : nullptr;
         a.err = j.err;
@@ -1102,6 +1105,7 @@ int run_lines(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs, hipStream_t 
     if ((rc = ensure(ctx, bs.st, j.st_pair * G)) != SM_OK) return rc;
     j.st = (uint8_t*)bs.st.p;
     j.ewarm = ew_warmup(ctx, n);
+    j.ewguess = ctx->tune_ew_guess;
     ctx->line_groups++;
     {
         StageTimer t(ctx, ctx->stream, SM_STAGE_PATHS, G);
@@ -2541,6 +2545,7 @@ int sm_compute_disparity_batch_device(sm_ctx* ctx, const uint8_t* dL, const uint
         ctx->twin->tune_ew_prio = ctx->tune_ew_prio;
         ctx->twin->tune_ew_warmup = ctx->tune_ew_warmup;
         ctx->twin->tune_sweep_lines = ctx->tune_sweep_lines;
+        ctx->twin->tune_ew_guess = ctx->tune_ew_guess;
         if (!ctx->cu_mask.empty() &&
             (rc = sm_set_cu_mask(ctx->twin, ctx->cu_mask.data(), (int)ctx->cu_mask.size())) != SM_OK)
             return fail(ctx, rc, "%s", ctx->twin->err.c_str());
@@ -2996,6 +3001,10 @@ int sm_set_tuning(sm_ctx* ctx, int key, int value)
     case SM_TUNE_EW_WARMUP:
         if (value < 0 || value > 4096) return fail(ctx, SM_E_ARG, "E/W segment warmup %d: 0..4096", value);
         ctx->tune_ew_warmup = value;
+        break;
+    case SM_TUNE_EW_GUESS:
+        if (value < 0 || value > 1) return fail(ctx, SM_E_ARG, "E/W guess %d: 0 or 1", value);
+        ctx->tune_ew_guess = value;
         break;
     case SM_TUNE_SWEEP_LINES:
         if (value < -1 || value > 1) return fail(ctx, SM_E_ARG, "sweep lines %d: -1, 0 or 1", value);

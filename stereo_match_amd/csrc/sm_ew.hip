@@ -71,8 +71,8 @@ namespace {
 template <int VL, int NP, typename CT>
 hipError_t run_patch(const EwPatchArgs& a, int npairs, hipStream_t stream)
 {
-    constexpr int LPW = 64 / VL;
-    hipLaunchKernelGGL((k_ew_patch<VL, NP, CT>), dim3((a.H + 4 * LPW - 1) / (4 * LPW), npairs), dim3(256), 0, stream, a);
+    // one wave per image row, four rows per workgroup
+    hipLaunchKernelGGL((k_ew_patch<VL, NP, CT>), dim3((a.H + 3) / 4, npairs), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
 

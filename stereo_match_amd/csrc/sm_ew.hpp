@@ -137,14 +137,18 @@ __global__ void __launch_bounds__(256) k_ew_patch(EwPatchArgs a)
     constexpr bool H16 = sizeof(CT) == 1 && EW_H16;
     constexpr bool SAT = sizeof(CT) == 2;
     constexpr uint32_t EDGE = H16 ? 0x7BFF7BFFu : (kBig | (kBig << 16));
-    constexpr int KB = 8;  // strips whose boundary states are loaded together
+    // check phase: line kl of the wave checks the strips i = 1 + kl + LPW * u (u < KU) of a
+    // chunk of LPW * KU path positions, all loads of a chunk in flight together
+    constexpr int KU = 8;
+    constexpr int CHUNK = LPW * KU;
+    constexpr int RC = 8;  // columns of a repaired segment loaded together
     if (a.guard && __hip_atomic_load(a.guard, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int g = lane % VL, kl = lane / VL;
-    const int y = ((int)blockIdx.x * 4 + wave) * LPW + kl;
+    const int y = (int)blockIdx.x * 4 + wave;  // one wave per image row (wave-uniform)
     const size_t pair = blockIdx.y;
     const int H = a.H, W1 = a.W1, nwg = a.nwg, CW = a.cw;
-    if (y >= H) return;  // line-uniform; the remaining lines' DPL steps stay inside their lanes
+    if (y >= H) return;
     const uint64_t cells = (uint64_t)H * W1 * D;
     const rsrc_t rc = make_rsrc(a.cost + pair * a.cost_pair, cells * sizeof(CT));
     const rsrc_t rp = make_rsrc((const uint8_t*)a.part + pair * a.part_pair, cells * 2);
@@ -173,97 +177,135 @@ __global__ void __launch_bounds__(256) k_ew_patch(EwPatchArgs a)
     };
     uint32_t nfix = 0;
     for (int dir = 0; dir < 2; dir++) {  // 0 = E (strips in x order), 1 = W (reverse)
-        bool same = true;  // the trusted state entering the next strip = the previous strip's stored end
-        uint32_t T[NP];
+        auto strip_of = [&](int i) { return dir ? nwg - 1 - i : i; };  // path position -> strip
+        for (int i0 = 1; i0 < nwg; i0 += CHUNK) {
+            // ---- check: does the state entering strip i equal the end state stored by strip i - 1?
+            RawBytes<CB> sb[KU], eb[KU];
 #pragma unroll
-        for (int i = 0; i < NP; i++) T[i] = 0;
-        for (int i0 = 1; i0 < nwg; i0 += KB) {
-            RawBytes<CB> sb[KB], eb[KB];
-#pragma unroll
-            for (int kk = 0; kk < KB; kk++) {
-                const int i = i0 + kk;
-                const int k = dir ? nwg - 1 - i : i, kp = dir ? k + 1 : k - 1;
-                sb[kk].load(rs, i < nwg ? soff(k, dir, 0) : kOOB);
-                eb[kk].load(rs, i < nwg ? soff(kp, dir, 1) : kOOB);
+            for (int u = 0; u < KU; u++) {
+                const int i = i0 + kl + LPW * u;
+                sb[u].load(rs, i < nwg ? soff(strip_of(i), dir, 0) : kOOB);
+                eb[u].load(rs, i < nwg ? soff(strip_of(i - 1), dir, 1) : kOOB);
             }
+            uint64_t bad = 0;  // bit i - i0: strip i's speculative start differs (wave-uniform below)
 #pragma unroll
-            for (int kk = 0; kk < KB; kk++) {
-                const int i = i0 + kk;
-                if (i >= nwg) break;
-                const int k = dir ? nwg - 1 - i : i;
-                uint32_t S[NP], E[NP];
-                unpack_ct_pk<CT, DPL>(sb[kk], S);
-                unpack_ct_pk<CT, DPL>(eb[kk], E);
-                if (same) {
+            for (int u = 0; u < KU; u++) {
+                bool ok = true;
 #pragma unroll
-                    for (int q = 0; q < NP; q++) T[q] = E[q];
-                }
-                if (same_state(S, T)) {  // the speculative segment started from the true state
-                    same = true;
-                    continue;
-                }
-                // recompute strip k from T beside its speculative trajectory
-                uint32_t Lq[2][NP], mq[2];
+                for (int q = 0; q < RawBytes<CB>::WORDS; q++) ok &= sb[u].w[q] == eb[u].w[q];
+                ok = line_all(ok);
+                if (!ok && i0 + kl + LPW * u < nwg) bad |= 1ull << (kl + LPW * u);
+            }
+            // OR over the wave's lines (their first lanes)
+            uint64_t m = 0;
 #pragma unroll
-                for (int q = 0; q < NP; q++) {
-                    Lq[0][q] = S[q];
-                    Lq[1][q] = T[q];
-                }
-                mq[0] = state_min(Lq[0]);
-                mq[1] = state_min(Lq[1]);
-                const int x0 = k * CW, ncol = ::min(CW, W1 - x0);  // W: every repaired strip is full
-                bool met = false;
-                for (int o = 0; o < ncol; o++) {
-                    const int c = dir ? x0 + CW - 1 - o : x0 + o;
-                    RawBytes<CB> cc;
-                    cc.load(rc, cell(c) * (uint32_t)sizeof(CT));
-                    uint32_t C2[2][NP], Ln[2][NP], mn[2];
-                    unpack_ct_pk<CT, DPL>(cc, C2[0]);
+            for (int l = 0; l < LPW; l++) {
+                const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)bad, l * VL);
+                const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(bad >> 32), l * VL);
+                m |= ((uint64_t)hi << 32) | lo;
+            }
+            if (m == 0) continue;  // every strip of the chunk started from the true state
+            // ---- repair walk (line 0) from the chunk's first failing strip to the path's end:
+            // the trusted state entering strip i is strip i - 1's stored end state while every
+            // earlier strip was exact (same), else the true state the walk carries
+            if (kl == 0) {
+                bool same = true;
+                uint32_t T[NP];
 #pragma unroll
-                    for (int q = 0; q < NP; q++) C2[1][q] = C2[0][q];
-                    sweep_step2n<VL, NP, H16, 2>(Lq, mq, C2, P1p, P2p, eL, eR, Ln, mn);
-                    if (same_state(Ln[0], Ln[1])) {
-                        met = true;
-                        break;
+                for (int q = 0; q < NP; q++) T[q] = 0;
+                for (int i = i0 + __builtin_ctzll(m); i < nwg; i++) {
+                    const bool flagged = i - i0 < CHUNK ? ((m >> (i - i0)) & 1ull) != 0 : true;
+                    if (same && !flagged) continue;  // checked above against the trusted end state
+                    const int k = strip_of(i);
+                    RawBytes<CB> s1, e1;
+                    s1.load(rs, soff(k, dir, 0));
+                    e1.load(rs, soff(strip_of(i - 1), dir, 1));
+                    uint32_t S[NP], E[NP];
+                    unpack_ct_pk<CT, DPL>(s1, S);
+                    unpack_ct_pk<CT, DPL>(e1, E);
+                    if (same) {
+#pragma unroll
+                        for (int q = 0; q < NP; q++) T[q] = E[q];
                     }
-                    RawBytes<DPL * 2> pb;
-                    pb.load(rp, cell(c) * 2u);
-                    uint32_t P[NP];
+                    if (same_state(S, T)) {  // the speculative segment started from the true state
+                        same = true;
+                        continue;
+                    }
+                    // recompute strip k from T beside its speculative trajectory
+                    uint32_t Lq[2][NP], mq[2];
 #pragma unroll
                     for (int q = 0; q < NP; q++) {
-                        if constexpr (SAT) {
-                            uint32_t h[2];
+                        Lq[0][q] = S[q];
+                        Lq[1][q] = T[q];
+                    }
+                    mq[0] = state_min(Lq[0]);
+                    mq[1] = state_min(Lq[1]);
+                    const int x0 = k * CW, ncol = ::min(CW, W1 - x0);  // W: every repaired strip is full
+                    bool met = false;
+                    // columns in chunks of RC: the chunk's costs and partial slices load together
+                    for (int o0 = 0; o0 < ncol && !met; o0 += RC) {
+                        RawBytes<CB> cc[RC];
+                        RawBytes<DPL * 2> pb[RC];
 #pragma unroll
-                            for (int e = 0; e < 2; e++) {
-                                const uint32_t pv = (pb.w[q] >> (16 * e)) & 0xFFFFu;
-                                const uint32_t sv = (Ln[0][q] >> (16 * e)) & 0xFFFFu;
-                                const uint32_t tv = (Ln[1][q] >> (16 * e)) & 0xFFFFu;
-                                h[e] = pv == 0xFFFFu ? pv : ::min(pv - sv + tv, 0xFFFFu);
+                        for (int u = 0; u < RC; u++) {
+                            const int o = o0 + u;
+                            const int c = dir ? x0 + CW - 1 - o : x0 + o;
+                            cc[u].load(rc, o < ncol ? cell(c) * (uint32_t)sizeof(CT) : kOOB);
+                            pb[u].load(rp, o < ncol ? cell(c) * 2u : kOOB);
+                        }
+#pragma unroll
+                        for (int u = 0; u < RC; u++) {  // (no break: the loop must unroll)
+                            const int o = o0 + u;
+                            if (o >= ncol || met) continue;
+                            const int c = dir ? x0 + CW - 1 - o : x0 + o;
+                            uint32_t C2[2][NP], Ln[2][NP], mn[2];
+                            unpack_ct_pk<CT, DPL>(cc[u], C2[0]);
+#pragma unroll
+                            for (int q = 0; q < NP; q++) C2[1][q] = C2[0][q];
+                            sweep_step2n<VL, NP, H16, 2>(Lq, mq, C2, P1p, P2p, eL, eR, Ln, mn);
+                            if (same_state(Ln[0], Ln[1])) {
+                                met = true;
+                                continue;
                             }
-                            P[q] = h[0] | (h[1] << 16);
-                        } else {  // census: every sum < 2^11, the u16 wrap is exact
-                            P[q] = pk_add(pk_sub(pb.w[q], Ln[0][q]), Ln[1][q]);
+                            uint32_t P[NP];
+#pragma unroll
+                            for (int q = 0; q < NP; q++) {
+                                if constexpr (SAT) {
+                                    uint32_t h[2];
+#pragma unroll
+                                    for (int e = 0; e < 2; e++) {
+                                        const uint32_t pv = (pb[u].w[q] >> (16 * e)) & 0xFFFFu;
+                                        const uint32_t sv = (Ln[0][q] >> (16 * e)) & 0xFFFFu;
+                                        const uint32_t tv = (Ln[1][q] >> (16 * e)) & 0xFFFFu;
+                                        h[e] = pv == 0xFFFFu ? pv : ::min(pv - sv + tv, 0xFFFFu);
+                                    }
+                                    P[q] = h[0] | (h[1] << 16);
+                                } else {  // census: every sum < 2^11, the u16 wrap is exact
+                                    P[q] = pk_add(pk_sub(pb[u].w[q], Ln[0][q]), Ln[1][q]);
+                                }
+                            }
+                            bstore_n<uint32_t, NP>(rp, cell(c) * 2u, P);
+#pragma unroll
+                            for (int q = 0; q < NP; q++) {
+                                Lq[0][q] = Ln[0][q];
+                                Lq[1][q] = Ln[1][q];
+                            }
+                            mq[0] = mn[0];
+                            mq[1] = mn[1];
                         }
                     }
-                    bstore_n<uint32_t, NP>(rp, cell(c) * 2u, P);
+                    nfix++;
+                    same = met;
+                    if (!met) {  // the true end state of strip k enters strip k + 1
 #pragma unroll
-                    for (int q = 0; q < NP; q++) {
-                        Lq[0][q] = Ln[0][q];
-                        Lq[1][q] = Ln[1][q];
+                        for (int q = 0; q < NP; q++) T[q] = Lq[1][q];
                     }
-                    mq[0] = mn[0];
-                    mq[1] = mn[1];
-                }
-                nfix++;
-                same = met;
-                if (!met) {  // the true end state of strip k enters strip k + 1
-#pragma unroll
-                    for (int q = 0; q < NP; q++) T[q] = Lq[1][q];
                 }
             }
+            break;  // the walk covered the rest of this direction
         }
     }
-    if (a.fixes && g == 0 && nfix) atomicAdd(a.fixes, nfix);
+    if (a.fixes && lane == 0 && nfix) atomicAdd(a.fixes, nfix);
 }
 
 }  // namespace smk

@@ -187,6 +187,26 @@ constexpr int wide_ncw(int D, int ct_bytes)
 #ifndef SWEEP_LINE_PRIO
 #define SWEEP_LINE_PRIO 2  // issue priority of the line waves (compute waves: 3 on the hand-off chain, else 1)
 #endif
+// cost loads in flight per line lane (at most; the largest divisor of CW / 2 below this, so
+// that the line's phases fall on ring-chunk boundaries): the lines run ahead of the compute
+// waves, so their loads are the first touch of each cost row (HBM latency, not a cache hit)
+#ifndef SWEEP_LPF8
+#define SWEEP_LPF8 12  // u8 costs: 2 VGPRs per slot
+#endif
+#ifndef SWEEP_LPF16
+#define SWEEP_LPF16 12  // u16 costs: 4 VGPRs per slot
+#endif
+constexpr int largest_divisor_upto(int n, int cap)
+{
+    for (int p = cap < n ? cap : n; p > 1; p--)
+        if (n % p == 0) return p;
+    return 1;
+}
+// rows the lines run ahead of the block the compute waves are in, in blocks of HB rows (a
+// whole block: the lines work on block b + 1 while the compute waves run block b)
+#ifndef SWEEP_LEAD_BLOCKS
+#define SWEEP_LEAD_BLOCKS 1
+#endif
 constexpr int kMaxLds = 163840;  // gfx950: LDS one workgroup may declare
 template <int VL, int DPL, int NCW_, int MODE>
 struct LineGeo {
@@ -199,11 +219,14 @@ struct LineGeo {
     static constexpr int BASE = 8 * G::COLS * G::D + 16 * G::COLS + 4 * NCW_ + 4 * 16 + 512;
     static constexpr int ROWB = G::CW * G::D * 2;  // ring row: u16 E + W sums of the own columns
     static constexpr int FIT = (kMaxLds - BASE) / ROWB;
-    static constexpr int LEAD0 = RPW * (G::HB / 2 / RPW > 0 ? G::HB / 2 / RPW : 1);
+    static constexpr int LEAD0 = SWEEP_LEAD_BLOCKS * G::HB;
     static constexpr int LEAD = LEAD0 + RPW <= FIT ? LEAD0 : (FIT > RPW ? (FIT - RPW) / RPW * RPW : 0);
     static constexpr int LR = LEAD + 2 * RPW <= FIT ? LEAD + 2 * RPW : LEAD + RPW;
     static constexpr bool BUILT = ON && NLW >= 1 && DPL % 2 == 0 && !SWEEP_U32 && LEAD + RPW <= FIT &&
                                   G::CW % 2 == 0 && G::HB % RPW == 0 && RPW >= 1;
+    // ring chunk of the line loop, per cost type (a divisor of CW / 2)
+    template <typename CT>
+    static constexpr int lpf() { return largest_divisor_upto(G::CW / 2, sizeof(CT) == 1 ? SWEEP_LPF8 : SWEEP_LPF16); }
 };
 template <int VL, int DPL, int NCW_, int MODE>
 constexpr int sweep_threads() { return SweepGeo<VL, DPL, NCW_>::THREADS + 64 * LineGeo<VL, DPL, NCW_, MODE>::NLW; }
@@ -549,18 +572,16 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
             constexpr int CB = DPL * (int)sizeof(CT);
             constexpr bool H16 = sizeof(CT) == 1 && SWEEP_H16;
             constexpr uint32_t EDGE2 = H16 ? 0x7BFF7BFFu : (kBig | (kBig << 16));
-            constexpr int LPF = 8;  // cost loads in flight per lane
+            constexpr int LPF = LG::template lpf<CT>();  // cost loads in flight per lane (a divisor of CW / 2)
             const int li = wave - NCW - 1;
             const int kl = lane / VL, g = lane % VL;
             const int dir = kl & 1, r = kl >> 1;
             const int H = a.H, W1 = a.W1, x0 = wg * CW;
-            const int w = a.ewarm, nsteps = w + CW;
             const uint32_t P1p = (uint32_t)a.P1 * 0x10001u, P2p = (uint32_t)a.P2 * 0x10001u;
             const uint32_t eL = g == 0 ? EDGE2 : 0u, eR = g == VL - 1 ? EDGE2 : 0u;
             const uint64_t cells = (uint64_t)H * W1 * D;
             const rsrc_t rc = make_rsrc(a.cost + (size_t)pair * a.cost_pair, cells * sizeof(CT));
             const rsrc_t rs = make_rsrc(a.st + (size_t)pair * a.st_pair, a.st_pair);
-            const int c0 = dir ? x0 + CW - 1 + w : x0 - w, cs = dir ? -1 : 1;  // column of step j: c0 + cs * j
             __builtin_amdgcn_s_setprio(SWEEP_LINE_PRIO);
             int bn = 0;  // barrier pairs passed (the compute waves' two per block of HB rows)
             auto barriers_to = [&](int y0) {
@@ -590,6 +611,21 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
                     __builtin_amdgcn_s_sleep(1);
                 }
             };
+            // Steps run in chunks of LPF (the cost-load ring): the warmup (rounded up to whole
+            // chunks, w >= a.ewarm: a longer warmup only makes the guess better), then the CW / 2
+            // own columns this line reaches first (plain ring writes), then the CW / 2 columns
+            // the other direction's line wrote first (ring += this line's values).  No memory
+            // operation of a step is conditional (a conditional store makes the compiler drain
+            // the load ring, vmcnt(0), at every step); the boundary states are stored between
+            // chunks.
+            const int wch = (max(a.ewarm, 1) + LPF - 1) / LPF;  // warmup chunks
+            const int w = wch * LPF, nsteps = w + CW;
+            const int c0 = dir ? x0 + CW - 1 + w : x0 - w, cs = dir ? -1 : 1;  // column of step j: c0 + cs * j
+            // loads are valid for steps j with (unsigned)(j - jlo) < jspan (columns in [0, W1))
+            const int jlo = dir ? max(c0 - (W1 - 1), 0) : max(-c0, 0);
+            const int jhi = min(nsteps, dir ? c0 + 1 : W1 - c0);
+            const int cstep = cs * D * (int)sizeof(CT);  // byte step of the cost offset
+            const int rstep = cs * D;                     // u16 step of the ring pointer (own column o)
             for (int t = 0;; t++) {
                 const int y0 = (t * NLW + li) * RPW;
                 if (y0 >= H) break;
@@ -597,67 +633,88 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
                 wait_cons(y0 + RPW - LR);
                 const int y = y0 + r;
                 const bool yl = y < H;
-                uint16_t* rrow = &ring[yl ? y % LR : 0][0][g * DPL];
-                auto coff = [&](int j) -> uint32_t {
-                    const int c = c0 + cs * j;
-                    return yl && j < nsteps && c >= 0 && c < W1
-                               ? (((uint32_t)y * (uint32_t)W1 + (uint32_t)c) * (uint32_t)D + (uint32_t)(g * DPL)) *
-                                     (uint32_t)sizeof(CT)
-                               : kOOB;
-                };
+                const uint32_t jspan = yl && jhi > jlo ? (uint32_t)(jhi - jlo) : 0u;
+                // byte offset of step 0's cost slice (wraps for columns left of 0; never used there)
+                const uint32_t coff = (((uint32_t)y * (uint32_t)W1 + (uint32_t)c0) * (uint32_t)D + (uint32_t)(g * DPL)) *
+                                      (uint32_t)sizeof(CT);
+                // ring row of y (a row >= H reuses a slot whose row every own wave has consumed
+                // and no later row needs); own column o = h (E) or CW - 1 - h (W) at step w + h
+                uint16_t* rp = &ring[y % LR][dir ? CW - 1 : 0][g * DPL];
                 // boundary states of (y, strip, dir): [0] entering the strip, [1] at its far end
                 const uint32_t so = yl ? ((((uint32_t)y * (uint32_t)a.nwg + (uint32_t)wg) * 2u + (uint32_t)dir) * 2u *
                                               (uint32_t)D + (uint32_t)(g * DPL)) * (uint32_t)sizeof(CT)
                                        : kOOB;
+                auto coff_at = [&](int j) -> uint32_t {
+                    return (uint32_t)(j - jlo) < jspan ? coff + (uint32_t)(j * cstep) : kOOB;
+                };
                 RawBytes<CB> cr[LPF];
 #pragma unroll
                 for (int k = 0; k < LPF; k++) {
-                    cr[k].load(rc, coff(k));
+                    cr[k].load(rc, coff_at(k));
                     asm volatile("" ::: "memory");  // issue order = slot order
                 }
-                uint32_t Lp[NP], mm = 0;
+                uint32_t Lp[NP], mm = 0, old[NP];
 #pragma unroll
-                for (int i = 0; i < NP; i++) Lp[i] = 0;
-                for (int j0 = 0; j0 < nsteps; j0 += LPF) {
+                for (int i = 0; i < NP; i++) Lp[i] = old[i] = 0;
+                // test mode: a deliberately wrong start state.  Only where the segment starts inside
+                // the domain: one that enters it from outside starts from the entry state (the zero
+                // state over zero costs), which makes the first strip of each path exact
+                if (a.ewguess && jlo == 0) {
+#pragma unroll
+                    for (int i = 0; i < NP; i++) {
+                        const uint32_t d0 = (uint32_t)(g * DPL + 2 * i);
+                        Lp[i] = ((d0 * 7u + (uint32_t)y) % 61u) | ((((d0 + 1u) * 7u + (uint32_t)y) % 61u) << 16);
+                    }
+                    uint32_t m = Lp[0];
+#pragma unroll
+                    for (int i = 1; i < NP; i++) m = pk_min(m, Lp[i]);
+                    m = min(m & 0xFFFFu, m >> 16);
+                    mm = group_min<VL>(m) * 0x10001u;
+                }
+                // one chunk of LPF steps; RING: 0 none (warmup), 1 plain writes, 2 ring += values
+                auto chunk = [&](int j0, auto ring_c) {
+                    constexpr int RING = decltype(ring_c)::value;
 #pragma unroll
                     for (int k = 0; k < LPF; k++) {
                         const int j = j0 + k;
-                        if (j >= nsteps) break;
-                        // the slot is read after the previous step and unpacked before its refill
-                        // is issued (sm_ew.hpp k_ew)
+                        // the slot is read after the previous step and unpacked before its
+                        // refill is issued (sm_ew.hpp k_ew)
 #pragma unroll
                         for (int q = 0; q < RawBytes<CB>::WORDS; q++) asm volatile("" : "+v"(cr[k].w[q]) : "v"(mm));
                         uint32_t C[1][NP];
                         unpack_ct_pk<CT, DPL>(cr[k], C[0]);
 #pragma unroll
                         for (int i = 0; i < NP; i++) asm volatile("" : "+v"(C[0][i])::"memory");
-                        cr[k].load(rc, coff(j + LPF));
+                        cr[k].load(rc, coff_at(j + LPF));
                         uint32_t Lq[1][NP], mq[1] = {mm}, Ln[1][NP], mn[1];
 #pragma unroll
                         for (int i = 0; i < NP; i++) Lq[0][i] = Lp[i];
                         sweep_step2n<VL, NP, H16, 1>(Lq, mq, C, P1p, P2p, eL, eR, Ln, mn);
-                        if (j == w - 1) store_pk<CT, NP>(rs, so, Ln[0]);  // the state entering the strip
-                        if (j >= w && yl) {
-                            const int h = j - w;
-                            const int o = dir ? CW - 1 - h : h;
-                            uint32_t v[NP];
-                            if (2 * h >= CW) {  // the other direction's line wrote this column first
-                                uint32_t old[NP];
-                                lds_get_pk<NP>(rrow + o * D, old);
-#pragma unroll
-                                for (int i = 0; i < NP; i++) v[i] = pk_add(old[i], Ln[0][i]);
-                            } else {
-#pragma unroll
-                                for (int i = 0; i < NP; i++) v[i] = Ln[0][i];
-                            }
-                            lds_put_pk<NP>(rrow + o * D, v);
-                        }
-                        if (j == nsteps - 1) store_pk<CT, NP>(rs, yl ? so + (uint32_t)(D * sizeof(CT)) : kOOB, Ln[0]);
 #pragma unroll
                         for (int i = 0; i < NP; i++) Lp[i] = Ln[0][i];
                         mm = mn[0];
+                        if constexpr (RING != 0) {
+                            uint16_t* p = rp + (j - w) * rstep;
+                            if constexpr (RING == 2) {
+                                uint32_t v[NP];
+#pragma unroll
+                                for (int i = 0; i < NP; i++) v[i] = pk_add(old[i], Lp[i]);
+                                lds_put_pk<NP>(p, v);
+                                lds_get_pk<NP>(p + rstep, old);  // the next column (the other line wrote it)
+                            } else {
+                                lds_put_pk<NP>(p, Lp);
+                            }
+                        }
                     }
-                }
+                };
+                const int half = CW / 2 / LPF;  // chunks per half strip
+                for (int c = 0; c < wch; c++) chunk(c * LPF, std::integral_constant<int, 0>{});
+                store_pk<CT, NP>(rs, so, Lp);  // the state entering the strip
+                for (int c = 0; c < half; c++) chunk(w + c * LPF, std::integral_constant<int, 1>{});
+                // the first far-half column: the other line wrote it in the last step of the loop above
+                lds_get_pk<NP>(rp + (CW / 2) * rstep, old);
+                for (int c = 0; c < half; c++) chunk(w + (half + c) * LPF, std::integral_constant<int, 2>{});
+                store_pk<CT, NP>(rs, yl ? so + (uint32_t)(D * sizeof(CT)) : kOOB, Lp);  // the far end
                 // the batch's ring rows are complete (LDS only: the state stores need no ordering)
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
                 __hip_atomic_store(&linecnt[li], (uint32_t)(t + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);

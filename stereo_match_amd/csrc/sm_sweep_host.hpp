@@ -40,6 +40,7 @@ struct SweepArgs {
     uint8_t* st;
     size_t st_pair;  // bytes
     int ewarm;
+    int ewguess;  // 0: the zero state; 1 (tests): a deliberately wrong start state, every segment repaired
 };
 
 

@@ -10,12 +10,12 @@ SRC="$ROOT/stereo_match_amd/csrc"
 F="-O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wall $*"
 HIPCC=/opt/rocm/bin/hipcc
 $HIPCC $F -c -o "$OBJ/api.o" "$SRC/sm_api.hip" &
-for m in 0 1 2; do
+for m in 0 1 2 3 4; do
   $HIPCC $F -DSWEEP_MODE=$m -c -o "$OBJ/sw$m.o" "$SRC/sm_sweep.hip" &
   $HIPCC $F -DSWEEP_MODE=$m -DSWEEP_WIDE=1 -c -o "$OBJ/sww$m.o" "$SRC/sm_sweep.hip" &
   $HIPCC $F -DSWEEP_MODE=$m -DSWEEP_WIDE=2 -c -o "$OBJ/swl$m.o" "$SRC/sm_sweep.hip" &
 done
 $HIPCC $F -c -o "$OBJ/ew.o" "$SRC/sm_ew.hip" &
 wait
-$HIPCC --offload-arch=gfx950 -fPIC -shared -o "$ROOT/var/lib_$NAME.so" "$OBJ"/api.o "$OBJ"/sw[0-2].o "$OBJ"/sww[0-2].o "$OBJ"/swl[0-2].o "$OBJ"/ew.o
+$HIPCC --offload-arch=gfx950 -fPIC -shared -o "$ROOT/var/lib_$NAME.so" "$OBJ"/api.o "$OBJ"/sw[0-4].o "$OBJ"/sww[0-4].o "$OBJ"/swl[0-4].o "$OBJ"/ew.o
 echo "built var/lib_$NAME.so"
