@@ -127,7 +127,12 @@ int sm_compute_batch_device_cn(sm_ctx* ctx, const uint8_t* d_left, const uint8_t
  * StereoSGBM's own; mc-cnn's -disp_max 228 volume has 228 planes: the kernels
  * run the next multiple of 16 with pad planes that never win).
  * Costs are quantised q = rint((c + offset) * scale)
- * (float32), clamped to [0, 4095], NaN -> 4095, then aggregated with the
+ * (float32), clamped to [0, 4095], NaN -> 4095 (counted: SM_COUNTER_VOLUME_CLAMPED /
+ * SM_COUNTER_VOLUME_NAN).  scale == 0 (or NaN) derives the window per pair on the device
+ * from the volume itself: offset = -min, scale = 4095 / (max - min) (float32, IEEE division)
+ * over the finite costs of the quantised cells (planes < D, columns [minX1, maxX1)), so no
+ * finite cost is clamped; offset is then ignored (no finite cost: 0 and 1).  P1 / P2 are in
+ * the quantised units.  The result is then aggregated with the
  * path recurrence / WTA / uniqueness / sub-pixel / LR / median of
  * sm_compute (p->mode paths; block_size and pre_filter_cap unused;
  * P2 <= 12288).  Output as sm_compute.  Host version is synchronous. */

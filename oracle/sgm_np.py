@@ -269,6 +269,44 @@ def quantize_volume(vol: np.ndarray, prm, offset: float, scale: float) -> np.nda
     return q.astype(np.int64).transpose(1, 2, 0)
 
 
+def volume_window(vol: np.ndarray, prm):
+    """The automatic quantisation window (sm_aggregate_cost_f32* with scale 0; own
+    definition, parity unpinned: the reference only memmaps the volume,
+    ``mapTo3D_mc_cnn.py:71``): over the finite costs of the cells that get quantised
+    (every plane, every row, columns [minX1, maxX1)), offset = -min and
+    scale = 4095 / (max - min) in float32 (one IEEE subtraction, one IEEE division);
+    (0, 1) without finite costs or with max == min."""
+    v = np.asarray(vol, np.float32)
+    if v.ndim == 4:
+        v = v[0]
+    W = v.shape[2]
+    minX1, maxX1 = geometry(W, prm["minD"], v.shape[0])
+    sub = v[:, :, minX1:maxX1]
+    fin = sub[np.isfinite(sub)]
+    if fin.size == 0:
+        return 0.0, 1.0
+    mn, mx = np.float32(fin.min()), np.float32(fin.max())
+    d = np.float32(mx - mn)
+    sc = np.float32(VOLUME_CMAX) / d if d > 0 and np.isfinite(d) else np.float32(1.0)
+    return float(np.float32(-mn)), float(sc)
+
+
+def quantize_counts(vol: np.ndarray, prm, offset: float, scale: float):
+    """(clamped, nan) cell counts of quantize_volume: finite-or-infinite costs whose
+    rint((c + offset) * scale) fell outside [0, 4095] (or was NaN), and NaN costs."""
+    v = np.asarray(vol, np.float32)
+    if v.ndim == 4:
+        v = v[0]
+    W = v.shape[2]
+    minX1, maxX1 = geometry(W, prm["minD"], v.shape[0])
+    sub = v[:, :, minX1:maxX1]
+    nan = np.isnan(sub)
+    with np.errstate(invalid="ignore", over="ignore"):
+        q = np.rint((sub + np.float32(offset)) * np.float32(scale))
+        bad = (q < 0) | (q > VOLUME_CMAX) | np.isnan(q)
+    return int(np.sum(bad & ~nan)), int(np.sum(nan))
+
+
 # --------------------------------------------------------------------------
 # Path aggregation
 # --------------------------------------------------------------------------

@@ -304,8 +304,10 @@ class Engine:
 
     # -- external cost volume (mc-cnn) ----------------------------------------
     def aggregate_cost_f32(self, vol: np.ndarray, params: SmParams, offset: float = 0.0,
-                           scale: float = 1.0) -> np.ndarray:
-        """SGM over a float32 d-major cost volume [D][H][W] (or [1][D][H][W])."""
+                           scale=None) -> np.ndarray:
+        """SGM over a float32 d-major cost volume [D][H][W] (or [1][D][H][W]).  scale None (or 0):
+        the quantisation window from the volume's own finite range (include/stereo_match_amd.h)."""
+        scale = 0.0 if scale is None else scale
         v = np.ascontiguousarray(vol, np.float32)
         if v.ndim == 4:
             if v.shape[0] != 1:

@@ -134,6 +134,7 @@ struct sm_ctx {
     hipStream_t wls_stream = nullptr;  // compute_disparity: WLS weights + pivots beside the matchers
     hipEvent_t ev_wls_fork = nullptr, ev_wls_ready = nullptr;
     DevBuf hop, sweep_err;  // sweep engine: strip-boundary granules, device error word
+    DevBuf volwin;          // external cost volumes, automatic window: [pair] min/max keys + offset/scale
     void* pin = nullptr;    // page-locked host staging of the host-pointer entry points (HostStage)
     size_t pin_n = 0;
     // compute_disparity: the right matcher runs on a twin context (own streams and
@@ -1579,7 +1580,32 @@ int run_group(sm_ctx* ctx, const Src& src, const Geo& g, const Norm& n, int16_t*
             }
         } else if (n.cost == SM_COST_VOLUME) {
             if ((rc = ensure(ctx, bs.cost, (size_t)G * g.vol * 2)) != SM_OK) return rc;
+            if ((rc = ensure_sweep_err(ctx)) != SM_OK) return rc;  // (holds the clamp / NaN counters)
+            const float* win = nullptr;
+            if (!(src.scale != 0.f)) {  // scale 0 (or NaN): the window from the volume's own range
+                if ((rc = ensure(ctx, ctx->volwin, (size_t)G * 16)) != SM_OK) return rc;
+                smk::VolWinArgs wa{};
+                wa.vol = src.vol;
+                wa.vol_pair = src.vol_pair;
+                wa.Dv = n.Dv;
+                wa.H = H;
+                wa.W = W;
+                wa.minX1 = n.minX1;
+                wa.width1 = n.width1;
+                wa.keys = (uint32_t*)ctx->volwin.p;
+                wa.win = (float*)ctx->volwin.p + 2 * G;
+                hipLaunchKernelGGL(smk::k_vol_keys_init, dim3((G + 255) / 256), dim3(256), 0, ctx->stream, wa.keys, G);
+                const int lines = n.Dv * H;
+                hipLaunchKernelGGL(smk::k_vol_minmax, dim3(std::min(lines, std::max(1, 2048 / G)), G), dim3(256), 0,
+                                   ctx->stream, wa);
+                hipLaunchKernelGGL(smk::k_vol_window, dim3((G + 255) / 256), dim3(256), 0, ctx->stream, wa, G);
+                HIP_TRY(ctx, hipGetLastError());
+                win = wa.win;
+            }
             smk::VolArgs va{};
+            va.win = win;
+            va.clamped = (unsigned long long*)((uint32_t*)ctx->sweep_err.p + ERR_VOL_CLAMPED);
+            va.nans = (unsigned long long*)((uint32_t*)ctx->sweep_err.p + ERR_VOL_NAN);
             va.vol = src.vol;
             va.vol_pair = src.vol_pair;
             va.C = (uint16_t*)bs.cost.p;

@@ -220,6 +220,32 @@ __device__ __forceinline__ uint32_t Line<64>::min(uint32_t v)
     return ::min(::min(a, b), ::min(c, d));
 }
 
+// whole-wave reductions (the result in every lane): 16-lane rows by DPP, then the four rows
+__device__ __forceinline__ uint32_t group_min_u32_wave(uint32_t v)
+{
+    v = row16_min(v);
+    return ::min(::min(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
+                 ::min(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
+}
+__device__ __forceinline__ uint32_t group_max_u32_wave(uint32_t v)
+{
+    v = ::max(v, perm_dpp<DPP_QP_XOR1>(v));
+    v = ::max(v, perm_dpp<DPP_QP_XOR2>(v));
+    v = ::max(v, perm_dpp<DPP_ROW_HALF_MIRROR>(v));
+    v = ::max(v, perm_dpp<DPP_ROW_MIRROR>(v));
+    return ::max(::max(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
+                 ::max(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
+}
+__device__ __forceinline__ uint32_t group_sum_u32_wave(uint32_t v)
+{
+    v += perm_dpp<DPP_QP_XOR1>(v);
+    v += perm_dpp<DPP_QP_XOR2>(v);
+    v += perm_dpp<DPP_ROW_HALF_MIRROR>(v);
+    v += perm_dpp<DPP_ROW_MIRROR>(v);
+    return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) + __builtin_amdgcn_readlane(v, 32) +
+           __builtin_amdgcn_readlane(v, 48);
+}
+
 // ------------------------------------------------------ vector load/store
 template <typename T, int N>
 struct Vec {

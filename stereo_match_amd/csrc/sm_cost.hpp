@@ -692,13 +692,114 @@ struct VolArgs {
     int cpad;  // vol_pad_cost(P2)
     int nt;  // 1: nontemporal stores (the launch group's volume exceeds the Infinity Cache)
     float offset, scale;
+    const float* win;  // automatic window: [pair][2] = offset, scale (k_vol_window), else null
+    // cells whose quantised value was clamped into [0, VOL_CMAX] / that were NaN (device counters)
+    unsigned long long *clamped, *nans;
     uint32_t* zero_word;  // see CensusArgs
 };
+
+// ---- automatic quantisation window (sm_aggregate_cost_f32* with scale == 0): per pair, the
+// finite minimum and maximum over the cells that get quantised (planes < Dv, every row, the
+// matcher's columns [minX1, minX1 + width1)), then offset = -min, scale = VOL_CMAX / (max - min)
+// in float32 (IEEE division; the oracle computes the same two roundings), so the whole range
+// maps onto [0, VOL_CMAX] and no finite cost is clamped.
+struct VolWinArgs {
+    const float* vol;
+    size_t vol_pair;  // elements between pairs
+    int Dv, H, W, minX1, width1;
+    uint32_t* keys;  // [pair][2]: order-preserving u32 keys of the minimum and the maximum
+    float* win;      // [pair][2]: offset, scale
+};
+
+// unsigned order of the key = order of the float (no NaN enters)
+__device__ inline uint32_t fkey(float f)
+{
+    const uint32_t b = __float_as_uint(f);
+    return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ inline float fkey_inv(uint32_t k) { return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k); }
+
+__global__ void k_vol_keys_init(uint32_t* keys, int npairs)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < npairs) {
+        keys[2 * i] = 0xFFFFFFFFu;
+        keys[2 * i + 1] = 0u;
+    }
+}
+
+// grid (blocks, pairs), 256 threads: block b reduces the domain rows (plane, y) = b, b + gridDim.x, ...
+__global__ void __launch_bounds__(256) k_vol_minmax(VolWinArgs a)
+{
+    __shared__ uint32_t smin[4], smax[4];
+    const float* v = a.vol + (size_t)blockIdx.y * a.vol_pair + a.minX1;
+    uint32_t kmin = 0xFFFFFFFFu, kmax = 0u;
+    const int lines = a.Dv * a.H;
+    for (int l = blockIdx.x; l < lines; l += gridDim.x) {
+        const float* row = v + (size_t)l * a.W;  // plane l / H, row l % H: planes are H*W apart
+        for (int x = threadIdx.x; x < a.width1; x += 256) {
+            const float f = __builtin_nontemporal_load(row + x);
+            if (__builtin_isfinite(f)) {
+                const uint32_t k = fkey(f);
+                kmin = min(kmin, k);
+                kmax = max(kmax, k);
+            }
+        }
+    }
+    kmin = group_min_u32_wave(kmin);
+    kmax = group_max_u32_wave(kmax);
+    const int wave = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        smin[wave] = kmin;
+        smax[wave] = kmax;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < 4; w++) {
+            kmin = min(kmin, smin[w]);
+            kmax = max(kmax, smax[w]);
+        }
+        if (kmin <= kmax) {
+            atomicMin(&a.keys[2 * blockIdx.y], kmin);
+            atomicMax(&a.keys[2 * blockIdx.y + 1], kmax);
+        }
+    }
+}
+
+__global__ void k_vol_window(VolWinArgs a, int npairs)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= npairs) return;
+    const uint32_t k0 = a.keys[2 * i], k1 = a.keys[2 * i + 1];
+    float off = 0.f, sc = 1.f;  // no finite cost at all
+    if (k0 <= k1) {
+        const float mn = fkey_inv(k0), mx = fkey_inv(k1);
+        off = -mn;
+        const float d = mx - mn;
+        sc = (d > 0.f && __builtin_isfinite(d)) ? (float)VOL_CMAX / d : 1.f;
+    }
+    a.win[2 * i] = off;
+    a.win[2 * i + 1] = sc;
+}
 
 __device__ inline uint32_t quant_cost(float c, float off, float sc)
 {
     if (c != c) return VOL_CMAX;
     const float v = __builtin_rintf((c + off) * sc);
+    if (!(v > 0.f)) return 0;
+    if (v > (float)VOL_CMAX) return VOL_CMAX;
+    return (uint32_t)v;
+}
+
+// quant_cost, counting NaN cells and cells clamped into [0, VOL_CMAX]
+__device__ inline uint32_t quant_cost_n(float c, float off, float sc, uint32_t& nclamp, uint32_t& nnan)
+{
+    if (c != c) {
+        nnan++;
+        return VOL_CMAX;
+    }
+    const float v = __builtin_rintf((c + off) * sc);
+    nclamp += (v < 0.f || v > (float)VOL_CMAX || v != v) ? 1u : 0u;
     if (!(v > 0.f)) return 0;
     if (v > (float)VOL_CMAX) return VOL_CMAX;
     return (uint32_t)v;
@@ -714,6 +815,8 @@ __global__ void __launch_bounds__(256) k_cost_volume_f32(VolArgs a)
     extern __shared__ uint32_t tile[];  // [TX][D/2 + 1] packed u16 pairs (d even | d odd << 16)
     const int half = a.D >> 1, rowdw = half + 1;
     const int x0 = blockIdx.x * TX, y = blockIdx.y, pair = blockIdx.z;
+    const float qoff = a.win ? a.win[2 * pair] : a.offset, qsc = a.win ? a.win[2 * pair + 1] : a.scale;
+    uint32_t nclamp = 0, nnan = 0;
     const int nx = min(TX, a.width1 - x0);
     const size_t plane = (size_t)a.H * a.W;
     const float* v = a.vol + pair * a.vol_pair + (size_t)y * a.W + a.minX1 + x0;
@@ -754,9 +857,19 @@ __global__ void __launch_bounds__(256) k_cost_volume_f32(VolArgs a)
         }
 #pragma unroll
         for (int k = 0; k < PL; k++) {
-            const uint32_t q0 = in0 ? quant_cost(c0[k], a.offset, a.scale) : (uint32_t)a.cpad;
-            const uint32_t q1 = in1 ? quant_cost(c1[k], a.offset, a.scale) : (uint32_t)a.cpad;
+            const bool x_in = xl + k < nx;  // (columns past the domain are loaded as 0, not counted)
+            uint32_t q0 = (uint32_t)a.cpad, q1 = (uint32_t)a.cpad;
+            if (in0) q0 = x_in ? quant_cost_n(c0[k], qoff, qsc, nclamp, nnan) : quant_cost(c0[k], qoff, qsc);
+            if (in1) q1 = x_in ? quant_cost_n(c1[k], qoff, qsc, nclamp, nnan) : quant_cost(c1[k], qoff, qsc);
             tile[(xl + k) * rowdw + dp] = q0 | (q1 << 16);
+        }
+    }
+    if (a.clamped) {  // one atomic per wave that saw any
+        nclamp = group_sum_u32_wave(nclamp);
+        nnan = group_sum_u32_wave(nnan);
+        if ((threadIdx.x & 63) == 0) {
+            if (nclamp) atomicAdd(a.clamped, (unsigned long long)nclamp);
+            if (nnan) atomicAdd(a.nans, (unsigned long long)nnan);
         }
     }
     __syncthreads();

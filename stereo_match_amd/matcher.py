@@ -111,7 +111,7 @@ class StereoSGBM:
             return disparity
         return out
 
-    def computeFromCost(self, cost, offset: float = 0.0, scale: float = 1.0):
+    def computeFromCost(self, cost, offset: float = 0.0, scale=None):
         """SGM over an external matching-cost volume (mc-cnn).
 
         ``cost``: float32 ``(1, D, H, W)`` or ``(D, H, W)``, d-major — the
@@ -120,9 +120,14 @@ class StereoSGBM:
         right x − (minDisparity + d).  Costs are quantised
         ``rint((c + offset) * scale)`` to [0, 4095] (NaN → 4095), then the
         same paths / WTA / LR / median as :meth:`compute` run (``mode`` picks
-        5 or 8 paths; ``blockSize``/``preFilterCap`` are unused).  numpy in →
-        int16 numpy out; a torch CUDA float32 tensor in → int16 CUDA tensor
-        (torch's current stream)."""
+        5 or 8 paths; ``blockSize``/``preFilterCap`` are unused).  ``scale``
+        None (the default) derives the window from the volume's own finite
+        range on the device (offset = -min, scale = 4095 / (max - min)), so
+        nothing is clamped whatever range the volume has; P1 / P2 are in the
+        quantised units either way.  Cells that were clamped or NaN are counted
+        (``_lib.engine().counters()``).  numpy in → int16 numpy out; a torch
+        CUDA float32 tensor in → int16 CUDA tensor (torch's current stream)."""
+        scale = 0.0 if scale is None else float(scale)
         prm = self.params()
         prm.cost_kind = _lib.SM_COST_VOLUME
         if _is_torch_cuda(cost):

@@ -177,3 +177,86 @@ def test_lines_tuning_arguments(eng):
         eng.set_tuning(eng.TUNE_EW_GUESS, 2)
     c = eng.counters()
     assert set(c) == {"sweep_fallbacks", "ew_repairs", "volume_clamped", "volume_nan", "line_groups"}
+
+
+# ------------------------------------------------------------------ mc-cnn quantisation window
+def _signed_volume(H, W, D, seed):
+    """An mc-cnn-like volume whose range nothing pins: negative costs, costs far above 1,
+    NaN where x - d leaves the right image (synthetic.absdiff_volume) and a few inf."""
+    left, right, _ = synthetic.random_dot_pair(H, W, D, seed=seed)
+    v = synthetic.absdiff_volume(left, right, D)[0]
+    rng = np.random.default_rng(seed)
+    v = (v * np.float32(7.0) - np.float32(2.5)).astype(np.float32)  # roughly [-2.5, 4.5]
+    v[:, :, -5:] = np.float32(np.inf)
+    v.flat[rng.integers(0, v.size, 50)] = np.float32(-np.inf)
+    v[:, 3, D + 3] = np.float32(np.nan)  # inside the matcher's columns (absdiff's NaNs are left of them)
+    return v
+
+
+@pytest.mark.parametrize("D,mode", [(64, 8), (48, 5), (37, 8)])
+def test_volume_automatic_window(eng, D, mode):
+    """scale None / 0: the device derives offset = -min, scale = 4095 / (max - min) over the
+    finite quantised cells; the maps equal the C oracle run with the same window
+    (oracle/sgm_np.volume_window), no finite cost is clamped, NaN cells are counted."""
+    from oracle import sgm_np
+
+    H, W = 31, D + 170
+    vol = _signed_volume(H, W, D, seed=D)
+    p = dict(synthetic.cost_volume_params(D), mode=mode)
+    prm = sgm_np.normalize_params(dict(p, cost=2))
+    off, sc = sgm_np.volume_window(vol, prm)
+    assert sc != 1.0 and off > 0  # a real window: the volume has negative costs
+    clamped_exp, nan_exp = sgm_np.quantize_counts(vol, prm, off, sc)
+    before = eng.counters()
+    out = eng.aggregate_cost_f32(vol, synthetic.to_sm_params(p))  # scale None: automatic
+    after = eng.counters()
+    exp = ref_c.compute_volume(vol, p, off, sc)
+    assert np.array_equal(out, exp), f"{np.sum(out != exp)} px differ"
+    # only the infinities leave the window
+    assert after["volume_clamped"] - before["volume_clamped"] == clamped_exp
+    assert clamped_exp == int(np.sum(np.isinf(vol[:, :, prm["minD"] + D:])))
+    assert after["volume_nan"] - before["volume_nan"] == nan_exp > 0
+
+
+def test_volume_explicit_window_counts_clamped_cells(eng):
+    """The documented fixed window (offset 0, scale 4000) on a volume with negative and large
+    costs: bit-exact against the oracle with that window, and every clamped cell counted."""
+    from oracle import sgm_np
+
+    D, H, W = 32, 27, 200
+    vol = _signed_volume(H, W, D, seed=7)
+    p = synthetic.cost_volume_params(D)
+    prm = sgm_np.normalize_params(dict(p, cost=2))
+    clamped_exp, nan_exp = sgm_np.quantize_counts(vol, prm, 0.0, 4000.0)
+    assert clamped_exp > 1000  # the fixed window flattens a large part of this volume
+    before = eng.counters()
+    out = eng.aggregate_cost_f32(vol, synthetic.to_sm_params(p), 0.0, 4000.0)
+    after = eng.counters()
+    assert np.array_equal(out, ref_c.compute_volume(vol, p, 0.0, 4000.0))
+    assert after["volume_clamped"] - before["volume_clamped"] == clamped_exp
+    assert after["volume_nan"] - before["volume_nan"] == nan_exp
+
+
+def test_volume_automatic_window_device_batch(eng):
+    """Per-pair windows in one device batch (each pair its own range)."""
+    import torch
+
+    from oracle import sgm_np
+
+    D, H, W, n = 32, 20, 150, 3
+    vols = [(_signed_volume(H, W, D, seed=40 + i) * np.float32(1 + 3 * i)).astype(np.float32) for i in range(n)]
+    p = synthetic.cost_volume_params(D)
+    prm = sgm_np.normalize_params(dict(p, cost=2))
+    V = torch.tensor(np.stack(vols), device="cuda")
+    out = torch.empty((n, H, W), dtype=torch.int16, device="cuda")
+    eng.set_stream(torch.cuda.current_stream().cuda_stream)
+    try:
+        eng.aggregate_cost_f32_device(V.data_ptr(), n, D * H * W, D, H, W, synthetic.to_sm_params(p), 0.0, 0.0,
+                                      out.data_ptr())
+        eng.synchronize()
+    finally:
+        eng.set_stream(None)
+    got = out.cpu().numpy()
+    for i in range(n):
+        off, sc = sgm_np.volume_window(vols[i], prm)
+        assert np.array_equal(got[i], ref_c.compute_volume(vols[i], p, off, sc)), i
