@@ -131,20 +131,52 @@ def source_hash() -> str:
     return h.hexdigest()[:16]
 
 
+def kernel_stage(name: str, names) -> "str | None":
+    """The engine stage (sm_set_timing's names) a profiled kernel belongs to; ``names`` are
+    all kernels of the profiled run (they tell the engine apart).  Shared by
+    tools/traffic_summary.py and tools/valu_summary.py, which sum a stage's kernels."""
+    targs = [t.strip() for t in name.split("<", 1)[1].split(">")[0].split(",")] if "<" in name else []
+    sweep_modes = set()
+    for n in names:
+        if "k_sweep<" in n:
+            sweep_modes.add([t.strip() for t in n.split("<", 1)[1].split(">")[0].split(",")][3])
+    sweep = bool(sweep_modes) or any("k_sweep2<" in n for n in names)
+    lines5 = "3" in sweep_modes and "4" not in sweep_modes  # in-sweep E/W lines, 5 paths: k_wta reads the partial
+    if bool(targs) and targs[-1] == "true" and ("k_sgm_paths" in name or "k_wta" in name):
+        return None  # the guarded fallback instances (run only when a strip gave up)
+    if "k_sweep2<" in name or "k_sweep<" in name:  # MODE 0 / 3: down sweep -> partial; 1 / 2 / 4: with WTA
+        return "sweep" if targs[4 if "k_sweep2<" in name else 3] in ("0", "3") else "sweep_wta"
+    if "k_ew_patch" in name or "k_ew<" in name or (sweep and "k_sgm_paths" in name):
+        return "horizontal"
+    if "k_sgm_paths" in name:
+        return "paths"
+    if "k_wta" in name or "k_row_wta" in name:
+        return "sweep_wta" if lines5 else "wta"
+    if "k_lr_rows" in name:
+        return "wta"
+    if any(c in name for c in ("k_census9x7", "k_census_cost8", "k_sgbm_prefilter", "k_sgbm_cost", "k_cost_volume_f32",
+                               "k_vol_")):
+        return "cost"
+    return None
+
+
 # ---------------------------------------------------------------------------
 # SURVEY.md §8(d) byte model, attributed to the engine's stages
 # ---------------------------------------------------------------------------
 def model_pair_bytes(mode: str, H: int, W: int, D: int, P: int) -> int:
-    """§8(d) algorithmic bytes per pair (per matcher call)."""
+    """§8(d) algorithmic bytes per pair (per matcher call).  volume8: the bytes an engine must
+    move for an f32 volume (read once, 4 B; the quantised u16 volume written, 2 B, and read
+    per path, 2 B; S written and read, 4 B), not §8(d)'s 4 B per path, which credits f32
+    re-reads no engine makes (round-4 verdict: a frac above 1)."""
     cells = H * W * D
     if mode == "volume8":
-        return cells * (4 * P + 8)
+        return cells * (4 + 2 + 2 * P + 4)
     if mode == "bm":
         return H * W * (2 + 2 * 2 + 2 + 4)
     return cells * (1 + P + 4) + 2 * H * W + 2 * H * W * 2
 
 
-def model_stage_bytes(stage: str, mode: str, H: int, W: int, D: int, P: int, sweep: bool) -> int:
+def model_stage_bytes(stage: str, mode: str, H: int, W: int, D: int, P: int, sweep: bool, lines: bool = False) -> int:
     """Share of ``model_pair_bytes`` owned by one engine stage, per pair.
 
     Model terms per cell: cost volume written once (1 B; f32 volume read once,
@@ -154,13 +186,15 @@ def model_stage_bytes(stage: str, mode: str, H: int, W: int, D: int, P: int, swe
     write and the image reads; each aggregation kernel the reads of the paths
     it aggregates (+ the S write when it completes S); the WTA stage the S
     read and the outputs.  Summed over the stages this is exactly
-    ``model_pair_bytes``.
+    ``model_pair_bytes``.  With the in-sweep E/W lines (``lines``) the down sweep aggregates
+    five paths (S, SE, SW, E, W; at 5 paths it completes S), the patch pass owns no model
+    bytes, and the WTA stage is the up sweep (8 paths) or the WTA kernel over S (5 paths).
     """
     cells, px = H * W * D, H * W
     if mode == "bm":
         return model_pair_bytes(mode, H, W, D, P) if stage in ("wta", "paths") else 0
     vol = mode == "volume8"
-    cw, r = (4, 4) if vol else (1, 1)
+    cw, r = (4 + 2, 2) if vol else (1, 1)  # volume8: f32 read + u16 written; paths read u16
     io_in, io_out = (0, 0) if vol else (2, 4)
     if stage == "cost":
         return cells * cw + px * io_in
@@ -169,6 +203,12 @@ def model_stage_bytes(stage: str, mode: str, H: int, W: int, D: int, P: int, swe
             return cells * (P * r + 2)
         if stage == "wta":
             return cells * 2 + px * io_out
+        return 0
+    if lines:  # down sweep with E/W lines -> partial; patch; up sweep + WTA (8) / WTA over S (5)
+        if stage == "sweep":
+            return cells * 5 * r + (cells * 2 if P == 5 else 0)
+        if stage == "sweep_wta":
+            return (cells * (3 * r + 2 + 2) if P == 8 else cells * 2) + px * io_out
         return 0
     # fused-sweep engine: E/W lines, [down sweep S+SE+SW -> partial], last sweep (+ S write/read) + WTA
     if stage == "horizontal":
@@ -294,6 +334,7 @@ class GpuWorkload:
         self.eng.synchronize()
         self.eng.set_timing(True)
         self.eng.reset_timing()
+        self._c0 = self.eng.counters()
 
     def profile_end(self, n_prof):
         self.eng.synchronize()  # device-side failures (sweep hand-off timeouts) fail the run here
@@ -302,9 +343,11 @@ class GpuWorkload:
         self.profile = self.eng.timing()
         args = self.args
         self.sweep = self.profile["sweep_wta"][1] > 0  # fused-sweep engine ran (its stages have launches)
+        # ... with the horizontal paths inside the down sweep (sm_get_counter SM_COUNTER_LINE_GROUPS)
+        self.lines = self.sweep and self.eng.counters()["line_groups"] > self._c0["line_groups"]
         self.P_dirs = 5 if args.mode in ("sgbm5", "disparity5") else 8
         self.kern, cands = design_kernels(args, self.profile, self.H, self.W, self.D, self.p, self.P_dirs, self.sweep,
-                                          self.bm)
+                                          self.bm, self.lines)
         self.cands = cands
         # the dominant kernel is fixed per engine (the stage that moves the most bytes by design:
         # the WTA sweep, the per-direction path kernel), not picked by a timing race between
@@ -321,7 +364,8 @@ class GpuWorkload:
                 continue
             launch_s = ms / 1e3 / launches
             ppl = pairs / launches
-            alg = model_stage_bytes(k, self.args.mode, self.H, self.W, self.D, self.P_dirs, self.sweep) * ppl
+            alg = model_stage_bytes(k, self.args.mode, self.H, self.W, self.D, self.P_dirs, self.sweep,
+                                    self.lines) * ppl
             out[k] = {"kernel": self.kern[k][0], "avg_launch_us": launch_s * 1e6, "alg_bytes_per_launch": alg,
                       "frac": alg / launch_s / 1e9 / HBM_PEAK_GBS if launch_s > 0 else None,
                       "design_bytes_per_launch": self.kern[k][1] * ppl, "source": "warmup profile"}
@@ -332,11 +376,14 @@ class GpuWorkload:
         # delays the stream, about 12 us per KITTI pair with all of them: include/stereo_match_amd.h)
         self.eng.set_timing(True, stages=[self.dom])
         self.eng.reset_timing()
+        self._ct0 = self.eng.counters()
 
     def timed_end(self):
         self.eng.synchronize()
         self.stages = self.eng.timing()
         self.eng.set_timing(False)
+        c1 = self.eng.counters()
+        self.timed_counters = {k: c1[k] - self._ct0[k] for k in c1}
 
     def report(self, elapsed, K, gpairs, world):
         """The bench line's workload-specific fields (rank 0)."""
@@ -347,7 +394,7 @@ class GpuWorkload:
         dom_ms, dom_launches, dom_pairs = self.stages[dom]
         launch_s = dom_ms / 1e3 / max(dom_launches, 1)
         pairs_per_launch = dom_pairs / max(dom_launches, 1)
-        alg_bytes = model_stage_bytes(dom, args.mode, H, W, D, P_dirs, sweep) * pairs_per_launch
+        alg_bytes = model_stage_bytes(dom, args.mode, H, W, D, P_dirs, sweep, self.lines) * pairs_per_launch
         design_bytes = kern[dom][1] * pairs_per_launch
         achieved = alg_bytes / launch_s / 1e9 if launch_s > 0 else None
         traffic, traffic_note = read_traffic(args, dom, kern[dom][0], pairs_per_launch, sweep)
@@ -361,8 +408,12 @@ class GpuWorkload:
                       "bm": "i32"}[args.mode],
             "data": "synthetic random-dot pairs (no dataset in the image)"
                     + ("; f32 cost = 3x3-smoothed |L-R|/255 volume per pair" if self.volume else ""),
+            # the timed region's engine counters: launch groups the guarded fallback recomputed,
+            # in-sweep E/W segments the patch pass repaired (sm_get_counter)
+            "counters": dict(self.timed_counters, ew_repairs_per_pair=self.timed_counters["ew_repairs"] / max(K * P, 1)),
             "config": {
-                "engine": "fused sweeps" if sweep else "per-direction",
+                "engine": ("fused sweeps, E/W lines in the down sweep" if self.lines else "fused sweeps") if sweep
+                          else "per-direction",
                 "workload": f"{args.config} {W}x{H} D={D} "
                             + {"census8": "census9x7 + 8-path SGM", "sgbm5": "OpenCV-SGBM 5-path",
                                "sgbm8": "OpenCV-SGBM 8-path (MODE_HH)",
@@ -374,11 +425,12 @@ class GpuWorkload:
             "mpix_disp_per_s": gpairs * K / elapsed * cells / 1e6,
             "roofline": {
                 "kernel": kern[dom][0],
-                "bound": "hbm",
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+                **(valu_roofline(valu, launch_s) if self.bm else {
+                    "bound": "hbm",
+                    "achieved": achieved,
+                    "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s",
+                    "frac": (achieved / HBM_PEAK_GBS) if achieved else None}),
                 "traffic": traffic,
                 "alg_bytes_per_launch": alg_bytes,
                 "alg_model": "SURVEY §8d bytes owned by this stage (bench.model_stage_bytes)",
@@ -390,11 +442,13 @@ class GpuWorkload:
                 "pairs_per_launch": pairs_per_launch,
                 "avg_launch_us": launch_s * 1e6,
                 "dominant_rule": "fixed per engine: the stage with the most design bytes (fused sweeps: the WTA "
-                                 "sweep; per-direction: the path kernel)",
+                                 "sweep; with the in-sweep E/W lines: the down sweep with its line waves; "
+                                 "per-direction: the path kernel)",
                 "stages": self.stage_fracs(),
             },
             "pipeline_roofline": {
-                "model": "SURVEY §8d " + ("H·W·D·(4P+8)" if self.volume else "H·W·(2+4+2+4) (no volume)" if self.bm
+                "model": "SURVEY §8d " + ("H·W·D·(4+2+2P+4) (f32 read once)" if self.volume
+                                          else "H·W·(2+4+2+4) (no volume)" if self.bm
                                           else "H·W·D·(1+P+4)+I/O")
                          + (" x2 matchers" if self.full else "") + " per pair",
                 "bytes_per_pair": survey_bytes,
@@ -621,7 +675,7 @@ def run_rank(args, wl, world, rank):
         dist.destroy_process_group()
 
 
-def design_kernels(args, stages, H, W, D, p, P_dirs, sweep, bm):
+def design_kernels(args, stages, H, W, D, p, P_dirs, sweep, bm, lines=False):
     """The engine's own bytes per pair for each timed stage (what the kernels
     move by design), and the stages that can be the dominant kernel."""
     width1 = W - D  # minDisparity 0
@@ -630,6 +684,14 @@ def design_kernels(args, stages, H, W, D, p, P_dirs, sweep, bm):
     if bm:  # SAD kernel reads the two prefiltered views, writes disparity (+ int32 cost)
         return {"paths": ("k_bm_sad (column sums in LDS + WTA)", H * W * (2 + 2 + 4)),
                 "wta": ("k_bm_sad (column sums in LDS + WTA)", H * W * (2 + 2 + 4))}, ("wta",)
+    if sweep and lines:
+        rec_b = 8 * H * width1
+        st = 4 * D * eb * H * ((width1 + 35) // 36)  # boundary states of the E/W segments (36-column strips)
+        kern = {"sweep": ("k_sweep MODE 3 (S+SE+SW + in-kernel E/W lines -> partial)", vol * eb + 2 * vol + st),
+                "horizontal": ("k_ew_patch (segment check + repairs)", st),
+                "sweep_wta": ("k_sweep MODE 4 (N+NE+NW + partial + WTA)", vol * eb + 2 * vol + rec_b) if P_dirs == 8
+                else ("k_wta over the partial", 2 * vol + 4 * H * W)}
+        return kern, tuple(k for k in ("horizontal", "sweep", "sweep_wta") if stages[k][1] > 0)
     if sweep:
         rec_b = 8 * H * width1  # WTA winner record + sub-pixel inputs per pixel
         # E/W kernel (sm_api.hip ew_lanes): packed lines of 32 / 16 lanes where D % 64 / D % 32 == 0,
@@ -646,6 +708,22 @@ def design_kernels(args, stages, H, W, D, p, P_dirs, sweep, bm):
     kern = {"paths": ("k_sgm_paths (all directions)", 2 * P_dirs * vol * eb),
             "wta": ("k_wta", P_dirs * vol * eb + 2 * H * W)}
     return kern, ("paths", "wta")
+
+
+# VALU issue ceiling of the chip: 1024 SIMDs x 2.4 GHz / 4 cycles per wave64 instruction
+VALU_PEAK_GINSTR = 1024 * 2.4 / 4
+
+
+def valu_roofline(valu, launch_s):
+    """StereoBM (no cost volume: the SAD window sums are VALU work): the dominant kernel against
+    the VALU issue ceiling, from the SQ_INSTS_VALU counter file (tools/valu.sh --mode bm)."""
+    insts = valu.get("insts_per_launch") if isinstance(valu, dict) else None
+    ach = insts / launch_s / 1e9 if insts and launch_s > 0 else None
+    return {"bound": "valu", "achieved": ach, "peak": VALU_PEAK_GINSTR, "unit": "G wave64 VALU instr/s",
+            "frac": ach / VALU_PEAK_GINSTR if ach else None,
+            "bound_note": "StereoBM has no cost volume to stream; its SAD sums are VALU work, so the frac is "
+                          "SQ_INSTS_VALU x 4 cycles / (1024 SIMDs x the launch's cycles at 2.4 GHz)"
+                          + ("" if ach else " (no VALU counter file for this mode: unmeasured)")}
 
 
 def read_traffic(args, dom, kernel_label, pairs_per_launch, sweep):

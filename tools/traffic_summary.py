@@ -28,20 +28,14 @@ for k, d in vals.items():
     wr = ws * 1024 if ws is not None else None
     summary["kernels"][k] = {"fetch_size_kb": fs, "write_size_kb": ws, "read_bytes_corrected": rd,
                              "write_bytes": wr, "hbm_bytes": (rd or 0) + (wr or 0)}
-    sweep = any("k_sweep" in n for n in vals)  # fused-sweep engine
-    targs = [t.strip() for t in k.split("<", 1)[1].split(">")[0].split(",")] if "<" in k else []
-    fallback = bool(targs) and targs[-1] == "true" and ("k_sgm_paths" in k or "k_wta" in k)  # guarded instances
-    if "k_sweep2<" in k or "k_sweep<" in k:  # sweep mode: 0 = down partial, 1/2 = with WTA
-        stage = "sweep" if targs[4 if "k_sweep2<" in k else 3] == "0" else "sweep_wta"
-    elif fallback:
-        stage = None
-    else:
-        stage = ("horizontal" if "k_ew<" in k or (sweep and "k_sgm_paths" in k) else "paths" if "k_sgm_paths" in k
-                 else "wta" if ("k_wta" in k or "k_row_wta" in k)
-                 else "cost" if any(c in k for c in ("k_census9x7", "k_sgbm_cost(", "k_cost_volume_f32")) else None)
-    if stage:
-        summary.setdefault("stages", {})[stage] = {"kernel": k, "hbm_bytes_per_launch": (rd or 0) + (wr or 0),
-                                                   "read_bytes": rd, "write_bytes": wr}
+    stage = bench.kernel_stage(k, vals)
+    if stage:  # a stage's kernels summed (the census cost stage = census images + Hamming volume)
+        st = summary.setdefault("stages", {}).setdefault(stage, {"kernel": "", "hbm_bytes_per_launch": 0.0,
+                                                                 "read_bytes": 0.0, "write_bytes": 0.0})
+        st["kernel"] = (st["kernel"] + " + " if st["kernel"] else "") + k
+        st["hbm_bytes_per_launch"] += (rd or 0) + (wr or 0)
+        st["read_bytes"] += rd or 0
+        st["write_bytes"] += wr or 0
 # pairs per launch of the profiled run, from the bench line it printed (launch groups can
 # be smaller than --pairs-per-gpu: sm_api.hip group_size)
 summary["pairs_per_launch"] = None

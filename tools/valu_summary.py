@@ -42,18 +42,21 @@ for k, d in vals.items():
         e["wait_any_frac"] = m.get("SQ_WAIT_ANY", 0) / m["SQ_WAVE_CYCLES"]
         e["active_frac"] = m.get("SQ_ACTIVE_INST_ANY", 0) / m["SQ_WAVE_CYCLES"]
     summary["kernels"][k] = e
-    targs = [t.strip() for t in k.split("<", 1)[1].split(">")[0].split(",")] if "<" in k else []
-    fallback = bool(targs) and targs[-1] == "true" and ("k_sgm_paths" in k or "k_wta" in k)
-    if "k_sweep2<" in k or "k_sweep<" in k:
-        stage = "sweep" if targs[4 if "k_sweep2<" in k else 3] == "0" else "sweep_wta"
-    elif fallback:
-        stage = None
-    else:
-        stage = ("horizontal" if "k_ew<" in k or (sweep and "k_sgm_paths" in k) else "paths" if "k_sgm_paths" in k
-                 else "wta" if ("k_wta" in k or "k_row_wta" in k)
-                 else "cost" if any(c in k for c in ("k_census9x7", "k_sgbm_cost(", "k_cost_volume_f32")) else None)
-    if stage:
-        summary.setdefault("stages", {})[stage] = dict(e, kernel=k)
+    stage = bench.kernel_stage(k, vals)
+    if stage:  # a stage's kernels summed (instructions and the cycles of its launches)
+        st = summary.setdefault("stages", {}).get(stage)
+        if st is None:
+            summary["stages"][stage] = dict(e, kernel=k)
+        else:
+            st["kernel"] += " + " + k
+            for c in ("sq_insts_valu", "sq_waves", "sq_wave_cycles", "sq_wait_any", "sq_active_inst_any", "kernel_cycles"):
+                if c in e and c in st:
+                    st[c] += e[c]
+            st["valu_issue_frac"] = st["sq_insts_valu"] * ISSUE_CYCLES / (SIMDS * st["kernel_cycles"]) \
+                if st.get("kernel_cycles") else None
+            if st.get("sq_wave_cycles"):
+                st["wait_any_frac"] = st.get("sq_wait_any", 0) / st["sq_wave_cycles"]
+                st["active_frac"] = st.get("sq_active_inst_any", 0) / st["sq_wave_cycles"]
 summary["pairs_per_launch"] = None
 for line in open(out + "/pmc.log"):
     if line.startswith("{"):
