@@ -19,7 +19,11 @@ buffers ("gather pair i while computing pair i+1").
 """
 from __future__ import annotations
 
+from collections import namedtuple
 from typing import Callable, Sequence
+
+# one point-to-point transfer of a gather: kind "send" | "recv", the byte view, the peer rank
+P2P = namedtuple("P2P", "kind tensor peer")
 
 
 def shard_range(npairs: int, rank: int, world: int):
@@ -43,24 +47,38 @@ def _bytes(t):
     return t.contiguous().view(torch.uint8)
 
 
-def _gather_ops(local, out, npairs: int, group=None):
-    """P2P operations of one gather: non-root ranks send ``local`` to rank 0;
+def _p2p_plan(local, out, npairs: int, rank: int, world: int):
+    """The transfers of one gather (group ranks): non-root ranks send ``local`` to rank 0;
     rank 0 receives every other rank's block into its rows of ``out``."""
-    import torch.distributed as dist
-
-    world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
     ops = []
     if rank == 0:
         for r in range(1, world):
             s, c = shard_range(npairs, r, world)
             if c:
-                ops.append(dist.P2POp(dist.irecv, _bytes(out[s:s + c]), dist.get_global_rank(group, r)
-                                      if group is not None else r, group))
+                ops.append(P2P("recv", _bytes(out[s:s + c]), r))
     elif local.shape[0]:
-        ops.append(dist.P2POp(dist.isend, _bytes(local), dist.get_global_rank(group, 0)
-                              if group is not None else 0, group))
+        ops.append(P2P("send", _bytes(local), 0))
     return ops
+
+
+def dist_transport(plan, group=None):
+    """The transfers of a plan as one ``batch_isend_irecv`` (RCCL / gloo); returns its works."""
+    import torch.distributed as dist
+
+    if not plan:
+        return []
+    ops = [dist.P2POp(dist.isend if o.kind == "send" else dist.irecv, o.tensor,
+                      dist.get_global_rank(group, o.peer) if group is not None else o.peer, group) for o in plan]
+    return dist.batch_isend_irecv(ops)
+
+
+def _gather_ops(local, out, npairs: int, group=None):
+    """torch P2P operations of one gather (see _p2p_plan)."""
+    import torch.distributed as dist
+
+    plan = _p2p_plan(local, out, npairs, dist.get_rank(group), dist.get_world_size(group))
+    return [dist.P2POp(dist.isend if o.kind == "send" else dist.irecv, o.tensor,
+                       dist.get_global_rank(group, o.peer) if group is not None else o.peer, group) for o in plan]
 
 
 def gather_to_root(local, npairs: int, group=None, out=None):
@@ -109,16 +127,24 @@ class OverlappedGather:
     ``exposed_ms()`` (CUDA): the time the caller's stream stood waiting for a
     gather (events around every wait, ``drain`` included), i.e. the part of
     the gather that compute did not hide.
+
+    ``transport(plan) -> works`` moves one step's transfers (a list of ``P2P``);
+    the default is ``dist_transport`` over the process group.  ``rank`` / ``world``
+    default to the group's.  tests/test_gpu_gather.py runs the CUDA branch with a
+    stream-ordered device-copy transport (two ranks' roles in one process on one
+    GPU: RCCL refuses two ranks on one device and torch refuses a send to self).
     """
 
-    def __init__(self, npairs: int, count: int, H: int, W: int, dtype, device, group=None, depth: int = 2):
+    def __init__(self, npairs: int, count: int, H: int, W: int, dtype, device, group=None, depth: int = 2,
+                 rank: int | None = None, world: int | None = None, transport: Callable | None = None):
         import torch
         import torch.distributed as dist
 
         self.torch, self.dist, self.group = torch, dist, group
         self.npairs, self.depth = npairs, depth
-        self.world = dist.get_world_size(group)
-        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group) if world is None else world
+        self.rank = dist.get_rank(group) if rank is None else rank
+        self.transport = transport or (lambda plan: dist_transport(plan, group))
         self.start, c = shard_range(npairs, self.rank, self.world)
         if c != count:
             raise ValueError(f"rank {self.rank} owns {c} pairs, got count {count}")
@@ -150,7 +176,7 @@ class OverlappedGather:
     def launch(self, k: int):
         """Start step k's transfers after the work already on the caller's stream."""
         slot = k % self.depth
-        ops = _gather_ops(self.blocks[slot], self.results[slot], self.npairs, self.group)
+        ops = _p2p_plan(self.blocks[slot], self.results[slot], self.npairs, self.rank, self.world)
         if not ops:  # world 1 (or an empty block): rank 0 computed into its rows already
             return
         if self.cuda:
@@ -162,7 +188,7 @@ class OverlappedGather:
                 if self.timing:
                     a = torch.cuda.Event(enable_timing=True)
                     a.record(self.stream)
-                for w in self.dist.batch_isend_irecv(ops):
+                for w in self.transport(ops):
                     w.wait()  # the side stream waits for RCCL's stream (no host wait)
                 ev = torch.cuda.Event(enable_timing=self.timing)
                 ev.record(self.stream)
@@ -172,7 +198,7 @@ class OverlappedGather:
             self.blocks[slot].record_stream(self.stream)
             self.pending[slot] = ev
         else:
-            self.pending[slot] = self.dist.batch_isend_irecv(ops)
+            self.pending[slot] = self.transport(ops)
 
     def wait(self, k: int):
         """The caller (its stream on CUDA) waits for step k's transfers."""
