@@ -3092,7 +3092,7 @@ long long sm_debug_fetch(sm_ctx* ctx, int what, void* host, size_t bytes)
     case 2: need = img * 2; break;
     case 3: need = img * 16; break;
 #if SWEEP_STATS
-    case 20: need = 24 * 8; break;  // sm_sweep.hpp SWEEP_STATS counters (read and cleared)
+    case 20: need = 48 * 8; break;  // sm_sweep.hpp SWEEP_STATS counters (read and cleared)
     case 21: need = 2048; break;    // the down sweep's workgroups' XCC ids (| 0x80), by linear id
     case 22: need = 6 * 65536 * 8; break;  // snapshot publish / observe times (s_memrealtime)
 #endif

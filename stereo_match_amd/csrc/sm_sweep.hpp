@@ -53,7 +53,9 @@ typedef __attribute__((address_space(1))) unsigned long long gu64;
 constexpr uint32_t SW_SPIN_LIMIT = 1u << 19;
 
 // SWEEP_STATS builds (tools/build_variant.sh): shader-clock cycles each wave spends in
-// the row / block synchronisation, summed per mode into SweepArgs::stats[8 * MODE + k]:
+// the row / block synchronisation, summed per mode into SweepArgs::stats[8 * MODE + k]
+// (MODE 3's line waves, words 40..44: 40 own waves in wait_lines, 41 line waves in wait_cons,
+// 42 line waves in barriers, 43 line waves' lifetime, 44 line waves):
 // 0 poller in polls, 1 poller in barriers, 2 compute waves in wait_row, 3 compute waves
 // in block barriers, 4 compute waves' lifetime, 5 compute waves, 6 poller lifetime
 #if SWEEP_STATS
@@ -584,16 +586,19 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
             const rsrc_t rs = make_rsrc(a.st + (size_t)pair * a.st_pair, a.st_pair);
             __builtin_amdgcn_s_setprio(SWEEP_LINE_PRIO);
             int bn = 0;  // barrier pairs passed (the compute waves' two per block of HB rows)
+            [[maybe_unused]] uint64_t lst_cons = 0, lst_bar = 0;
+            SW_T0(lst_life);
             auto barriers_to = [&](int y0) {
                 while (bn < nblk && (bn + 1) * HB + LEAD <= y0) {
+                    SW_T0(tb);
                     if (!(a.dbg & 4)) lds_barrier();
                     if (bn + 1 < nblk) lds_barrier();
+                    SW_ACC(lst_bar, tb);
                     bn++;
                 }
             };
             // every own wave has consumed the rows below `need` from the ring
-            auto wait_cons = [&](int need) {
-                if (need <= 0) return;
+            auto wait_cons_spin = [&](int need) {
                 for (uint32_t spins = 0;; spins++) {
                     uint32_t m = 0xFFFFFFFFu;
 #pragma unroll
@@ -610,6 +615,12 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
                     }
                     __builtin_amdgcn_s_sleep(1);
                 }
+            };
+            auto wait_cons = [&](int need) {
+                if (need <= 0) return;
+                SW_T0(tc);
+                wait_cons_spin(need);
+                SW_ACC(lst_cons, tc);
             };
             // Steps run in chunks of LPF (the cost-load ring): the warmup (rounded up to whole
             // chunks, w >= a.ewarm: a longer warmup only makes the guess better), then the CW / 2
@@ -720,6 +731,14 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
                 __hip_atomic_store(&linecnt[li], (uint32_t)(t + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
             barriers_to(0x7FFFFFFF);
+#if SWEEP_STATS
+            if (a.stats && lane == 0) {
+                atomicAdd(a.stats + 41, (unsigned long long)lst_cons);
+                atomicAdd(a.stats + 42, (unsigned long long)lst_bar);
+                atomicAdd(a.stats + 43, (unsigned long long)(__builtin_readcyclecounter() - lst_life));
+                atomicAdd(a.stats + 44, 1ull);
+            }
+#endif
             return;
         }
     }
@@ -772,7 +791,8 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
         SW_ACC(st_wait, tw);
     };
     // MODE 3: row s of the ring is complete (its line wave has finished the batch holding it)
-    auto wait_lines = [&](int s) {
+    [[maybe_unused]] uint64_t st_wl = 0;
+    auto wait_lines_spin = [&](int s) {
         if constexpr (LINES) {
             const int li = (s / LG::RPW) % LG::NLW;
             const uint32_t need = (uint32_t)(s / (LG::RPW * LG::NLW) + 1);
@@ -792,6 +812,11 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
         } else {
             (void)s;
         }
+    };
+    auto wait_lines = [&](int s) {
+        SW_T0(twl);
+        wait_lines_spin(s);
+        SW_ACC(st_wl, twl);
     };
     auto end_row = [&](int j, int s) {
         if (!ROWSYNC || j == HB - 1) {
@@ -1209,6 +1234,7 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
                 atomicAdd(a.stats + 8 * MODE + 3, (unsigned long long)st_bbar);
                 atomicAdd(a.stats + 8 * MODE + 4, (unsigned long long)(__builtin_readcyclecounter() - st_clife));
                 atomicAdd(a.stats + 8 * MODE + 5, 1ull);
+                if (LINES) atomicAdd(a.stats + 40, (unsigned long long)st_wl);
             }
 #endif
         };

@@ -31,10 +31,15 @@ eng.reset_timing()
 for _ in range(reps):
     eng.compute_batch_device(L.data_ptr(), R.data_ptr(), n, H * W, H, W, W, sp, out.data_ptr())
 eng.synchronize()
-raw = np.frombuffer(eng.debug_fetch(20), np.uint64).reshape(3, 8)
+raw = np.frombuffer(eng.debug_fetch(20), np.uint64).reshape(6, 8)
 st = raw.astype(np.float64)
 print({k: round(v[0] * 1e3 / max(v[2], 1), 1) for k, v in eng.timing().items() if v[1]})
-for m in range(3):
+ln = st[5]
+if ln[4]:  # MODE 3's line waves (words 40..44)
+    own_life = st[3][4]
+    print(f"mode 3 lines: {int(ln[4])} line waves, life {ln[3] / ln[4] / reps:.0f} cyc/launch; wait_cons "
+          f"{ln[1] / ln[3]:.3f}, barriers {ln[2] / ln[3]:.3f}; own waves in wait_lines {ln[0] / max(own_life, 1):.3f}")
+for m in range(5):
     s = st[m]
     if s[5] == 0:
         continue
