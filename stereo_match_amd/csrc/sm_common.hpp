@@ -224,8 +224,10 @@ __device__ __forceinline__ uint32_t Line<64>::min(uint32_t v)
 __device__ __forceinline__ uint32_t group_min_u32_wave(uint32_t v)
 {
     v = row16_min(v);
-    return ::min(::min(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
-                 ::min(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
+    // readlane returns int: compare as unsigned (keys use the top bit)
+    const uint32_t a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, 16),
+                   c = __builtin_amdgcn_readlane(v, 32), d = __builtin_amdgcn_readlane(v, 48);
+    return ::min(::min(a, b), ::min(c, d));
 }
 __device__ __forceinline__ uint32_t group_max_u32_wave(uint32_t v)
 {
@@ -233,8 +235,9 @@ __device__ __forceinline__ uint32_t group_max_u32_wave(uint32_t v)
     v = ::max(v, perm_dpp<DPP_QP_XOR2>(v));
     v = ::max(v, perm_dpp<DPP_ROW_HALF_MIRROR>(v));
     v = ::max(v, perm_dpp<DPP_ROW_MIRROR>(v));
-    return ::max(::max(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
-                 ::max(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
+    const uint32_t a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, 16),
+                   c = __builtin_amdgcn_readlane(v, 32), d = __builtin_amdgcn_readlane(v, 48);
+    return ::max(::max(a, b), ::max(c, d));
 }
 __device__ __forceinline__ uint32_t group_sum_u32_wave(uint32_t v)
 {

@@ -187,7 +187,8 @@ constexpr int wide_ncw(int D, int ct_bytes)
 #define SWEEP_NLW 4  // line waves per workgroup (one per SIMD)
 #endif
 #ifndef SWEEP_LINE_PRIO
-#define SWEEP_LINE_PRIO 2  // issue priority of the line waves (compute waves: 3 on the hand-off chain, else 1)
+#define SWEEP_LINE_PRIO 1  // issue priority of the line waves (compute waves: 3 on the hand-off chain, else 1;
+                           // measured: 2 costs 9 us per pair, 0 and 1 tie)
 #endif
 // cost loads in flight per line lane (at most; the largest divisor of CW / 2 below this, so
 // that the line's phases fall on ring-chunk boundaries): the lines run ahead of the compute
@@ -209,6 +210,15 @@ constexpr int largest_divisor_upto(int n, int cap)
 #ifndef SWEEP_LEAD_BLOCKS
 #define SWEEP_LEAD_BLOCKS 1
 #endif
+// MODE 3 without workgroup barriers: the block hand-off (the poller's halo write) is ordered by
+// LDS counters (the halo waves' row counters -> the poller, the poller's block counter -> the
+// compute waves), so the line waves never stand in an s_barrier: they fill the cycles the
+// compute waves spend waiting for the neighbouring strips with E / W work, throttled only by
+// the ring (any LR >= RPW is deadlock-free: the earliest unproduced batch needs only rows the
+// own waves can consume without it)
+#ifndef SWEEP_LINE_NOBAR
+#define SWEEP_LINE_NOBAR 1
+#endif
 constexpr int kMaxLds = 163840;  // gfx950: LDS one workgroup may declare
 template <int VL, int DPL, int NCW_, int MODE>
 struct LineGeo {
@@ -223,8 +233,9 @@ struct LineGeo {
     static constexpr int FIT = (kMaxLds - BASE) / ROWB;
     static constexpr int LEAD0 = SWEEP_LEAD_BLOCKS * G::HB;
     static constexpr int LEAD = LEAD0 + RPW <= FIT ? LEAD0 : (FIT > RPW ? (FIT - RPW) / RPW * RPW : 0);
-    static constexpr int LR = LEAD + 2 * RPW <= FIT ? LEAD + 2 * RPW : LEAD + RPW;
-    static constexpr bool BUILT = ON && NLW >= 1 && DPL % 2 == 0 && !SWEEP_U32 && LEAD + RPW <= FIT &&
+    static constexpr int LR = SWEEP_LINE_NOBAR ? FIT : LEAD + 2 * RPW <= FIT ? LEAD + 2 * RPW : LEAD + RPW;
+    static constexpr bool BUILT = ON && NLW >= 1 && DPL % 2 == 0 && !SWEEP_U32 &&
+                                  (SWEEP_LINE_NOBAR ? RPW <= FIT : LEAD + RPW <= FIT) &&
                                   G::CW % 2 == 0 && G::HB % RPW == 0 && RPW >= 1;
     // ring chunk of the line loop, per cost type (a divisor of CW / 2)
     template <typename CT>
@@ -410,6 +421,7 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
     constexpr bool EWIN = MODE == 1 || MODE == 2;   // E / W path volumes read (k_ew)
     constexpr bool PARTR = MODE == 2 || MODE == 4;  // the down sweep's partial read
     constexpr bool LINES = MODE == 3;               // E / W lines in the kernel (line waves)
+    constexpr bool NOBAR = LINES && SWEEP_LINE_NOBAR;  // block hand-off by LDS counters
     static_assert(!LINES || LG::BUILT, "MODE 3 instance not built for this geometry");
     static_assert(MODE < 3 || (DPL % 2 == 0 && !SWEEP_U32), "MODES 3 / 4 run the packed row loops only");
     constexpr int NTH = sweep_threads<VL, DPL, NCW_, MODE>();
@@ -450,11 +462,13 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
     // rows each own wave has consumed from the ring
     __shared__ __attribute__((aligned(16))) uint16_t ring[LINES ? LG::LR : 1][LINES ? CW : 1][LINES ? D : 2];
     __shared__ uint32_t linecnt[LINES ? LG::NLW : 1], conscnt[NCW];
+    __shared__ uint32_t pollcnt;  // NOBAR: blocks whose halo snapshot the poller has written
 
     for (int i = threadIdx.x; i < 2 * 2 * COLS * D / 2; i += NTH)
         reinterpret_cast<uint32_t*>(&lv[0][0][0][0])[i] = 0;
     for (int i = threadIdx.x; i < 2 * 2 * COLS; i += NTH) (&lmin[0][0][0])[i] = 0;
     for (int i = threadIdx.x; i < NCW; i += NTH) rowcnt[i] = conscnt[i] = 0;
+    if (threadIdx.x == 0) pollcnt = 0;
     if constexpr (LINES)
         for (int i = threadIdx.x; i < LG::NLW; i += NTH) linecnt[i] = 0;
     __syncthreads();
@@ -510,7 +524,29 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
 #endif
                 }
             };
-            if (ROWSYNC) {
+            if (NOBAR) {
+                // the neighbours' snapshot, then the halo waves' last row of the block in LDS (the
+                // halo slots the poller overwrites; their readers wait for pollcnt)
+                poll();
+                SW_T0(tb);
+                const uint32_t need = (uint32_t)((b + 1) * HB);
+                for (uint32_t spins = 0; !(a.dbg & 4); spins++) {
+                    const uint32_t n0 = __builtin_amdgcn_readfirstlane(
+                        __hip_atomic_load(&rowcnt[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+                    const uint32_t n1 = __builtin_amdgcn_readfirstlane(
+                        __hip_atomic_load(&rowcnt[NCW - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+                    if (min(n0, n1) >= need) {
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+                        break;
+                    }
+                    if (spins >= SW_SPIN_LIMIT) {
+                        if (lane == 0) atomicOr(a.err, 1u);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                SW_ACC(st_bar, tb);
+            } else if (ROWSYNC) {
                 if (SWEEP_EARLY_XCHG == 2) poll();
                 SW_T0(tb);
                 if (!(a.dbg & 4)) lds_barrier();  // the compute waves' end-of-block barrier
@@ -522,7 +558,7 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
                     if (!(a.dbg & 4)) lds_barrier();  // 4: timing only, no row barriers
                 }
             }
-            if (SWEEP_EARLY_XCHG != 2) poll();
+            if (SWEEP_EARLY_XCHG != 2 && !NOBAR) poll();
             if (b + 1 < nblk) {
                 if (xchg) {
                     const int wb = (b * HB + HB - 1) & 1;
@@ -542,9 +578,14 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
                         }
                     }
                 }
-                SW_T0(tb2);
-                lds_barrier();
-                SW_ACC(st_bar, tb2);
+                if (NOBAR) {
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+                    __hip_atomic_store(&pollcnt, (uint32_t)(b + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                } else {
+                    SW_T0(tb2);
+                    lds_barrier();
+                    SW_ACC(st_bar, tb2);
+                }
             }
         }
 #if SWEEP_STATS
@@ -589,6 +630,7 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
             [[maybe_unused]] uint64_t lst_cons = 0, lst_bar = 0;
             SW_T0(lst_life);
             auto barriers_to = [&](int y0) {
+                if constexpr (NOBAR) return;
                 while (bn < nblk && (bn + 1) * HB + LEAD <= y0) {
                     SW_T0(tb);
                     if (!(a.dbg & 4)) lds_barrier();
@@ -818,6 +860,27 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
         wait_lines_spin(s);
         SW_ACC(st_wl, twl);
     };
+    // NOBAR: the poller has written block b's halo snapshot into LDS
+    auto wait_poll = [&](int b) {
+        if constexpr (NOBAR) {
+            for (uint32_t spins = 0; !sync_dead; spins++) {
+                const uint32_t n = __builtin_amdgcn_readfirstlane(
+                    __hip_atomic_load(&pollcnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+                if (n >= (uint32_t)b) {
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+                    return;
+                }
+                if (spins >= SW_SPIN_LIMIT) {
+                    if (lane == 0) atomicOr(a.err, 1u);
+                    sync_dead = true;
+                    return;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        } else {
+            (void)b;
+        }
+    };
     auto end_row = [&](int j, int s) {
         if (!ROWSYNC || j == HB - 1) {
             if (!(a.dbg & 4)) lds_barrier();
@@ -950,7 +1013,7 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
                         if constexpr (OWN && PARTR) asm volatile("" : "+v"(Pin[i])::"memory");
                     }
                     issue_r(k, s + PF);
-                    if (ROWSYNC && j > 0) wait_row(s);
+                    if (ROWSYNC && (j > 0 || NOBAR)) wait_row(s);
                     // diagonal predecessors: column c-1 (A) and c+1 (B) of the previous row
                     uint32_t LA[NS][NP], LB[NS][NP], mA[NS], mB[NS];
 #pragma unroll
@@ -1087,7 +1150,7 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
                     // the row is published (neighbour counters) or, at a block end and
                     // without row sync, closed by a barrier; the poller writes the halo
                     // snapshot after the block-end barrier, while the waves run their WTA
-                    if (!ROWSYNC || j == HB - 1) {
+                    if (!ROWSYNC || (j == HB - 1 && !NOBAR)) {
                         SW_T0(tb);
                         if (!(a.dbg & 4)) lds_barrier();
                         SW_ACC(st_bbar, tb);
@@ -1224,7 +1287,8 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
                 }
                 if (b + 1 < nblk) {
                     SW_T0(tb);
-                    lds_barrier();  // the poller has written the halo snapshot
+                    if constexpr (NOBAR) wait_poll(b + 1);
+                    else lds_barrier();  // the poller has written the halo snapshot
                     SW_ACC(st_bbar, tb);
                 }
             }
