@@ -274,12 +274,16 @@ int sm_get_counters(sm_ctx* ctx, long long* sweep_fallbacks);
  *                               quantised value fell outside [0, 4095] and was clamped;
  *   SM_COUNTER_VOLUME_NAN       external cost-volume cells that were NaN (cost 4095);
  *   SM_COUNTER_LINE_GROUPS      launch groups whose horizontal paths ran inside the down
- *                               sweep (host-side count of the engine's choice). */
+ *                               sweep (host-side count of the engine's choice);
+ *   SM_COUNTER_EW_OPEN          of the EW_REPAIRS segments, those whose recomputed values had
+ *                               not met the speculative ones by the strip's far end (the true
+ *                               state was carried into the next strip). */
 #define SM_COUNTER_SWEEP_FALLBACKS 0
 #define SM_COUNTER_EW_REPAIRS 1
 #define SM_COUNTER_VOLUME_CLAMPED 2
 #define SM_COUNTER_VOLUME_NAN 3
 #define SM_COUNTER_LINE_GROUPS 4
+#define SM_COUNTER_EW_OPEN 5
 int sm_get_counter(sm_ctx* ctx, int which, long long* value);
 
 /* Restrict the context's own streams (the default stream and its internal

@@ -426,14 +426,16 @@ class Engine:
     def synchronize(self):
         self._check(self._lib.sm_synchronize(self.ctx))
 
-    COUNTERS = ("sweep_fallbacks", "ew_repairs", "volume_clamped", "volume_nan", "line_groups")  # SM_COUNTER_*
+    COUNTERS = ("sweep_fallbacks", "ew_repairs", "volume_clamped", "volume_nan", "line_groups",
+                "ew_open")  # SM_COUNTER_*
 
     def counters(self) -> dict:
         """Counters since the engine was created (include/stereo_match_amd.h SM_COUNTER_*):
         sweep_fallbacks (launch groups the guarded fallback recomputed), ew_repairs (in-sweep
         E/W strip segments the patch pass recomputed), volume_clamped / volume_nan (external
         cost-volume cells clamped by the quantisation window / NaN), line_groups (launch groups
-        whose E/W paths ran inside the down sweep)."""
+        whose E/W paths ran inside the down sweep), ew_open (of the ew_repairs, segments whose
+        recomputation had not met the speculative values by the strip's end)."""
         out = {}
         n = ctypes.c_longlong()
         for i, name in enumerate(self.COUNTERS):

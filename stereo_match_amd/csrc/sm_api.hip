@@ -110,9 +110,10 @@ constexpr int DBG_FORCE_FALLBACK = 1 << 23;
 // up waiting; cleared by the host before each group), the sticky error of the
 // (unguarded) hybrid engine, and the count of fallback recomputations
 constexpr int ERR_GROUP0 = 0, ERR_STICKY = 32, ERR_FALLBACKS = 48;
-// E/W strip segments the patch pass recomputed (u32), and (u64 words at 52, 54) the external
-// cost-volume cells clamped by the quantisation window / NaN cells
-constexpr int ERR_EW_REPAIRS = 49, ERR_VOL_CLAMPED = 52, ERR_VOL_NAN = 54;
+// E/W strip segments the patch pass recomputed and (50) those whose walk never met within the
+// strip (u32), and (u64 words at 52, 54) the external cost-volume cells clamped by the
+// quantisation window / NaN cells
+constexpr int ERR_EW_REPAIRS = 49, ERR_EW_OPEN = 50, ERR_VOL_CLAMPED = 52, ERR_VOL_NAN = 54;
 // timing ablation: no guarded fallback launches after the sweeps
 constexpr int DBG_NO_FALLBACK = (int)0x80000000u;
 // flags only the ablation build (SM_ABLATIONS) accepts: timing switches whose results are
@@ -831,6 +832,7 @@ bool sweeps_fit(sm_ctx* ctx, const Norm& n, bool hybrid, bool lines = false)
     for (int k = 0; k < count; k++) {
         SweepFit f;
         if (!sweep_capacity(ctx, n, modes[k], 0, f)) return false;
+        if (lines && modes[k] == 3 && f.nwg > smk::patch_max_strips(n.D)) return false;  // the patch pass's masks
     }
     return true;
 }
@@ -2905,7 +2907,7 @@ int sm_get_counter(sm_ctx* ctx, int which, long long* value)
 {
     if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
     if (!value) return fail(ctx, SM_E_ARG, "value is NULL");
-    if (which < SM_COUNTER_SWEEP_FALLBACKS || which > SM_COUNTER_LINE_GROUPS)
+    if (which < SM_COUNTER_SWEEP_FALLBACKS || which > SM_COUNTER_EW_OPEN)
         return fail(ctx, SM_E_ARG, "unknown counter %d", which);
     long long v = 0;
     if (which == SM_COUNTER_LINE_GROUPS) {
@@ -2921,7 +2923,9 @@ int sm_get_counter(sm_ctx* ctx, int which, long long* value)
             v = (long long)u;
         } else {
             uint32_t u = 0;
-            const int word = which == SM_COUNTER_SWEEP_FALLBACKS ? ERR_FALLBACKS : ERR_EW_REPAIRS;
+            const int word = which == SM_COUNTER_SWEEP_FALLBACKS ? ERR_FALLBACKS
+                             : which == SM_COUNTER_EW_OPEN         ? ERR_EW_OPEN
+                                                                   : ERR_EW_REPAIRS;
             HIP_TRY(ctx, hipMemcpy(&u, (uint32_t*)ctx->sweep_err.p + word, 4, hipMemcpyDeviceToHost));
             v = u;
         }

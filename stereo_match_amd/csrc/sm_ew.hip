@@ -96,6 +96,7 @@ hipError_t patch_d(int D, const EwPatchArgs& a, int npairs, hipStream_t stream)
 
 hipError_t ew_patch_launch(int D, int ct_bytes, const EwPatchArgs& a, int npairs, hipStream_t stream)
 {
+    if (a.nwg > patch_max_strips(D)) return hipErrorInvalidValue;
     return ct_bytes == 1 ? patch_d<uint8_t>(D, a, npairs, stream) : patch_d<uint16_t>(D, a, npairs, stream);
 }
 

@@ -118,14 +118,21 @@ __global__ void __launch_bounds__(256) k_ew(EwArgs a)
 // ---------------------------------------------------------------------------
 // Patch pass after a MODE 3 sweep (sm_sweep.hpp line waves).  Strip k's E line
 // started from the zero state `ewarm` columns before the strip, so its values are exact from
-// the column where its state met the true one.  Walking one row's strips in path order, the
-// trusted state entering strip k is strip k-1's stored end state as long as every earlier
-// strip was exact (or was repaired up to the meeting point); where the stored entering state
-// of strip k differs from it, the segment is recomputed from the trusted state beside the
-// speculative one (from k's stored entering state) and the partial gets (true - speculative)
-// column by column until the two trajectories are equal, after which every later value is
-// equal.  A segment that never meets hands its true end state to the next strip.  One line of
-// VL lanes per image row walks E, then W, so no two lines touch one partial cell.
+// the column where its state met the true one.  Stored per (row, strip, direction): s_k, the
+// state entering the strip, and e_k, the state at its far end.  Along a row's path order a
+// strip is exact iff the state truly entering it equals the one its values came from; the
+// first strip of each path enters from outside the domain (exact).
+//   check: strip k is flagged where s_k != e_{k-1};
+//   phase A (the wave's LPW lines in parallel, one flagged strip each): recompute strip k
+//     from e_{k-1} beside its speculative trajectory from s_k and add (true - speculative)
+//     to the partial column by column until the two trajectories are equal (every later
+//     value is then equal).  Exact when strip k-1 is exact at its far end, i.e. unless
+//     strip k-1's own walk never met;
+//   phase B (rare; one line, in path order): after a strip whose walk never met (its end
+//     state c_k, kept in its s_k slot), the next strips' values came from e_{k-1} while the
+//     true state is the carried one: the same walk with (applied, true) = (e_{k-1}, carried)
+//     until a strip's trajectories meet.
+// E then W (the two directions touch the same partial cells), four rows per workgroup.
 // u16 costs: the MODE 3 partial saturates at 0xFFFF; a cell below that holds the exact sum
 // (every term >= 0), one at 0xFFFF stays there (the true five-path sum is then still
 // >= 65535 - 2 * 16383 > 32767, so the WTA's 32767 clamp sees the same value).
@@ -175,10 +182,107 @@ __global__ void __launch_bounds__(256) k_ew_patch(EwPatchArgs a)
         m = ::min(m & 0xFFFFu, m >> 16);
         return group_min<VL>(m) * 0x10001u;
     };
-    uint32_t nfix = 0;
+    auto load_state = [&](uint32_t off, uint32_t (&v)[NP]) {
+        RawBytes<CB> b;
+        b.load(rs, off);
+        unpack_ct_pk<CT, DPL>(b, v);
+    };
+    // the values of strip k (direction dir) came from the trajectory entering at A; the true
+    // one enters at T: add (true - applied) to the partial until the two meet.  Returns met;
+    // otherwise T holds the true trajectory's state at the strip's far end.  Line-divergent.
+    auto walk = [&](int k, int dir, const uint32_t (&A)[NP], uint32_t (&T)[NP]) -> bool {
+        uint32_t Lq[2][NP], mq[2];
+#pragma unroll
+        for (int q = 0; q < NP; q++) {
+            Lq[0][q] = A[q];
+            Lq[1][q] = T[q];
+        }
+        mq[0] = state_min(Lq[0]);
+        mq[1] = state_min(Lq[1]);
+        const int x0 = k * CW, ncol = ::min(CW, W1 - x0);  // W: every repaired strip is full
+        bool met = false;
+        // columns in chunks of RC: the chunk's costs and partial slices load together
+        for (int o0 = 0; o0 < ncol && !met; o0 += RC) {
+            RawBytes<CB> cc[RC];
+            RawBytes<DPL * 2> pb[RC];
+#pragma unroll
+            for (int u = 0; u < RC; u++) {
+                const int o = o0 + u;
+                const int c = dir ? x0 + CW - 1 - o : x0 + o;
+                cc[u].load(rc, o < ncol ? cell(c) * (uint32_t)sizeof(CT) : kOOB);
+                pb[u].load(rp, o < ncol ? cell(c) * 2u : kOOB);
+            }
+#pragma unroll
+            for (int u = 0; u < RC; u++) {  // (no break: the loop must unroll)
+                const int o = o0 + u;
+                if (o >= ncol || met) continue;
+                const int c = dir ? x0 + CW - 1 - o : x0 + o;
+                uint32_t C2[2][NP], Ln[2][NP], mn[2];
+                unpack_ct_pk<CT, DPL>(cc[u], C2[0]);
+#pragma unroll
+                for (int q = 0; q < NP; q++) C2[1][q] = C2[0][q];
+                sweep_step2n<VL, NP, H16, 2>(Lq, mq, C2, P1p, P2p, eL, eR, Ln, mn);
+                if (same_state(Ln[0], Ln[1])) {
+                    met = true;
+                    continue;
+                }
+                uint32_t P[NP];
+#pragma unroll
+                for (int q = 0; q < NP; q++) {
+                    if constexpr (SAT) {
+                        uint32_t h[2];
+#pragma unroll
+                        for (int e = 0; e < 2; e++) {
+                            const uint32_t pv = (pb[u].w[q] >> (16 * e)) & 0xFFFFu;
+                            const uint32_t sv = (Ln[0][q] >> (16 * e)) & 0xFFFFu;
+                            const uint32_t tv = (Ln[1][q] >> (16 * e)) & 0xFFFFu;
+                            h[e] = pv == 0xFFFFu ? pv : ::min(pv - sv + tv, 0xFFFFu);
+                        }
+                        P[q] = h[0] | (h[1] << 16);
+                    } else {  // census: every sum < 2^11, the u16 wrap is exact
+                        P[q] = pk_add(pk_sub(pb[u].w[q], Ln[0][q]), Ln[1][q]);
+                    }
+                }
+                bstore_n<uint32_t, NP>(rp, cell(c) * 2u, P);
+#pragma unroll
+                for (int q = 0; q < NP; q++) {
+                    Lq[0][q] = Ln[0][q];
+                    Lq[1][q] = Ln[1][q];
+                }
+                mq[0] = mn[0];
+                mq[1] = mn[1];
+            }
+        }
+        if (!met) {
+#pragma unroll
+            for (int q = 0; q < NP; q++) T[q] = Lq[1][q];
+        }
+        return met;
+    };
+    // OR over the wave's lines (their first lanes) of a per-line 64-bit mask
+    auto lines_or = [&](uint64_t v) -> uint64_t {
+        uint64_t m = 0;
+#pragma unroll
+        for (int l = 0; l < LPW; l++) {
+            const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, l * VL);
+            const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), l * VL);
+            m |= ((uint64_t)hi << 32) | lo;
+        }
+        return m;
+    };
+    // the other lanes' partial / state stores land before this wave's later loads of the same
+    // cells (one wave: workgroup scope, i.e. vmcnt(0); agent scope would write back the L2)
+    auto order_partial = [&]() {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    };
+    // phase A's open strips (walk never met), one bit per path position i >= 1
+    __shared__ uint64_t openm[4][kPatchMaxChunks];
+    uint32_t nfix = 0, nopen = 0;  // walks (per line), open strips (wave-uniform)
     for (int dir = 0; dir < 2; dir++) {  // 0 = E (strips in x order), 1 = W (reverse)
         auto strip_of = [&](int i) { return dir ? nwg - 1 - i : i; };  // path position -> strip
-        for (int i0 = 1; i0 < nwg; i0 += CHUNK) {
+        int first_open = nwg;  // wave-uniform
+        for (int i0 = 1, ch = 0; i0 < nwg; i0 += CHUNK, ch++) {
             // ---- check: does the state entering strip i equal the end state stored by strip i - 1?
             RawBytes<CB> sb[KU], eb[KU];
 #pragma unroll
@@ -187,7 +291,7 @@ __global__ void __launch_bounds__(256) k_ew_patch(EwPatchArgs a)
                 sb[u].load(rs, i < nwg ? soff(strip_of(i), dir, 0) : kOOB);
                 eb[u].load(rs, i < nwg ? soff(strip_of(i - 1), dir, 1) : kOOB);
             }
-            uint64_t bad = 0;  // bit i - i0: strip i's speculative start differs (wave-uniform below)
+            uint64_t bad = 0;  // bit i - i0: strip i's speculative start differs
 #pragma unroll
             for (int u = 0; u < KU; u++) {
                 bool ok = true;
@@ -196,116 +300,73 @@ __global__ void __launch_bounds__(256) k_ew_patch(EwPatchArgs a)
                 ok = line_all(ok);
                 if (!ok && i0 + kl + LPW * u < nwg) bad |= 1ull << (kl + LPW * u);
             }
-            // OR over the wave's lines (their first lanes)
-            uint64_t m = 0;
+            const uint64_t m = lines_or(bad);  // wave-uniform
+            uint64_t open = 0;
+            // ---- phase A: the flagged strips in rounds of LPW, line kl takes the round's kl-th
+            uint64_t rest = m;
+            while (rest) {
+                int mine = -1;
 #pragma unroll
-            for (int l = 0; l < LPW; l++) {
-                const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)bad, l * VL);
-                const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(bad >> 32), l * VL);
-                m |= ((uint64_t)hi << 32) | lo;
-            }
-            if (m == 0) continue;  // every strip of the chunk started from the true state
-            // ---- repair walk (line 0) from the chunk's first failing strip to the path's end:
-            // the trusted state entering strip i is strip i - 1's stored end state while every
-            // earlier strip was exact (same), else the true state the walk carries
-            if (kl == 0) {
-                bool same = true;
-                uint32_t T[NP];
-#pragma unroll
-                for (int q = 0; q < NP; q++) T[q] = 0;
-                for (int i = i0 + __builtin_ctzll(m); i < nwg; i++) {
-                    const bool flagged = i - i0 < CHUNK ? ((m >> (i - i0)) & 1ull) != 0 : true;
-                    if (same && !flagged) continue;  // checked above against the trusted end state
-                    const int k = strip_of(i);
-                    RawBytes<CB> s1, e1;
-                    s1.load(rs, soff(k, dir, 0));
-                    e1.load(rs, soff(strip_of(i - 1), dir, 1));
-                    uint32_t S[NP], E[NP];
-                    unpack_ct_pk<CT, DPL>(s1, S);
-                    unpack_ct_pk<CT, DPL>(e1, E);
-                    if (same) {
-#pragma unroll
-                        for (int q = 0; q < NP; q++) T[q] = E[q];
-                    }
-                    if (same_state(S, T)) {  // the speculative segment started from the true state
-                        same = true;
-                        continue;
-                    }
-                    // recompute strip k from T beside its speculative trajectory
-                    uint32_t Lq[2][NP], mq[2];
-#pragma unroll
-                    for (int q = 0; q < NP; q++) {
-                        Lq[0][q] = S[q];
-                        Lq[1][q] = T[q];
-                    }
-                    mq[0] = state_min(Lq[0]);
-                    mq[1] = state_min(Lq[1]);
-                    const int x0 = k * CW, ncol = ::min(CW, W1 - x0);  // W: every repaired strip is full
-                    bool met = false;
-                    // columns in chunks of RC: the chunk's costs and partial slices load together
-                    for (int o0 = 0; o0 < ncol && !met; o0 += RC) {
-                        RawBytes<CB> cc[RC];
-                        RawBytes<DPL * 2> pb[RC];
-#pragma unroll
-                        for (int u = 0; u < RC; u++) {
-                            const int o = o0 + u;
-                            const int c = dir ? x0 + CW - 1 - o : x0 + o;
-                            cc[u].load(rc, o < ncol ? cell(c) * (uint32_t)sizeof(CT) : kOOB);
-                            pb[u].load(rp, o < ncol ? cell(c) * 2u : kOOB);
-                        }
-#pragma unroll
-                        for (int u = 0; u < RC; u++) {  // (no break: the loop must unroll)
-                            const int o = o0 + u;
-                            if (o >= ncol || met) continue;
-                            const int c = dir ? x0 + CW - 1 - o : x0 + o;
-                            uint32_t C2[2][NP], Ln[2][NP], mn[2];
-                            unpack_ct_pk<CT, DPL>(cc[u], C2[0]);
-#pragma unroll
-                            for (int q = 0; q < NP; q++) C2[1][q] = C2[0][q];
-                            sweep_step2n<VL, NP, H16, 2>(Lq, mq, C2, P1p, P2p, eL, eR, Ln, mn);
-                            if (same_state(Ln[0], Ln[1])) {
-                                met = true;
-                                continue;
-                            }
-                            uint32_t P[NP];
-#pragma unroll
-                            for (int q = 0; q < NP; q++) {
-                                if constexpr (SAT) {
-                                    uint32_t h[2];
-#pragma unroll
-                                    for (int e = 0; e < 2; e++) {
-                                        const uint32_t pv = (pb[u].w[q] >> (16 * e)) & 0xFFFFu;
-                                        const uint32_t sv = (Ln[0][q] >> (16 * e)) & 0xFFFFu;
-                                        const uint32_t tv = (Ln[1][q] >> (16 * e)) & 0xFFFFu;
-                                        h[e] = pv == 0xFFFFu ? pv : ::min(pv - sv + tv, 0xFFFFu);
-                                    }
-                                    P[q] = h[0] | (h[1] << 16);
-                                } else {  // census: every sum < 2^11, the u16 wrap is exact
-                                    P[q] = pk_add(pk_sub(pb[u].w[q], Ln[0][q]), Ln[1][q]);
-                                }
-                            }
-                            bstore_n<uint32_t, NP>(rp, cell(c) * 2u, P);
-#pragma unroll
-                            for (int q = 0; q < NP; q++) {
-                                Lq[0][q] = Ln[0][q];
-                                Lq[1][q] = Ln[1][q];
-                            }
-                            mq[0] = mn[0];
-                            mq[1] = mn[1];
-                        }
-                    }
+                for (int l = 0; l < LPW; l++) {
+                    if (rest && l == kl) mine = __builtin_ctzll(rest);
+                    if (rest) rest &= rest - 1;
+                }
+                if (mine >= 0) {
+                    const int i = i0 + mine, k = strip_of(i);
+                    uint32_t S[NP], T[NP];
+                    load_state(soff(k, dir, 0), S);
+                    load_state(soff(strip_of(i - 1), dir, 1), T);
                     nfix++;
-                    same = met;
-                    if (!met) {  // the true end state of strip k enters strip k + 1
-#pragma unroll
-                        for (int q = 0; q < NP; q++) T[q] = Lq[1][q];
+                    if (!walk(k, dir, S, T)) {
+                        // c_k, the true trajectory's far-end state, replaces s_k (read only above)
+                        store_pk<CT, NP>(rs, soff(k, dir, 0), T);
+                        open |= 1ull << mine;
                     }
                 }
             }
-            break;  // the walk covered the rest of this direction
+            open = lines_or(open);
+            nopen += (uint32_t)__builtin_popcountll(open);
+            if (lane == 0) openm[wave][ch] = open;
+            if (open && first_open == nwg) first_open = i0 + __builtin_ctzll(open);
         }
+        if (first_open < nwg) {
+            // ---- phase B (line 0, path order from the first open strip): `carry` = the true
+            // state entering strip i is T while strip i's values came from e_{i-1}
+            order_partial();  // the other lanes' partial and c_k stores
+            if (kl == 0) {
+                bool carry = false;
+                uint32_t T[NP];
+#pragma unroll
+                for (int q = 0; q < NP; q++) T[q] = 0;
+                for (int i = first_open; i < nwg; i++) {
+                    const int k = strip_of(i);
+                    if (carry) {
+                        uint32_t Ep[NP];
+                        load_state(soff(strip_of(i - 1), dir, 1), Ep);
+                        if (same_state(T, Ep)) {
+                            carry = false;
+                        } else {
+                            nfix++;
+                            if (walk(k, dir, Ep, T)) carry = false;
+                        }
+                    }
+                    // an open strip's values (from e_{i-1}, or corrected to the true trajectory
+                    // where that met them) end at c_k: the next strip needs c_k, not e_k
+                    const bool open_i = ((openm[wave][(i - 1) / CHUNK] >> ((i - 1) % CHUNK)) & 1ull) != 0;
+                    if (!carry && open_i) {
+                        load_state(soff(k, dir, 0), T);
+                        carry = true;
+                    }
+                }
+            }
+        }
+        if (dir == 0) order_partial();  // W touches the cells E wrote
     }
-    if (a.fixes && lane == 0 && nfix) atomicAdd(a.fixes, nfix);
+    if (a.fixes) {
+        nfix = group_sum_u32_wave(g == 0 ? nfix : 0u);  // every line's walks
+        if (lane == 0 && nfix) atomicAdd(a.fixes, nfix);
+        if (lane == 0 && nopen) atomicAdd(a.fixes + 1, nopen);  // (the next counter word)
+    }
 }
 
 }  // namespace smk

@@ -531,66 +531,6 @@ __device__ __forceinline__ void wta_row(const WtaArgs& a, const int y, const int
     const LT* __restrict__ Lb = (const LT*)(a.L + (size_t)pair * a.L_pair_bytes) + g * DPL;
     const size_t slot = a.slot_bytes / sizeof(LT);
     const int u = a.uniq;
-    // one column: WTA, uniqueness, sub-pixel, the right view's keys
-    auto decide = [&](const int x, uint32_t (&S)[DPL]) {
-        uint32_t key = 0xFFFFFFFFu;
-#pragma unroll
-        for (int i = 0; i < DPL; i++) {
-            S[i] = min(S[i], 32767u);
-            if (g * DPL + i >= a.Dv) S[i] = 0xFFFFu;  // pad planes of a cost volume: never the minimum
-            key = min(key, (S[i] << 16) | wta_rank(g * DPL + i, a.lane8));
-        }
-        key = row16_min(key);
-        const int minS = (int)(key >> 16), best = wta_unrank(key & 0xFFFF, a.lane8);
-        uint32_t bad = 0, nb = 0;
-#pragma unroll
-        for (int i = 0; i < DPL; i++) {
-            const int d = g * DPL + i;
-            const int dd = best - d;
-            bad |= ((int)S[i] * (100 - u) < minS * 100 && (dd > 1 || dd < -1) && d < a.Dv) ? 1u : 0u;
-            nb |= d == best - 1 ? S[i] : 0u;
-            nb |= d == best + 1 ? (S[i] << 16) : 0u;
-        }
-        bad = row16_or(bad);
-        nb = row16_or(nb);
-        if (g == 0 && !bad && minS < 32767) {
-            const int X = x + minX1;
-            const int x2 = X - best - minD;
-            atomicMin(&key2[x2], ((uint32_t)minS << 16) | (uint32_t)(0xFFFF - X));
-            int d16;
-            if (best > 0 && best < a.Dv - 1) {
-                const int Sm = (int)(nb & 0xFFFF), Sq = (int)(nb >> 16);
-                const int den = max(Sm + Sq - 2 * minS, 1);
-                d16 = best * 16 + ((Sm - Sq) * 16 + den) / (den * 2);  // C truncation
-            } else {
-                d16 = best * 16;
-            }
-            drow[X] = d16 + minD * 16;
-            if (a.wta) brow[X] = (int16_t)best;
-        }
-    };
-    if (a.nslots == 0 && a.part) {
-        // the patched MODE 3 partial only (5 paths): PD columns' loads in flight per lane group
-        // (one round trip per column otherwise: the row's 18 iterations ran latency-bound)
-        constexpr int PD = 4, STEP = NT / 16;
-        const uint16_t* P = a.part + (size_t)pair * a.part_pair + (size_t)y * a.width1 * D + g * DPL;
-        const int xl = a.width1 - 1;
-        uint32_t t[PD][DPL];
-#pragma unroll
-        for (int k = 0; k < PD; k++) load_n<DPL>(P + (size_t)min(grp + k * STEP, xl) * D, t[k]);
-        for (int x0 = grp; x0 < a.width1; x0 += PD * STEP) {
-#pragma unroll
-            for (int k = 0; k < PD; k++) {
-                const int x = x0 + k * STEP;
-                uint32_t S[DPL];
-#pragma unroll
-                for (int i = 0; i < DPL; i++) S[i] = t[k][i];
-                // unconditional (clamped) refill: a load under a branch is waited for at its end
-                load_n<DPL>(P + (size_t)min(x + PD * STEP, xl) * D, t[k]);
-                if (x < a.width1) decide(x, S);
-            }
-        }
-    } else {
     for (int x = grp; x < a.width1; x += NT / 16) {
         const size_t off = ((size_t)y * a.width1 + x) * D;
         uint32_t S[DPL];
@@ -645,14 +585,47 @@ __device__ __forceinline__ void wta_row(const WtaArgs& a, const int y, const int
                 for (int i = 0; i < DPL; i++) S[i] += t[i];
             }
         }
-        if (a.part) {  // wave-uniform (with slots: the hybrid engine)
+        if (a.part) {  // wave-uniform
             uint32_t t[DPL];
             load_n<DPL>(a.part + (size_t)pair * a.part_pair + off + g * DPL, t);
 #pragma unroll
             for (int i = 0; i < DPL; i++) S[i] += t[i];
         }
-        decide(x, S);
-    }
+        uint32_t key = 0xFFFFFFFFu;
+#pragma unroll
+        for (int i = 0; i < DPL; i++) {
+            S[i] = min(S[i], 32767u);
+            if (g * DPL + i >= a.Dv) S[i] = 0xFFFFu;  // pad planes of a cost volume: never the minimum
+            key = min(key, (S[i] << 16) | wta_rank(g * DPL + i, a.lane8));
+        }
+        key = row16_min(key);
+        const int minS = (int)(key >> 16), best = wta_unrank(key & 0xFFFF, a.lane8);
+        uint32_t bad = 0, nb = 0;
+#pragma unroll
+        for (int i = 0; i < DPL; i++) {
+            const int d = g * DPL + i;
+            const int dd = best - d;
+            bad |= ((int)S[i] * (100 - u) < minS * 100 && (dd > 1 || dd < -1) && d < a.Dv) ? 1u : 0u;
+            nb |= d == best - 1 ? S[i] : 0u;
+            nb |= d == best + 1 ? (S[i] << 16) : 0u;
+        }
+        bad = row16_or(bad);
+        nb = row16_or(nb);
+        if (g == 0 && !bad && minS < 32767) {
+            const int X = x + minX1;
+            const int x2 = X - best - minD;
+            atomicMin(&key2[x2], ((uint32_t)minS << 16) | (uint32_t)(0xFFFF - X));
+            int d16;
+            if (best > 0 && best < a.Dv - 1) {
+                const int Sm = (int)(nb & 0xFFFF), Sq = (int)(nb >> 16);
+                const int den = max(Sm + Sq - 2 * minS, 1);
+                d16 = best * 16 + ((Sm - Sq) * 16 + den) / (den * 2);  // C truncation
+            } else {
+                d16 = best * 16;
+            }
+            drow[X] = d16 + minD * 16;
+            if (a.wta) brow[X] = (int16_t)best;
+        }
     }
     __syncthreads();
     int16_t* out = a.disp + (size_t)pair * a.H * W + (size_t)y * W;

@@ -219,6 +219,11 @@ constexpr int largest_divisor_upto(int n, int cap)
 #ifndef SWEEP_LINE_NOBAR
 #define SWEEP_LINE_NOBAR 1
 #endif
+// the same counter hand-off in the sweeps without line waves (bit MODE; row-synchronised modes
+// only): the strip's waves away from the halos may start a block while the halo waves wait
+#ifndef SWEEP_NOBAR_MODES
+#define SWEEP_NOBAR_MODES 0
+#endif
 constexpr int kMaxLds = 163840;  // gfx950: LDS one workgroup may declare
 template <int VL, int DPL, int NCW_, int MODE>
 struct LineGeo {
@@ -421,7 +426,6 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
     constexpr bool EWIN = MODE == 1 || MODE == 2;   // E / W path volumes read (k_ew)
     constexpr bool PARTR = MODE == 2 || MODE == 4;  // the down sweep's partial read
     constexpr bool LINES = MODE == 3;               // E / W lines in the kernel (line waves)
-    constexpr bool NOBAR = LINES && SWEEP_LINE_NOBAR;  // block hand-off by LDS counters
     static_assert(!LINES || LG::BUILT, "MODE 3 instance not built for this geometry");
     static_assert(MODE < 3 || (DPL % 2 == 0 && !SWEEP_U32), "MODES 3 / 4 run the packed row loops only");
     constexpr int NTH = sweep_threads<VL, DPL, NCW_, MODE>();
@@ -446,6 +450,9 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
 #define SWEEP_ROWSYNC_M1 0
 #endif
     constexpr bool ROWSYNC = SWEEP_ROW_SYNC && (MODE != 1 || SWEEP_ROWSYNC_M1);
+    // block hand-off by LDS counters instead of the two workgroup barriers per block
+    constexpr bool NOBAR = ROWSYNC && DPL % 2 == 0 && !SWEEP_U32 &&  // (the packed row loops)
+                           (LINES ? SWEEP_LINE_NOBAR != 0 : ((SWEEP_NOBAR_MODES >> MODE) & 1) != 0);
     static_assert(!LINES || ROWSYNC, "the line waves mirror the row-synchronised barrier pattern");
     constexpr int LPW = G::LPW, NCW = G::NCW, HB = G::HB, NCOL = G::NCOL, COLS = G::COLS, CW = G::CW, D = G::D;
     constexpr int NG = G::NG, SNG = G::SNG, PF = G::PF, HM = G::HM, HW = G::HW;

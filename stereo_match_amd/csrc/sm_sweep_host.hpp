@@ -162,8 +162,12 @@ struct EwPatchArgs {
     size_t st_pair;       // bytes
     int H, W1, nwg, cw, P1, P2;
     const uint32_t* guard;  // the group's give-up flag: nothing to patch when set (the fallback recomputes)
-    uint32_t* fixes;        // strip segments recomputed (device counter, atomic)
+    uint32_t* fixes;        // [0] strip segments recomputed, [1] of them never met within the strip (atomic)
 };
+// chunks of LPW * 8 path positions per row and direction the patch pass handles (its open-strip
+// masks in LDS): strips of a pair it accepts (16-lane lines where D % 32 == 0, else 8-lane)
+constexpr int kPatchMaxChunks = 8;
+constexpr int patch_max_strips(int D) { return 1 + kPatchMaxChunks * (D % 32 == 0 ? 4 : 8) * 8; }
 hipError_t ew_patch_launch(int D, int ct_bytes, const EwPatchArgs& a, int npairs, hipStream_t stream);
 
 }  // namespace smk

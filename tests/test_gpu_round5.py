@@ -120,6 +120,25 @@ def test_lines_adversarial(eng, name, make, cost, mode, D, P1, P2, guess):
     _check(out, left, right, p)
 
 
+@pytest.mark.parametrize("name", ["const", "wide_bands"])
+def test_lines_open_strips_carry_the_true_state(eng, name):
+    """Flat images and flat bands wider than a strip with a wrong start guess: the repaired
+    values of a segment never meet the speculative ones inside its strip (SM_COUNTER_EW_OPEN),
+    so the patch pass carries the true state into the next strips (its phase B) — over a full
+    KITTI row of strips, both cost types."""
+    make = dict(ADV)[name]
+    H, W, D = 12, synthetic.CONFIGS["kitti"][1], 64
+    left, right = make(H, W)
+    for cost, mode in ((1, 8), (0, 5)):
+        p = dict(_params(cost, D, mode), P1=10, P2=120)
+        c0 = eng.counters()
+        out = _run(eng, left, right, p, ew_guess=1)
+        _check(out, left, right, p)
+        c1 = eng.counters()
+        assert c1["ew_open"] > c0["ew_open"], (name, cost, c1)
+        assert c1["ew_repairs"] - c0["ew_repairs"] >= c1["ew_open"] - c0["ew_open"]
+
+
 def test_lines_match_classic_engine_kitti_batch(eng):
     """8 KITTI census pairs through one launch group: the in-sweep lines and the E/W volume
     kernel (SM_TUNE_SWEEP_LINES -1) give identical maps, and both equal the oracle."""
@@ -176,7 +195,7 @@ def test_lines_tuning_arguments(eng):
     with pytest.raises(ValueError):
         eng.set_tuning(eng.TUNE_EW_GUESS, 2)
     c = eng.counters()
-    assert set(c) == {"sweep_fallbacks", "ew_repairs", "volume_clamped", "volume_nan", "line_groups"}
+    assert set(c) == {"sweep_fallbacks", "ew_repairs", "volume_clamped", "volume_nan", "line_groups", "ew_open"}
 
 
 # ------------------------------------------------------------------ mc-cnn quantisation window
