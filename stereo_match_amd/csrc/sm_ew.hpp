@@ -191,6 +191,21 @@ __global__ void __launch_bounds__(256) k_ew_patch(EwPatchArgs a)
     // one enters at T: add (true - applied) to the partial until the two meet.  Returns met;
     // otherwise T holds the true trajectory's state at the strip's far end.  Line-divergent.
     auto walk = [&](int k, int dir, const uint32_t (&A)[NP], uint32_t (&T)[NP]) -> bool {
+        const int x0 = k * CW, ncol = ::min(CW, W1 - x0);  // W: every repaired strip is full
+        // columns in chunks of RC: the chunk's costs and partial slices load together (the
+        // first chunk's beside the caller's state loads)
+        RawBytes<CB> cc[RC];
+        RawBytes<DPL * 2> pb[RC];
+        auto issue = [&](int o0) {
+#pragma unroll
+            for (int u = 0; u < RC; u++) {
+                const int o = o0 + u;
+                const int c = dir ? x0 + CW - 1 - o : x0 + o;
+                cc[u].load(rc, o < ncol ? cell(c) * (uint32_t)sizeof(CT) : kOOB);
+                pb[u].load(rp, o < ncol ? cell(c) * 2u : kOOB);
+            }
+        };
+        issue(0);
         uint32_t Lq[2][NP], mq[2];
 #pragma unroll
         for (int q = 0; q < NP; q++) {
@@ -199,19 +214,9 @@ __global__ void __launch_bounds__(256) k_ew_patch(EwPatchArgs a)
         }
         mq[0] = state_min(Lq[0]);
         mq[1] = state_min(Lq[1]);
-        const int x0 = k * CW, ncol = ::min(CW, W1 - x0);  // W: every repaired strip is full
         bool met = false;
-        // columns in chunks of RC: the chunk's costs and partial slices load together
         for (int o0 = 0; o0 < ncol && !met; o0 += RC) {
-            RawBytes<CB> cc[RC];
-            RawBytes<DPL * 2> pb[RC];
-#pragma unroll
-            for (int u = 0; u < RC; u++) {
-                const int o = o0 + u;
-                const int c = dir ? x0 + CW - 1 - o : x0 + o;
-                cc[u].load(rc, o < ncol ? cell(c) * (uint32_t)sizeof(CT) : kOOB);
-                pb[u].load(rp, o < ncol ? cell(c) * 2u : kOOB);
-            }
+            if (o0 > 0) issue(o0);
 #pragma unroll
             for (int u = 0; u < RC; u++) {  // (no break: the loop must unroll)
                 const int o = o0 + u;
@@ -230,15 +235,12 @@ __global__ void __launch_bounds__(256) k_ew_patch(EwPatchArgs a)
 #pragma unroll
                 for (int q = 0; q < NP; q++) {
                     if constexpr (SAT) {
-                        uint32_t h[2];
-#pragma unroll
-                        for (int e = 0; e < 2; e++) {
-                            const uint32_t pv = (pb[u].w[q] >> (16 * e)) & 0xFFFFu;
-                            const uint32_t sv = (Ln[0][q] >> (16 * e)) & 0xFFFFu;
-                            const uint32_t tv = (Ln[1][q] >> (16 * e)) & 0xFFFFu;
-                            h[e] = pv == 0xFFFFu ? pv : ::min(pv - sv + tv, 0xFFFFu);
-                        }
-                        P[q] = h[0] | (h[1] << 16);
+                        // a half pv < 0xFFFF is the exact sum, pv >= sv: (pv - sv) + tv saturating;
+                        // pv == 0xFFFF stays (sat: 0xFFFF exactly there, from pv + 1 wrapping to 0)
+                        const uint32_t pv = pb[u].w[q];
+                        const uint32_t x = pk_adds(pk_sub(pv, Ln[0][q]), Ln[1][q]);
+                        const uint32_t sat = pk_sub(pk_min(pk_add(pv, 0x00010001u), 0x00010001u), 0x00010001u);
+                        P[q] = pkw(__builtin_elementwise_max(pkv(x), pkv(sat)));
                     } else {  // census: every sum < 2^11, the u16 wrap is exact
                         P[q] = pk_add(pk_sub(pb[u].w[q], Ln[0][q]), Ln[1][q]);
                     }
