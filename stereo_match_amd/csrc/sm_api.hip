@@ -833,6 +833,9 @@ bool sweeps_fit(sm_ctx* ctx, const Norm& n, bool hybrid, bool lines = false)
         SweepFit f;
         if (!sweep_capacity(ctx, n, modes[k], 0, f)) return false;
         if (lines && modes[k] == 3 && f.nwg > smk::patch_max_strips(n.D)) return false;  // the patch pass's masks
+        // lines in narrow strips (no wide MODE 3 instance: D = 256 u8) pay the warmup on 20
+        // columns and lost to the E/W volumes (Middlebury D = 256, 4 pairs: 167 vs 225 pairs/s)
+        if (lines && modes[k] == 3 && f.si.ncw < 11) return false;
     }
     return true;
 }

@@ -24,6 +24,7 @@
 //  * outputs: one LT volume per direction [slot][H][width1][D] (d fastest).
 #pragma once
 #include "sm_common.hpp"
+#include "sm_pk.hpp"
 
 namespace smk {
 
@@ -511,6 +512,97 @@ struct WtaArgs {
     int npairs;
 };
 
+// The row's columns of a u16 partial that holds every path's sum (the MODE 3 lines' patched
+// partial, 5 paths), packed: two disparities per VOP3P instruction for the clamp, the WTA key
+// and the uniqueness window (the fused sweep's form, sm_sweep.hpp), S[best -+ 1] from a row of
+// S in LDS.  Same decisions as wta_row's scalar loop (sgbm5 KITTI: 26 VALU lane-ops per cell
+// there, the kernel at full VALU issue).
+template <int DPL, int NT>
+__device__ __forceinline__ void wta_part_cols(const WtaArgs& a, const int y, const int pair, uint32_t* key2, int* drow,
+                                              int16_t* brow)
+{
+    constexpr int NP = DPL / 2;
+    __shared__ __attribute__((aligned(16))) uint16_t srow[NT / 16][16 * DPL];
+    const int D = a.D, minD = a.minD, minX1 = a.minX1, Dv = a.Dv;
+    const int g = threadIdx.x & 15, grp = threadIdx.x >> 4;
+    const bool pad = Dv < D;
+    const int ku = 100 - a.uniq;
+    uint32_t rk[DPL], padm[NP], dpk[NP];
+#pragma unroll
+    for (int i = 0; i < DPL; i++) rk[i] = wta_rank(g * DPL + i, a.lane8);
+#pragma unroll
+    for (int j = 0; j < NP; j++) {
+        const int d0 = g * DPL + 2 * j;
+        padm[j] = (d0 >= Dv ? 0x0000FFFFu : 0u) | (d0 + 1 >= Dv ? 0xFFFF0000u : 0u);
+        dpk[j] = (uint32_t)(d0 + 1) * 0x10001u + 0x10000u;  // d + 1 per half
+    }
+    const uint16_t* P = a.part + (size_t)pair * a.part_pair + (size_t)y * a.width1 * D + g * DPL;
+    uint16_t* sr = &srow[grp][0];
+    for (int x = grp; x < a.width1; x += NT / 16) {
+        uint32_t Sp[NP];
+        const uint16_t* src = P + (size_t)x * D;
+        if constexpr (NP % 4 == 0) {
+#pragma unroll
+            for (int k = 0; k < NP / 4; k++) {
+                const uint4 q = reinterpret_cast<const uint4*>(src)[k];
+                Sp[4 * k] = q.x; Sp[4 * k + 1] = q.y; Sp[4 * k + 2] = q.z; Sp[4 * k + 3] = q.w;
+            }
+        } else if constexpr (NP % 2 == 0) {
+#pragma unroll
+            for (int k = 0; k < NP / 2; k++) {
+                const uint2 q = reinterpret_cast<const uint2*>(src)[k];
+                Sp[2 * k] = q.x; Sp[2 * k + 1] = q.y;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < NP; k++) Sp[k] = reinterpret_cast<const uint32_t*>(src)[k];
+        }
+        uint32_t key = 0xFFFFFFFFu;
+#pragma unroll
+        for (int j = 0; j < NP; j++) {
+            Sp[j] = pk_min(Sp[j], 0x7FFF7FFFu);  // min(S, 32767)
+            if (pad) Sp[j] |= padm[j];           // pad planes of a cost volume: never the minimum
+            key = ::min(key, ::min((Sp[j] << 16) | rk[2 * j], (Sp[j] & 0xFFFF0000u) | rk[2 * j + 1]));
+        }
+        // (u32 stores, u16 loads of the same LDS row: the compiler barriers keep type-based
+        // alias analysis from moving the loads across the stores, here and in the next column)
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int j = 0; j < NP; j++) reinterpret_cast<uint32_t*>(sr + g * DPL)[j] = Sp[j];
+        asm volatile("" ::: "memory");
+        key = row16_min(key);
+        const uint32_t minS = key >> 16;
+        const int best = wta_unrank(key & 0xFFFF, a.lane8);
+        // uniqueness: m2 = min S outside best-1..best+1 (window entries pushed to >= 0xFFFD)
+        const uint32_t bm1p = (uint32_t)best * 0x10001u;
+        uint32_t m2p = 0xFFFFFFFFu;
+#pragma unroll
+        for (int j = 0; j < NP; j++) {
+            uint32_t t = pk_sub(dpk[j], bm1p);  // d + 1 - best: 0, 1, 2 inside the window
+            t = pkw(__builtin_elementwise_sub_sat(pkv(0x00030003u), pkv(t)));
+            t = pkw(pkv(t) * pkv(0xFFFFFFFFu));
+            m2p = pk_min(m2p, pk_adds(Sp[j], t));
+        }
+        const uint32_t m2 = row16_min(::min(m2p & 0xFFFFu, m2p >> 16));
+        const bool bad = (int)m2 * ku < (int)minS * 100 && (!pad || m2 <= 32767u);
+        if (g == 0 && !bad && minS < 32767u) {
+            const int X = x + minX1;
+            const int x2 = X - best - minD;
+            atomicMin(&key2[x2], (minS << 16) | (uint32_t)(0xFFFF - X));
+            int d16;
+            if (best > 0 && best < Dv - 1) {
+                const int Sm = sr[best - 1], Sq = sr[best + 1];
+                const int den = max(Sm + Sq - 2 * (int)minS, 1);
+                d16 = best * 16 + ((Sm - Sq) * 16 + den) / (den * 2);  // C truncation
+            } else {
+                d16 = best * 16;
+            }
+            drow[X] = d16 + minD * 16;
+            if (a.wta) brow[X] = (int16_t)best;
+        }
+    }
+}
+
 template <int DPL, typename LT, int NT>
 __device__ __forceinline__ void wta_row(const WtaArgs& a, const int y, const int pair, uint32_t* smem)
 {
@@ -531,6 +623,12 @@ __device__ __forceinline__ void wta_row(const WtaArgs& a, const int y, const int
     const LT* __restrict__ Lb = (const LT*)(a.L + (size_t)pair * a.L_pair_bytes) + g * DPL;
     const size_t slot = a.slot_bytes / sizeof(LT);
     const int u = a.uniq;
+    if constexpr (DPL % 2 == 0) {
+        if (a.nslots == 0 && a.part) {  // (block-uniform) the in-sweep lines' patched partial
+            wta_part_cols<DPL, NT>(a, y, pair, key2, drow, brow);
+            goto tail;
+        }
+    }
     for (int x = grp; x < a.width1; x += NT / 16) {
         const size_t off = ((size_t)y * a.width1 + x) * D;
         uint32_t S[DPL];
@@ -627,6 +725,7 @@ __device__ __forceinline__ void wta_row(const WtaArgs& a, const int y, const int
             if (a.wta) brow[X] = (int16_t)best;
         }
     }
+tail:
     __syncthreads();
     int16_t* out = a.disp + (size_t)pair * a.H * W + (size_t)y * W;
     for (int X = threadIdx.x; X < W; X += NT) {

@@ -243,8 +243,12 @@ struct LineGeo {
                                   (SWEEP_LINE_NOBAR ? RPW <= FIT : LEAD + RPW <= FIT) &&
                                   G::CW % 2 == 0 && G::HB % RPW == 0 && RPW >= 1;
     // ring chunk of the line loop, per cost type (a divisor of CW / 2)
+    // (8-lane lines: 9, the D = 64 u8 / D = 48 u16 wide instances spilled at 12)
     template <typename CT>
-    static constexpr int lpf() { return largest_divisor_upto(G::CW / 2, sizeof(CT) == 1 ? SWEEP_LPF8 : SWEEP_LPF16); }
+    static constexpr int lpf()
+    {
+        return largest_divisor_upto(G::CW / 2, VL == 8 ? 9 : sizeof(CT) == 1 ? SWEEP_LPF8 : SWEEP_LPF16);
+    }
 };
 template <int VL, int DPL, int NCW_, int MODE>
 constexpr int sweep_threads() { return SweepGeo<VL, DPL, NCW_>::THREADS + 64 * LineGeo<VL, DPL, NCW_, MODE>::NLW; }
@@ -1253,7 +1257,9 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
                             for (int i = 0; i < NP; i++)
                                 key = min(key, min((Sp[i] << 16) | wta_rank(g * DPL + 2 * i, MODE == 1),
                                                    (Sp[i] & 0xFFFF0000u) | wta_rank(g * DPL + 2 * i + 1, MODE == 1)));
+                            asm volatile("" ::: "memory");  // u32 / u128 stores, u16 loads of srow: no reordering
                             lds_put_pk<NP>(&srow[(wave - 1) % (NCW - 2)][kl][g * DPL], Sp);
+                            asm volatile("" ::: "memory");
                             key = group_min<VL>(key);
                             const uint32_t minS = key >> 16;
                             const int best = wta_unrank(key & 0xFFFF, MODE == 1);  // MODE 1 = 5 paths
@@ -1421,7 +1427,9 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
                         S[i] = t;
                         key = min(key, (t << 16) | wta_rank(g * DPL + i, MODE == 1));
                     }
+                    asm volatile("" ::: "memory");  // u32 / u128 stores, u16 loads of srow: no reordering
                     lds_put<DPL>(&srow[(wave - 1) % (NCW - 2)][kl][g * DPL], S);
+                    asm volatile("" ::: "memory");
                     key = group_min<VL>(key);
                     const uint32_t minS = key >> 16;
                     const int best = wta_unrank(key & 0xFFFF, MODE == 1);  // MODE 1 = 5 paths
