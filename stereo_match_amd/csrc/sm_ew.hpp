@@ -115,6 +115,12 @@ __global__ void __launch_bounds__(256) k_ew(EwArgs a)
     }
 }
 
+// columns of a repaired segment whose cost and partial slices load together (one memory round
+// trip per RC columns on the walks' serial chain; the pass runs ~3 waves per SIMD, so the
+// registers are there)
+#ifndef EW_PATCH_RC
+#define EW_PATCH_RC 16
+#endif
 // ---------------------------------------------------------------------------
 // Patch pass after a MODE 3 sweep (sm_sweep.hpp line waves).  Strip k's E line
 // started from the zero state `ewarm` columns before the strip, so its values are exact from
@@ -148,7 +154,7 @@ __global__ void __launch_bounds__(256) k_ew_patch(EwPatchArgs a)
     // chunk of LPW * KU path positions, all loads of a chunk in flight together
     constexpr int KU = 8;
     constexpr int CHUNK = LPW * KU;
-    constexpr int RC = 8;  // columns of a repaired segment loaded together
+    constexpr int RC = EW_PATCH_RC;  // columns of a repaired segment loaded together
     if (a.guard && __hip_atomic_load(a.guard, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int g = lane % VL, kl = lane / VL;
