@@ -611,6 +611,9 @@ int launch_wta_t(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs)
     }
     if (ctx->fb_guard)
         hipLaunchKernelGGL((smk::k_wta<DPLV, LT, 1024, true>), grid, dim3(1024), smem, stream_b(ctx), wa);
+    else if (wa.nslots == 0 && wa.part)
+        hipLaunchKernelGGL((smk::k_wta<DPLV, LT, WTA_NT, false, DPLV % 2 == 0>), grid, dim3(WTA_NT), smem, stream_b(ctx),
+                           wa);
     else
         hipLaunchKernelGGL((smk::k_wta<DPLV, LT, WTA_NT>), grid, dim3(WTA_NT), smem, stream_b(ctx), wa);
     HIP_TRY(ctx, hipGetLastError());

@@ -512,13 +512,13 @@ struct WtaArgs {
     int npairs;
 };
 
-// The row's columns of a u16 partial that holds every path's sum (the MODE 3 lines' patched
-// partial, 5 paths), packed: two disparities per VOP3P instruction for the clamp, the WTA key
+// The row's columns from u16 sums (the MODE 3 lines' patched partial with every path, or the
+// per-direction engine's u16 volumes + partial), packed: two disparities per VOP3P instruction for the clamp, the WTA key
 // and the uniqueness window (the fused sweep's form, sm_sweep.hpp), S[best -+ 1] from a row of
 // S in LDS.  Same decisions as wta_row's scalar loop (sgbm5 KITTI: 26 VALU lane-ops per cell
 // there, the kernel at full VALU issue).
-template <int DPL, int NT>
-__device__ __forceinline__ void wta_part_cols(const WtaArgs& a, const int y, const int pair, uint32_t* key2, int* drow,
+template <int DPL, typename LT, int NT, bool PART_ONLY>
+__device__ __forceinline__ void wta_packed_cols(const WtaArgs& a, const int y, const int pair, uint32_t* key2, int* drow,
                                               int16_t* brow)
 {
     constexpr int NP = DPL / 2;
@@ -536,26 +536,52 @@ __device__ __forceinline__ void wta_part_cols(const WtaArgs& a, const int y, con
         padm[j] = (d0 >= Dv ? 0x0000FFFFu : 0u) | (d0 + 1 >= Dv ? 0xFFFF0000u : 0u);
         dpk[j] = (uint32_t)(d0 + 1) * 0x10001u + 0x10000u;  // d + 1 per half
     }
-    const uint16_t* P = a.part + (size_t)pair * a.part_pair + (size_t)y * a.width1 * D + g * DPL;
+    // S = the u16 partial (MODE 3 lines: every path) and / or the u16 per-direction volumes
+    // (k < nslots), summed saturating: min(sum, 65535) clamped at 32767 below = min(sum, 32767)
+    const size_t rowo = (size_t)y * a.width1 * D + g * DPL;
+    const uint16_t* P = a.part ? a.part + (size_t)pair * a.part_pair + rowo : nullptr;
+    const uint16_t* Lb = sizeof(LT) == 2 ? (const uint16_t*)(a.L + (size_t)pair * a.L_pair_bytes) + rowo : nullptr;
+    const size_t slot = a.slot_bytes / 2;
+    const int nslots = sizeof(LT) == 2 && !PART_ONLY ? a.nslots : 0;
+    constexpr int MS = PART_ONLY ? 1 : 4;  // slots in flight (the partial-only kernel keeps none)
     uint16_t* sr = &srow[grp][0];
-    for (int x = grp; x < a.width1; x += NT / 16) {
-        uint32_t Sp[NP];
-        const uint16_t* src = P + (size_t)x * D;
+    auto ldw = [&](const uint16_t* src, uint32_t (&w)[NP]) {
         if constexpr (NP % 4 == 0) {
 #pragma unroll
             for (int k = 0; k < NP / 4; k++) {
                 const uint4 q = reinterpret_cast<const uint4*>(src)[k];
-                Sp[4 * k] = q.x; Sp[4 * k + 1] = q.y; Sp[4 * k + 2] = q.z; Sp[4 * k + 3] = q.w;
+                w[4 * k] = q.x; w[4 * k + 1] = q.y; w[4 * k + 2] = q.z; w[4 * k + 3] = q.w;
             }
         } else if constexpr (NP % 2 == 0) {
 #pragma unroll
             for (int k = 0; k < NP / 2; k++) {
                 const uint2 q = reinterpret_cast<const uint2*>(src)[k];
-                Sp[2 * k] = q.x; Sp[2 * k + 1] = q.y;
+                w[2 * k] = q.x; w[2 * k + 1] = q.y;
             }
         } else {
 #pragma unroll
-            for (int k = 0; k < NP; k++) Sp[k] = reinterpret_cast<const uint32_t*>(src)[k];
+            for (int k = 0; k < NP; k++) w[k] = reinterpret_cast<const uint32_t*>(src)[k];
+        }
+    };
+    for (int x = grp; x < a.width1; x += NT / 16) {
+        uint32_t Sp[NP], t[MS][NP], tp[NP];
+        if (P) ldw(P + (size_t)x * D, tp);
+#pragma unroll
+        for (int j = 0; j < NP; j++) Sp[j] = 0u;
+        for (int k0 = 0; k0 < nslots; k0 += MS) {  // MS slots' loads in flight before their adds
+#pragma unroll
+            for (int k = 0; k < MS; k++)
+                if (k0 + k < nslots) ldw(Lb + (size_t)(k0 + k) * slot + (size_t)x * D, t[k]);
+#pragma unroll
+            for (int k = 0; k < MS; k++)
+                if (k0 + k < nslots) {
+#pragma unroll
+                    for (int j = 0; j < NP; j++) Sp[j] = pk_adds(Sp[j], t[k][j]);
+                }
+        }
+        if (P) {
+#pragma unroll
+            for (int j = 0; j < NP; j++) Sp[j] = pk_adds(Sp[j], tp[j]);
         }
         uint32_t key = 0xFFFFFFFFu;
 #pragma unroll
@@ -603,7 +629,7 @@ __device__ __forceinline__ void wta_part_cols(const WtaArgs& a, const int y, con
     }
 }
 
-template <int DPL, typename LT, int NT>
+template <int DPL, typename LT, int NT, bool PART_ONLY = false>
 __device__ __forceinline__ void wta_row(const WtaArgs& a, const int y, const int pair, uint32_t* smem)
 {
     const int W = a.W, D = a.D, minD = a.minD, minX1 = a.minX1;
@@ -624,8 +650,12 @@ __device__ __forceinline__ void wta_row(const WtaArgs& a, const int y, const int
     const size_t slot = a.slot_bytes / sizeof(LT);
     const int u = a.uniq;
     if constexpr (DPL % 2 == 0) {
-        if (a.nslots == 0 && a.part) {  // (block-uniform) the in-sweep lines' patched partial
-            wta_part_cols<DPL, NT>(a, y, pair, key2, drow, brow);
+        // the in-sweep lines' patched partial (PART_ONLY), or u16 direction volumes (+ partial)
+        if constexpr (PART_ONLY) {
+            wta_packed_cols<DPL, LT, NT, true>(a, y, pair, key2, drow, brow);
+            goto tail;
+        } else if (sizeof(LT) == 2 && DPL <= 12) {  // (block-uniform; DPL 14, 16: the scalar loop's registers)
+            wta_packed_cols<DPL, LT, NT, false>(a, y, pair, key2, drow, brow);
             goto tail;
         }
     }
@@ -751,7 +781,9 @@ tail:
     }
 }
 
-template <int DPL, typename LT, int NT, bool FB = false>
+// PART_ONLY: a.nslots == 0 and a.part set (the MODE 3 lines' 5-path partial), its own
+// instance so the row loop keeps the registers of two workgroups per CU
+template <int DPL, typename LT, int NT, bool FB = false, bool PART_ONLY = false>
 __global__ void __launch_bounds__(NT) k_wta(WtaArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
@@ -759,11 +791,11 @@ __global__ void __launch_bounds__(NT) k_wta(WtaArgs a)
         if (guard_clear(a.guard)) return;
         if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(a.fallbacks, 1u);
         for (int v = blockIdx.x; v < a.H * a.npairs; v += gridDim.x) {
-            wta_row<DPL, LT, NT>(a, v % a.H, v / a.H, smem);
+            wta_row<DPL, LT, NT, PART_ONLY>(a, v % a.H, v / a.H, smem);
             __syncthreads();  // the next row reuses the shared row buffers
         }
     } else {
-        wta_row<DPL, LT, NT>(a, blockIdx.x, blockIdx.y, smem);
+        wta_row<DPL, LT, NT, PART_ONLY>(a, blockIdx.x, blockIdx.y, smem);
     }
 }
 
