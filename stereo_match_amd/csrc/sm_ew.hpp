@@ -118,6 +118,10 @@ __global__ void __launch_bounds__(256) k_ew(EwArgs a)
 // columns of a repaired segment whose cost and partial slices load together (one memory round
 // trip per RC columns on the walks' serial chain; the pass runs ~3 waves per SIMD, so the
 // registers are there)
+// timing ablation (results wrong where a walk never met): no phase-B carries
+#ifndef EW_PATCH_NO_CARRY
+#define EW_PATCH_NO_CARRY 0
+#endif
 #ifndef EW_PATCH_RC
 #define EW_PATCH_RC 16
 #endif
@@ -337,7 +341,7 @@ __global__ void __launch_bounds__(256) k_ew_patch(EwPatchArgs a)
             if (lane == 0) openm[wave][ch] = open;
             if (open && first_open == nwg) first_open = i0 + __builtin_ctzll(open);
         }
-        if (first_open < nwg) {
+        if (first_open < nwg && !EW_PATCH_NO_CARRY) {
             // ---- phase B (line 0, path order from the first open strip): `carry` = the true
             // state entering strip i is T while strip i's values came from e_{i-1}
             order_partial();  // the other lanes' partial and c_k stores
