@@ -197,13 +197,15 @@ __global__ void __launch_bounds__(256) k_ew_patch(EwPatchArgs a)
         b.load(rs, off);
         unpack_ct_pk<CT, DPL>(b, v);
     };
-    // the values of strip k (direction dir) came from the trajectory entering at A; the true
-    // one enters at T: add (true - applied) to the partial until the two meet.  Returns met;
-    // otherwise T holds the true trajectory's state at the strip's far end.  Line-divergent.
-    auto walk = [&](int k, int dir, const uint32_t (&A)[NP], uint32_t (&T)[NP]) -> bool {
+    // the values of strip k (direction dir) came from the trajectory entering at A (the state
+    // at aoff); the true one enters at T (the state at toff, or the caller's registers for
+    // toff == kOOB): add (true - applied) to the partial until the two meet.  Returns 1 met,
+    // 0 never met (T then holds the true trajectory's state at the strip's far end), 2 with
+    // `check` where A == T (nothing to do).  Line-divergent.
+    auto walk = [&](int k, int dir, uint32_t aoff, uint32_t toff, uint32_t (&T)[NP], bool check) -> int {
         const int x0 = k * CW, ncol = ::min(CW, W1 - x0);  // W: every repaired strip is full
         // columns in chunks of RC: the chunk's costs and partial slices load together (the
-        // first chunk's beside the caller's state loads)
+        // first chunk's beside the state loads: one memory round trip for both)
         RawBytes<CB> cc[RC];
         RawBytes<DPL * 2> pb[RC];
         auto issue = [&](int o0) {
@@ -216,6 +218,10 @@ __global__ void __launch_bounds__(256) k_ew_patch(EwPatchArgs a)
             }
         };
         issue(0);
+        uint32_t A[NP];
+        load_state(aoff, A);
+        if (toff != kOOB) load_state(toff, T);
+        if (check && same_state(A, T)) return 2;
         uint32_t Lq[2][NP], mq[2];
 #pragma unroll
         for (int q = 0; q < NP; q++) {
@@ -269,7 +275,7 @@ __global__ void __launch_bounds__(256) k_ew_patch(EwPatchArgs a)
 #pragma unroll
             for (int q = 0; q < NP; q++) T[q] = Lq[1][q];
         }
-        return met;
+        return met ? 1 : 0;
     };
     // OR over the wave's lines (their first lanes) of a per-line 64-bit mask
     auto lines_or = [&](uint64_t v) -> uint64_t {
@@ -325,11 +331,9 @@ __global__ void __launch_bounds__(256) k_ew_patch(EwPatchArgs a)
                 }
                 if (mine >= 0) {
                     const int i = i0 + mine, k = strip_of(i);
-                    uint32_t S[NP], T[NP];
-                    load_state(soff(k, dir, 0), S);
-                    load_state(soff(strip_of(i - 1), dir, 1), T);
+                    uint32_t T[NP];
                     nfix++;
-                    if (!walk(k, dir, S, T)) {
+                    if (walk(k, dir, soff(k, dir, 0), soff(strip_of(i - 1), dir, 1), T, false) == 0) {
                         // c_k, the true trajectory's far-end state, replaces s_k (read only above)
                         store_pk<CT, NP>(rs, soff(k, dir, 0), T);
                         open |= 1ull << mine;
@@ -352,15 +356,10 @@ __global__ void __launch_bounds__(256) k_ew_patch(EwPatchArgs a)
                 for (int q = 0; q < NP; q++) T[q] = 0;
                 for (int i = first_open; i < nwg; i++) {
                     const int k = strip_of(i);
-                    if (carry) {
-                        uint32_t Ep[NP];
-                        load_state(soff(strip_of(i - 1), dir, 1), Ep);
-                        if (same_state(T, Ep)) {
-                            carry = false;
-                        } else {
-                            nfix++;
-                            if (walk(k, dir, Ep, T)) carry = false;
-                        }
+                    if (carry) {  // applied: e_{i-1}; the walk's first chunk loads beside it
+                        const int r = walk(k, dir, soff(strip_of(i - 1), dir, 1), kOOB, T, true);
+                        nfix += r != 2;
+                        if (r != 0) carry = false;
                     }
                     // an open strip's values (from e_{i-1}, or corrected to the true trajectory
                     // where that met them) end at c_k: the next strip needs c_k, not e_k
