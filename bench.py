@@ -142,8 +142,12 @@ def kernel_stage(name: str, names) -> "str | None":
             sweep_modes.add([t.strip() for t in n.split("<", 1)[1].split(">")[0].split(",")][3])
     sweep = bool(sweep_modes) or any("k_sweep2<" in n for n in names)
     lines5 = "3" in sweep_modes and "4" not in sweep_modes  # in-sweep E/W lines, 5 paths: k_wta reads the partial
-    if bool(targs) and targs[-1] == "true" and ("k_sgm_paths" in name or "k_wta" in name):
-        return None  # the guarded fallback instances (run only when a strip gave up)
+    # the guarded fallback instances (run only when a strip gave up): k_sgm_paths<..., FB>,
+    # k_wta<DPL, LT, NT, FB, PART_ONLY>
+    if "k_sgm_paths" in name and targs and targs[-1] == "true":
+        return None
+    if "k_wta<" in name and len(targs) >= 4 and targs[3] == "true":
+        return None
     if "k_sweep2<" in name or "k_sweep<" in name:  # MODE 0 / 3: down sweep -> partial; 1 / 2 / 4: with WTA
         return "sweep" if targs[4 if "k_sweep2<" in name else 3] in ("0", "3") else "sweep_wta"
     if "k_ew_patch" in name or "k_ew<" in name or (sweep and "k_sgm_paths" in name):
