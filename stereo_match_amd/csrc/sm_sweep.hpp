@@ -184,7 +184,14 @@ constexpr int wide_ncw(int D, int ct_bytes)
 // (b + 1) * HB + LEAD, for which it needed rows up to (b + 1) * HB + LEAD + RPW - 1 - LR <=
 // (b + 1) * HB - 2 consumed, all of which the compute waves consume before that barrier.
 #ifndef SWEEP_NLW
-#define SWEEP_NLW 4  // line waves per workgroup (one per SIMD)
+#define SWEEP_NLW 4  // line waves per workgroup (3: the down sweep 13 us per pair slower, 5: 4 us)
+#endif
+// MODE 3 without the poller wave: each halo wave polls its neighbour strip's snapshot itself at
+// the block end and writes it into its own LDS slots before it publishes the block's last row,
+// so the snapshot is ordered by the row counters the neighbouring own wave already waits for
+// (census8 down sweep 75.3 -> 74.6 us per pair; a fifth line wave in the freed slot: 78.9)
+#ifndef SWEEP_HALO_POLL
+#define SWEEP_HALO_POLL 1
 #endif
 #ifndef SWEEP_LINE_PRIO
 #define SWEEP_LINE_PRIO 1  // issue priority of the line waves (compute waves: 3 on the hand-off chain, else 1;
@@ -229,8 +236,10 @@ template <int VL, int DPL, int NCW_, int MODE>
 struct LineGeo {
     using G = SweepGeo<VL, DPL, NCW_>;
     static constexpr bool ON = MODE == 3;
+    static constexpr bool HPOLL = ON && SWEEP_LINE_NOBAR && SWEEP_HALO_POLL && SWEEP_ROW_SYNC;
+    static constexpr int POLLER = HPOLL ? 0 : 1;  // poller waves
     // at most 16 waves per workgroup (1024 threads): compute waves + poller + lines
-    static constexpr int NLW = !ON ? 0 : (SWEEP_NLW < 15 - NCW_ ? SWEEP_NLW : 15 - NCW_);
+    static constexpr int NLW = !ON ? 0 : (SWEEP_NLW < 16 - POLLER - NCW_ ? SWEEP_NLW : 16 - POLLER - NCW_);
     static constexpr int RPW = G::LPW / 2;  // rows per line wave and batch
     // LDS besides the ring: lv, lmin, the counters, a margin
     static constexpr int BASE = 8 * G::COLS * G::D + 16 * G::COLS + 4 * NCW_ + 4 * 16 + 512;
@@ -239,7 +248,7 @@ struct LineGeo {
     static constexpr int LEAD0 = SWEEP_LEAD_BLOCKS * G::HB;
     static constexpr int LEAD = LEAD0 + RPW <= FIT ? LEAD0 : (FIT > RPW ? (FIT - RPW) / RPW * RPW : 0);
     static constexpr int LR = SWEEP_LINE_NOBAR ? FIT : LEAD + 2 * RPW <= FIT ? LEAD + 2 * RPW : LEAD + RPW;
-    static constexpr bool BUILT = ON && NLW >= 1 && DPL % 2 == 0 && !SWEEP_U32 &&
+    static constexpr bool BUILT = ON && NLW >= 3 && DPL % 2 == 0 && !SWEEP_U32 &&
                                   (SWEEP_LINE_NOBAR ? RPW <= FIT : LEAD + RPW <= FIT) &&
                                   G::CW % 2 == 0 && G::HB % RPW == 0 && RPW >= 1;
     // ring chunk of the line loop, per cost type (a divisor of CW / 2)
@@ -251,7 +260,11 @@ struct LineGeo {
     }
 };
 template <int VL, int DPL, int NCW_, int MODE>
-constexpr int sweep_threads() { return SweepGeo<VL, DPL, NCW_>::THREADS + 64 * LineGeo<VL, DPL, NCW_, MODE>::NLW; }
+constexpr int sweep_threads()
+{
+    using LG = LineGeo<VL, DPL, NCW_, MODE>;
+    return SweepGeo<VL, DPL, NCW_>::THREADS + 64 * (LG::NLW - (LG::HPOLL ? 1 : 0));
+}
 
 // NP packed words of one lane <-> LDS (widest aligned chunks)
 template <int NP>
@@ -430,6 +443,7 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
     constexpr bool EWIN = MODE == 1 || MODE == 2;   // E / W path volumes read (k_ew)
     constexpr bool PARTR = MODE == 2 || MODE == 4;  // the down sweep's partial read
     constexpr bool LINES = MODE == 3;               // E / W lines in the kernel (line waves)
+    constexpr bool HPOLL = LG::HPOLL;               // the halo waves poll their neighbours (no poller wave)
     static_assert(!LINES || LG::BUILT, "MODE 3 instance not built for this geometry");
     static_assert(MODE < 3 || (DPL % 2 == 0 && !SWEEP_U32), "MODES 3 / 4 run the packed row loops only");
     constexpr int NTH = sweep_threads<VL, DPL, NCW_, MODE>();
@@ -493,7 +507,7 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
     unsigned long long* hopp = a.hop + (size_t)pair * a.hop_pair;
     auto gbase = [&](int strip, int dir, int b) -> size_t { return ((size_t)(strip * 2 + dir) * nblk + b) * SNG; };
 
-    if (wave == NCW) {
+    if (!HPOLL && wave == NCW) {
         // ---- poller: halo snapshots of the neighbouring strips, once per block.  Granule
         // k*64 + lane of the two records (A from the left strip, then B from the right)
         constexpr int NDAT = G::NDAT;
@@ -614,7 +628,7 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
     }
 
     if constexpr (LINES) {
-        if (wave > NCW) {
+        if (wave >= NCW + LG::POLLER) {
             // ---- line waves (MODE 3): line kl of the wave (VL lanes, DPL disparities per lane)
             // runs direction kl & 1 (0 = E, x ascending; 1 = W) of row y0 + (kl >> 1), over the
             // strip's own columns plus `ewarm` columns before them in its direction, from the
@@ -627,7 +641,7 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
             constexpr bool H16 = sizeof(CT) == 1 && SWEEP_H16;
             constexpr uint32_t EDGE2 = H16 ? 0x7BFF7BFFu : (kBig | (kBig << 16));
             constexpr int LPF = LG::template lpf<CT>();  // cost loads in flight per lane (a divisor of CW / 2)
-            const int li = wave - NCW - 1;
+            const int li = wave - NCW - LG::POLLER;
             const int kl = lane / VL, g = lane % VL;
             const int dir = kl & 1, r = kl >> 1;
             const int H = a.H, W1 = a.W1, x0 = wg * CW;
@@ -1158,6 +1172,43 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
                             if (g == 0) lmin[wb][1][ch + 1] = mnB[h];
                         }
                     }
+                    if constexpr (HPOLL && !OWN) {
+                        // the block's last row: the neighbour strip's state of it replaces this
+                        // halo wave's (stale) columns before the row is published
+                        if (j == HB - 1 && b + 1 < nblk) {
+                            constexpr int dirh = HAS_A ? 0 : 1;  // left halo: A from the left strip
+                            if ((dirh == 0 ? has_left : has_right) && !(a.dbg & 2)) {
+                                constexpr int GH = (SNG + 63) / 64, NDAT = G::NDAT;
+                                const gu64* src[GH];
+                                bool need[GH];
+                                uint32_t v[GH];
+#pragma unroll
+                                for (int k = 0; k < GH; k++) {
+                                    const int r = k * 64 + lane;
+                                    need[k] = r < SNG;
+                                    src[k] = (const gu64*)(hopp + gbase(wg + (dirh ? 1 : -1), dirh, b) + (need[k] ? r : 0));
+                                }
+                                SW_T0(tp);
+                                poll_set<GH>(src, need, tag0 | (uint32_t)(b + 1), v, sync_dead, a.err);
+                                SW_ACC(st_bbar, tp);
+#pragma unroll
+                                for (int k = 0; k < GH; k++) {
+                                    if (!need[k]) continue;
+                                    const int r = k * 64 + lane;
+                                    if (r < NDAT) {
+                                        const int q = r / (HW * VL), pcol = (r / VL) % HW, gg = r % VL;
+                                        const int col = (dirh == 0 ? pcol : NCOL - HW + pcol) + 1;  // LDS column slot
+                                        const int d = gg * DPL + 2 * q;
+                                        if (2 * q + 1 < DPL) *reinterpret_cast<uint32_t*>(&lv[wb][dirh][col][d]) = v[k];
+                                        else lv[wb][dirh][col][d] = (uint16_t)v[k];
+                                    } else {
+                                        const int pcol = r - NDAT;
+                                        lmin[wb][dirh][(dirh == 0 ? pcol : NCOL - HW + pcol) + 1] = v[k];
+                                    }
+                                }
+                            }
+                        }
+                    }
                     // the row is published (neighbour counters) or, at a block end and
                     // without row sync, closed by a barrier; the poller writes the halo
                     // snapshot after the block-end barrier, while the waves run their WTA
@@ -1298,7 +1349,7 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
                         }
                     }
                 }
-                if (b + 1 < nblk) {
+                if (b + 1 < nblk && !HPOLL) {
                     SW_T0(tb);
                     if constexpr (NOBAR) wait_poll(b + 1);
                     else lds_barrier();  // the poller has written the halo snapshot
