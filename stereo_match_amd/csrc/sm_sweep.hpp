@@ -227,16 +227,34 @@ constexpr int largest_divisor_upto(int n, int cap)
 #define SWEEP_LINE_NOBAR 1
 #endif
 // the same counter hand-off in the sweeps without line waves (bit MODE; row-synchronised modes
-// only): the strip's waves away from the halos may start a block while the halo waves wait
+// only): the strip's waves away from the halos may start a block while the halo waves wait.
+// With the halo waves polling (SWEEP_HALO_POLL, no poller wave) the MODE 4 up + WTA sweep ran
+// 60.6 -> 57.2 us per pair (census8); with the poller wave it had measured level
 #ifndef SWEEP_NOBAR_MODES
-#define SWEEP_NOBAR_MODES 0
+#define SWEEP_NOBAR_MODES 16
 #endif
 constexpr int kMaxLds = 163840;  // gfx950: LDS one workgroup may declare
+// neighbour-counter row sync: KITTI 8 pairs, down sweep census8 96.4 -> 92.0 us per pair,
+// sgbm8 124.0 -> 120.8, census8 WTA sweep level (96.6 / 96.0); the 5-path WTA sweep is
+// slower with it (95.3 -> 97.9) and keeps the row barriers
+#ifndef SWEEP_ROWSYNC_M1
+#define SWEEP_ROWSYNC_M1 0
+#endif
+// the counter hand-off (no block barriers) and, with it, the halo waves' own polling: MODE 3
+// (its line waves), the other row-synchronised modes in SWEEP_NOBAR_MODES
+template <int DPL, int MODE>
+constexpr bool sweep_nobar()
+{
+    return SWEEP_ROW_SYNC && (MODE != 1 || SWEEP_ROWSYNC_M1) && DPL % 2 == 0 && !SWEEP_U32 &&
+           (MODE == 3 ? SWEEP_LINE_NOBAR != 0 : ((SWEEP_NOBAR_MODES >> MODE) & 1) != 0);
+}
+template <int DPL, int MODE>
+constexpr bool sweep_halo_poll() { return sweep_nobar<DPL, MODE>() && SWEEP_HALO_POLL; }
 template <int VL, int DPL, int NCW_, int MODE>
 struct LineGeo {
     using G = SweepGeo<VL, DPL, NCW_>;
     static constexpr bool ON = MODE == 3;
-    static constexpr bool HPOLL = ON && SWEEP_LINE_NOBAR && SWEEP_HALO_POLL && SWEEP_ROW_SYNC;
+    static constexpr bool HPOLL = sweep_halo_poll<DPL, MODE>();
     static constexpr int POLLER = HPOLL ? 0 : 1;  // poller waves
     // at most 16 waves per workgroup (1024 threads): compute waves + poller + lines
     static constexpr int NLW = !ON ? 0 : (SWEEP_NLW < 16 - POLLER - NCW_ ? SWEEP_NLW : 16 - POLLER - NCW_);
@@ -263,7 +281,7 @@ template <int VL, int DPL, int NCW_, int MODE>
 constexpr int sweep_threads()
 {
     using LG = LineGeo<VL, DPL, NCW_, MODE>;
-    return SweepGeo<VL, DPL, NCW_>::THREADS + 64 * (LG::NLW - (LG::HPOLL ? 1 : 0));
+    return SweepGeo<VL, DPL, NCW_>::THREADS + 64 * (LG::NLW - (LG::HPOLL ? 1 : 0));  // (HPOLL: no poller)
 }
 
 // NP packed words of one lane <-> LDS (widest aligned chunks)
@@ -461,16 +479,9 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
 #endif
     constexpr int PRIO_HI = 3, PRIO_LO = MODE == 0 ? 2 : 1;  // mode 0 stays above the E/W kernel
     if constexpr (MODE == 0 && SWEEP_PRIO > 0) __builtin_amdgcn_s_setprio(SWEEP_PRIO);
-    // neighbour-counter row sync: KITTI 8 pairs, down sweep census8 96.4 -> 92.0 us per pair,
-    // sgbm8 124.0 -> 120.8, census8 WTA sweep level (96.6 / 96.0); the 5-path WTA sweep is
-    // slower with it (95.3 -> 97.9) and keeps the row barriers
-#ifndef SWEEP_ROWSYNC_M1
-#define SWEEP_ROWSYNC_M1 0
-#endif
     constexpr bool ROWSYNC = SWEEP_ROW_SYNC && (MODE != 1 || SWEEP_ROWSYNC_M1);
     // block hand-off by LDS counters instead of the two workgroup barriers per block
-    constexpr bool NOBAR = ROWSYNC && DPL % 2 == 0 && !SWEEP_U32 &&  // (the packed row loops)
-                           (LINES ? SWEEP_LINE_NOBAR != 0 : ((SWEEP_NOBAR_MODES >> MODE) & 1) != 0);
+    constexpr bool NOBAR = sweep_nobar<DPL, MODE>();  // (the packed row loops)
     static_assert(!LINES || ROWSYNC, "the line waves mirror the row-synchronised barrier pattern");
     constexpr int LPW = G::LPW, NCW = G::NCW, HB = G::HB, NCOL = G::NCOL, COLS = G::COLS, CW = G::CW, D = G::D;
     constexpr int NG = G::NG, SNG = G::SNG, PF = G::PF, HM = G::HM, HW = G::HW;
