@@ -229,9 +229,11 @@ constexpr int largest_divisor_upto(int n, int cap)
 // the same counter hand-off in the sweeps without line waves (bit MODE; row-synchronised modes
 // only): the strip's waves away from the halos may start a block while the halo waves wait.
 // With the halo waves polling (SWEEP_HALO_POLL, no poller wave) the MODE 4 up + WTA sweep ran
-// 60.6 -> 57.2 us per pair (census8); with the poller wave it had measured level
+// 60.6 -> 57.2 us per pair (census8), Middlebury's MODE 2 2078 -> 1951 (modes 0 / 2 with E/W
+// volumes: D = 256, mc-cnn); with the poller wave it had measured level.  MODE 1 (5 paths
+// without lines) keeps its row barriers (SWEEP_ROWSYNC_M1)
 #ifndef SWEEP_NOBAR_MODES
-#define SWEEP_NOBAR_MODES 16
+#define SWEEP_NOBAR_MODES 21
 #endif
 constexpr int kMaxLds = 163840;  // gfx950: LDS one workgroup may declare
 // neighbour-counter row sync: KITTI 8 pairs, down sweep census8 96.4 -> 92.0 us per pair,
