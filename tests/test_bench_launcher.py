@@ -104,3 +104,27 @@ def test_headline_model_numbers():
     assert bench.model_pair_bytes("census8", H, W, D, 8) == 59_616_000 * 13 + 6 * H * W
     # per-direction aggregation owns P reads + the u16 S write: 10 B per cell (4.77 GB / 8 pairs)
     assert bench.model_stage_bytes("paths", "census8", H, W, D, 8, False) * 8 == 4_769_280_000
+
+
+def test_kernel_stage_attribution_of_the_engines_kernels():
+    """The PMC / SQ summaries sum a stage's kernels by name (tools/traffic_summary.py,
+    valu_summary.py): the guarded fallback instances belong to no stage, the partial-only WTA
+    instance (k_wta<..., false, true>) is the 5-path lines engine's WTA stage."""
+    lines5 = ["void smk::k_sweep<16, 8, unsigned short, 3, 11>(smk::SweepArgs)",
+              "void smk::k_ew_patch<16, 4, unsigned short>(smk::EwPatchArgs)",
+              "void smk::k_wta<8, unsigned short, 1024, false, true>(smk::WtaArgs)",
+              "void smk::k_wta<8, unsigned short, 1024, true, false>(smk::WtaArgs)",
+              "void smk::k_sgm_paths<8, 16, 16, 8, false, unsigned short, true>(smk::PathsArgs)",
+              "void smk::k_sgbm_cost2<2, 8, 1>(smk::SgbmCost2Args)"]
+    st = {n: bench.kernel_stage(n, lines5) for n in lines5}
+    assert st[lines5[0]] == "sweep" and st[lines5[1]] == "horizontal"
+    assert st[lines5[2]] == "sweep_wta"
+    assert st[lines5[3]] is None and st[lines5[4]] is None  # fallback instances
+    assert st[lines5[5]] == "cost"
+    lines8 = ["void smk::k_sweep<16, 8, unsigned char, 3, 11>(smk::SweepArgs)",
+              "void smk::k_sweep<16, 8, unsigned char, 4, 11>(smk::SweepArgs)",
+              "smk::k_lr_rows(unsigned int const*, unsigned int const*, short*, short*, int, int, int, int, int, int, int, unsigned int const*)"]
+    assert [bench.kernel_stage(n, lines8) for n in lines8] == ["sweep", "sweep_wta", "wta"]
+    perdir = ["void smk::k_sgm_paths<8, 16, 16, 8, true, unsigned char, false>(smk::PathsArgs)",
+              "void smk::k_wta<8, unsigned char, 1024, false, false>(smk::WtaArgs)"]
+    assert [bench.kernel_stage(n, perdir) for n in perdir] == ["paths", "wta"]
