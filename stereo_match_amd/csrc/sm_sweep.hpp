@@ -194,8 +194,10 @@ constexpr int wide_ncw(int D, int ct_bytes)
 #define SWEEP_HALO_POLL 1
 #endif
 #ifndef SWEEP_LINE_PRIO
-#define SWEEP_LINE_PRIO 1  // issue priority of the line waves (compute waves: 3 on the hand-off chain, else 1;
-                           // measured: 2 costs 9 us per pair, 0 and 1 tie)
+#define SWEEP_LINE_PRIO 2  // issue priority of the line waves (compute waves: 3 on the hand-off chain, else 1;
+                           // with the counter hand-off and the halo waves polling: 1 -> 2 census8 down
+                           // sweep 76.0 -> 70.5 us per pair, sgbm5 89 -> 83, 3 level with 2, 0 level
+                           // with 1; with block barriers 2 had cost 9 us)
 #endif
 // cost loads in flight per line lane (at most; the largest divisor of CW / 2 below this, so
 // that the line's phases fall on ring-chunk boundaries): the lines run ahead of the compute
