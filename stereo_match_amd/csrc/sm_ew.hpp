@@ -122,6 +122,9 @@ __global__ void __launch_bounds__(256) k_ew(EwArgs a)
 #ifndef EW_PATCH_NO_CARRY
 #define EW_PATCH_NO_CARRY 0
 #endif
+#ifndef EW_PATCH_B64
+#define EW_PATCH_B64 1  // phase B's carried walks on 64-lane lines where D % 128 == 0
+#endif
 #ifndef EW_PATCH_RC
 #define EW_PATCH_RC 16
 #endif
@@ -277,6 +280,110 @@ __global__ void __launch_bounds__(256) k_ew_patch(EwPatchArgs a)
         }
         return met ? 1 : 0;
     };
+    // phase B on the whole wave: 64-lane lines (D % 128 == 0), DPLW disparities per lane, so a
+    // carried walk's serial step is a quarter of a 16-lane line's per-lane work
+    constexpr int DPLW = D % 128 == 0 ? D / 64 : 2, NPW = DPLW / 2;
+    constexpr int CBW = DPLW * (int)sizeof(CT);
+    auto soff64 = [&](int k, int dir, int which) -> uint32_t {
+        return (((((uint32_t)y * (uint32_t)nwg + (uint32_t)k) * 2u + (uint32_t)dir) * 2u + (uint32_t)which) *
+                    (uint32_t)D + (uint32_t)(lane * DPLW)) * (uint32_t)sizeof(CT);
+    };
+    auto cell64 = [&](int c) -> uint32_t {
+        return ((uint32_t)y * (uint32_t)W1 + (uint32_t)c) * (uint32_t)D + (uint32_t)(lane * DPLW);
+    };
+    auto load_state64 = [&](uint32_t off, uint32_t (&v)[NPW]) {
+        RawBytes<CBW> b;
+        b.load(rs, off);
+        unpack_ct_pk<CT, DPLW>(b, v);
+    };
+    auto same_state64 = [&](const uint32_t (&x)[NPW], const uint32_t (&z)[NPW]) -> bool {
+        bool ok = true;
+#pragma unroll
+        for (int i = 0; i < NPW; i++) ok &= x[i] == z[i];
+        return __all(ok);
+    };
+    auto state_min64 = [&](const uint32_t (&x)[NPW]) -> uint32_t {
+        uint32_t m = x[0];
+#pragma unroll
+        for (int i = 1; i < NPW; i++) m = pk_min(m, x[i]);
+        m = ::min(m & 0xFFFFu, m >> 16);
+        return Line<64>::min(m) * 0x10001u;
+    };
+    auto walk64 = [&](int k, int dir, uint32_t aoff, uint32_t toff, uint32_t (&T)[NPW], bool check) -> int {
+        const int x0 = k * CW, ncol = ::min(CW, W1 - x0);  // W: every repaired strip is full
+        // columns in chunks of RC: the chunk's costs and partial slices load together (the
+        // first chunk's beside the state loads: one memory round trip for both)
+        RawBytes<CBW> cc[RC];
+        RawBytes<DPLW * 2> pb[RC];
+        auto issue = [&](int o0) {
+#pragma unroll
+            for (int u = 0; u < RC; u++) {
+                const int o = o0 + u;
+                const int c = dir ? x0 + CW - 1 - o : x0 + o;
+                cc[u].load(rc, o < ncol ? cell64(c) * (uint32_t)sizeof(CT) : kOOB);
+                pb[u].load(rp, o < ncol ? cell64(c) * 2u : kOOB);
+            }
+        };
+        issue(0);
+        uint32_t A[NPW];
+        load_state64(aoff, A);
+        if (toff != kOOB) load_state64(toff, T);
+        if (check && same_state64(A, T)) return 2;
+        uint32_t Lq[2][NPW], mq[2];
+#pragma unroll
+        for (int q = 0; q < NPW; q++) {
+            Lq[0][q] = A[q];
+            Lq[1][q] = T[q];
+        }
+        mq[0] = state_min64(Lq[0]);
+        mq[1] = state_min64(Lq[1]);
+        bool met = false;
+        for (int o0 = 0; o0 < ncol && !met; o0 += RC) {
+            if (o0 > 0) issue(o0);
+#pragma unroll
+            for (int u = 0; u < RC; u++) {  // (no break: the loop must unroll)
+                const int o = o0 + u;
+                if (o >= ncol || met) continue;
+                const int c = dir ? x0 + CW - 1 - o : x0 + o;
+                uint32_t C2[2][NPW], Ln[2][NPW], mn[2];
+                unpack_ct_pk<CT, DPLW>(cc[u], C2[0]);
+#pragma unroll
+                for (int q = 0; q < NPW; q++) C2[1][q] = C2[0][q];
+                sweep_step2n<64, NPW, H16, 2>(Lq, mq, C2, P1p, P2p, 0u, 0u, Ln, mn);
+                if (same_state64(Ln[0], Ln[1])) {
+                    met = true;
+                    continue;
+                }
+                uint32_t P[NPW];
+#pragma unroll
+                for (int q = 0; q < NPW; q++) {
+                    if constexpr (SAT) {
+                        // a half pv < 0xFFFF is the exact sum, pv >= sv: (pv - sv) + tv saturating;
+                        // pv == 0xFFFF stays (sat: 0xFFFF exactly there, from pv + 1 wrapping to 0)
+                        const uint32_t pv = pb[u].w[q];
+                        const uint32_t x = pk_adds(pk_sub(pv, Ln[0][q]), Ln[1][q]);
+                        const uint32_t sat = pk_sub(pk_min(pk_add(pv, 0x00010001u), 0x00010001u), 0x00010001u);
+                        P[q] = pkw(__builtin_elementwise_max(pkv(x), pkv(sat)));
+                    } else {  // census: every sum < 2^11, the u16 wrap is exact
+                        P[q] = pk_add(pk_sub(pb[u].w[q], Ln[0][q]), Ln[1][q]);
+                    }
+                }
+                bstore_n<uint32_t, NPW>(rp, cell64(c) * 2u, P);
+#pragma unroll
+                for (int q = 0; q < NPW; q++) {
+                    Lq[0][q] = Ln[0][q];
+                    Lq[1][q] = Ln[1][q];
+                }
+                mq[0] = mn[0];
+                mq[1] = mn[1];
+            }
+        }
+        if (!met) {
+#pragma unroll
+            for (int q = 0; q < NPW; q++) T[q] = Lq[1][q];
+        }
+        return met ? 1 : 0;
+    };
     // OR over the wave's lines (their first lanes) of a per-line 64-bit mask
     auto lines_or = [&](uint64_t v) -> uint64_t {
         uint64_t m = 0;
@@ -345,7 +452,27 @@ __global__ void __launch_bounds__(256) k_ew_patch(EwPatchArgs a)
             if (lane == 0) openm[wave][ch] = open;
             if (open && first_open == nwg) first_open = i0 + __builtin_ctzll(open);
         }
-        if (first_open < nwg && !EW_PATCH_NO_CARRY) {
+        if (first_open < nwg && !EW_PATCH_NO_CARRY && D % 128 == 0 && EW_PATCH_B64) {
+            // ---- phase B on 64-lane lines (the same walk, the whole wave)
+            order_partial();  // the other lanes' partial and c_k stores
+            bool carry = false;
+            uint32_t T[NPW];
+#pragma unroll
+            for (int q = 0; q < NPW; q++) T[q] = 0;
+            for (int i = first_open; i < nwg; i++) {
+                const int k = strip_of(i);
+                if (carry) {
+                    const int r = walk64(k, dir, soff64(strip_of(i - 1), dir, 1), kOOB, T, true);
+                    nfix += r != 2 && kl == 0;
+                    if (r != 0) carry = false;
+                }
+                const bool open_i = ((openm[wave][(i - 1) / CHUNK] >> ((i - 1) % CHUNK)) & 1ull) != 0;
+                if (!carry && open_i) {
+                    load_state64(soff64(k, dir, 0), T);
+                    carry = true;
+                }
+            }
+        } else if (first_open < nwg && !EW_PATCH_NO_CARRY) {
             // ---- phase B (line 0, path order from the first open strip): `carry` = the true
             // state entering strip i is T while strip i's values came from e_{i-1}
             order_partial();  // the other lanes' partial and c_k stores
