@@ -84,8 +84,9 @@ def parse():
                          "(sm_set_tuning; every value gives the same disparities)")
     ap.add_argument("--cpu-baseline-pairs", type=int, default=8,
                     help="pairs timed on the host C port per thread (rank 0, N=1 only); 0 = skip")
-    ap.add_argument("--cpu-threads", type=int, default=16,
-                    help="host threads for the multi-core CPU baseline (the box's CPU share is 16)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="host threads for the multi-core CPU baseline; 0 = the process's CPU share "
+                         "(cpu_share(): OMP_NUM_THREADS where the pool sets it, else the affinity mask)")
     ap.add_argument("--host-surface-calls", type=int, default=20,
                     help="rank 0, N=1: timed calls of the reference surface compute_disparity (host numpy in/out, "
                          "settings.ini, KITTI size); 0 = skip")
@@ -429,12 +430,7 @@ class GpuWorkload:
             "mpix_disp_per_s": gpairs * K / elapsed * cells / 1e6,
             "roofline": {
                 "kernel": kern[dom][0],
-                **(valu_roofline(valu, launch_s) if self.bm else {
-                    "bound": "hbm",
-                    "achieved": achieved,
-                    "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s",
-                    "frac": (achieved / HBM_PEAK_GBS) if achieved else None}),
+                **(valu_roofline(valu, launch_s) if self.bm else hbm_roofline(achieved, valu)),
                 "traffic": traffic,
                 "alg_bytes_per_launch": alg_bytes,
                 "alg_model": "SURVEY §8d bytes owned by this stage (bench.model_stage_bytes)",
@@ -458,7 +454,10 @@ class GpuWorkload:
                 "bytes_per_pair": survey_bytes,
                 "wall_us_per_pair": pair_s * 1e6,
                 "achieved_GBs": survey_bytes / pair_s / 1e9 if pair_s > 0 else None,
-                "frac": survey_bytes / pair_s / 1e9 / HBM_PEAK_GBS if pair_s > 0 else None,
+                # StereoBM streams no cost volume: its few bytes per pixel against HBM say nothing
+                # (its ceiling is VALU issue, roofline.valu)
+                "frac": None if self.bm else survey_bytes / pair_s / 1e9 / HBM_PEAK_GBS if pair_s > 0 else None,
+                **({"frac_note": "none for StereoBM: no cost volume; VALU-bound (roofline)"} if self.bm else {}),
             },
             "stage_us_per_pair": {k: v[0] * 1e3 / max(v[2], 1) for k, v in self.profile.items()},
             "stage_profile": f"last {self.n_prof} warmup steps, every stage timed; the timed region times only "
@@ -718,6 +717,21 @@ def design_kernels(args, stages, H, W, D, p, P_dirs, sweep, bm, lines=False):
 VALU_PEAK_GINSTR = 1024 * 2.4 / 4
 
 
+def hbm_roofline(achieved, valu):
+    """The dominant kernel's HBM roofline (achieved = SURVEY §8(d) bytes / launch time) and the
+    ceiling that binds it: ``bound`` names VALU when the kernel's VALU issue fraction (SQ counters,
+    read_valu) exceeds its HBM fraction.  achieved / peak / frac stay the HBM figures; both
+    fractions are quoted."""
+    f_hbm = achieved / HBM_PEAK_GBS if achieved else None
+    f_valu = valu.get("frac") if isinstance(valu, dict) else None
+    binding = "valu" if f_valu is not None and f_hbm is not None and f_valu > f_hbm else "hbm"
+    return {"bound": binding, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": f_hbm,
+            "frac_hbm": f_hbm, "frac_valu": f_valu,
+            "bound_note": "achieved/peak/frac: SURVEY §8(d) bytes against HBM; bound = the larger of the HBM "
+                          "and VALU-issue fractions (frac_valu = SQ_INSTS_VALU x 4 cycles over the launch, "
+                          "roofline.valu)" + ("" if f_valu is not None else "; no VALU counter file: HBM assumed")}
+
+
 def valu_roofline(valu, launch_s):
     """StereoBM (no cost volume: the SAD window sums are VALU work): the dominant kernel against
     the VALU issue ceiling, from the SQ_INSTS_VALU counter file (tools/valu.sh --mode bm)."""
@@ -875,7 +889,8 @@ def cpu_baseline(args, H, W, D, p, lefts, rights, out0, volume, full=False, hs=N
     from stereo_match_amd import synthetic
 
     n = args.cpu_baseline_pairs
-    T = max(1, args.cpu_threads)
+    share, share_src = cpu_share()
+    T = max(1, args.cpu_threads or share)
     if volume:
         n = max(1, n // 4)  # ~4x the work per pair (D=192, u16 volume, cost quantisation)
         vol0 = synthetic.absdiff_volume(lefts[0], rights[0], D)[0]
@@ -934,6 +949,12 @@ def cpu_baseline(args, H, W, D, p, lefts, rights, out0, volume, full=False, hs=N
         "single_thread": {"value": n1 / dt1, "unit": "pairs/s", "cores": 1, "sample": f"{n1} {what}, {dt1:.1f} s"},
         "mpix_disp_per_s": T * n * H * W * D / dtT / 1e6,
         "host_cpus_visible": os.cpu_count(),
+        "affinity_cpus": len(os.sched_getaffinity(0)),
+        "cpu_share": share,
+        "cores_rule": f"--cpu-threads {args.cpu_threads}" if args.cpu_threads else
+                      f"the process's CPU share, {share_src}: the GPU pool gives one GPU's job 16 host CPUs and "
+                      f"sets OMP_NUM_THREADS to that share, while os.cpu_count() and the affinity mask show the "
+                      f"whole machine",
         "gpu_matches_port_pair0": bool(np.array_equal(first, out0)),
     }
     # BASELINE.md CPU plan step 2: the numpy oracle on Tsukuba (config 1), median of 5 after 1 warm-up
@@ -964,6 +985,16 @@ def cpu_baseline(args, H, W, D, p, lefts, rights, out0, volume, full=False, hs=N
             "gpu_matches_port": bool(np.array_equal(dl, displ) and np.array_equal(fl, filt)),
         }
     return out
+
+
+def cpu_share():
+    """Host threads this job may use: OMP_NUM_THREADS where the environment sets it (the GPU pool
+    sets it to the job's CPU share), else the CPUs in this process's affinity mask."""
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    if env.isdigit() and int(env) > 0:
+        return int(env), f"OMP_NUM_THREADS={env}"
+    n = len(os.sched_getaffinity(0))
+    return n, f"affinity mask ({n} CPUs)"
 
 
 def _wls_oracle_params(p, D):

@@ -88,6 +88,17 @@ def compute(left: np.ndarray, right: np.ndarray, params: dict, median: bool = Tr
     return out
 
 
+def compute_many(pairs, params: dict, threads: int = 8, median: bool = True):
+    """compute() over a list of (left, right) pairs on host threads (ctypes releases the GIL
+    during the call; the port is single-threaded per pair): the batch tests' checker for every
+    pair of a launch group."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    load()
+    with ThreadPoolExecutor(max_workers=max(1, min(threads, len(pairs)))) as ex:
+        return list(ex.map(lambda lr: compute(lr[0], lr[1], params, median), pairs))
+
+
 def compute_wta(left: np.ndarray, right: np.ndarray, params: dict, median: bool = True):
     """(disparity int16 [H, W], integer WTA index int16 [H, W]) of a gray pair: the index is
     OpenCV's bestDisp in [0, D) where the pixel passes the uniqueness test, -1 elsewhere

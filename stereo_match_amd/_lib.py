@@ -145,6 +145,22 @@ def wls_default_params(left: SmParams) -> SmWlsParams:
     return out
 
 
+def volume_scale(scale) -> float:
+    """The C-ABI's scale argument for an external cost volume: "auto" -> 0.0 (the window derived
+    per pair on the device), else the explicit float (NaN is refused: it would quantise every
+    cell to NaN; the C-ABI itself treats NaN like 0)."""
+    if isinstance(scale, str):
+        if scale != "auto":
+            raise ValueError(f"scale must be a number or 'auto', not {scale!r}")
+        return 0.0
+    if scale is None:
+        raise ValueError("scale=None is ambiguous: pass 'auto' for the per-pair window or a number")
+    s = float(scale)
+    if s != s:
+        raise ValueError("scale is NaN: pass 'auto' for the per-pair window")
+    return s
+
+
 def header_symbols(path: str = HEADER_PATH):
     """Function names declared in include/stereo_match_amd.h."""
     with open(path) as f:
@@ -304,10 +320,12 @@ class Engine:
 
     # -- external cost volume (mc-cnn) ----------------------------------------
     def aggregate_cost_f32(self, vol: np.ndarray, params: SmParams, offset: float = 0.0,
-                           scale=None) -> np.ndarray:
-        """SGM over a float32 d-major cost volume [D][H][W] (or [1][D][H][W]).  scale None (or 0):
-        the quantisation window from the volume's own finite range (include/stereo_match_amd.h)."""
-        scale = 0.0 if scale is None else scale
+                           scale=1.0) -> np.ndarray:
+        """SGM over a float32 d-major cost volume [D][H][W] (or [1][D][H][W]).  scale "auto"
+        (opt-in): the quantisation window from the volume's own finite range, per pair
+        (include/stereo_match_amd.h: scale 0 at the C-ABI); default: the explicit window
+        offset 0, scale 1."""
+        scale = volume_scale(scale)
         v = np.ascontiguousarray(vol, np.float32)
         if v.ndim == 4:
             if v.shape[0] != 1:
@@ -322,10 +340,10 @@ class Engine:
         return out
 
     def aggregate_cost_f32_device(self, d_cost: int, npairs: int, pair_stride_elems: int, D: int, H: int,
-                                  W: int, params: SmParams, offset: float, scale: float, d_out: int):
+                                  W: int, params: SmParams, offset: float, scale, d_out: int):
         self._check(self._lib.sm_aggregate_cost_f32_device(
             self.ctx, ctypes.c_void_p(d_cost), npairs, pair_stride_elems, D, H, W, ctypes.byref(params),
-            float(offset), float(scale), ctypes.c_void_p(d_out)))
+            float(offset), volume_scale(scale), ctypes.c_void_p(d_out)))
 
     # -- WLS post-filter --------------------------------------------------------
     def wls_filter(self, displ: np.ndarray, guide: np.ndarray, dispr, params: "SmWlsParams") -> np.ndarray:

@@ -110,10 +110,10 @@ constexpr int DBG_FORCE_FALLBACK = 1 << 23;
 // up waiting; cleared by the host before each group), the sticky error of the
 // (unguarded) hybrid engine, and the count of fallback recomputations
 constexpr int ERR_GROUP0 = 0, ERR_STICKY = 32, ERR_FALLBACKS = 48;
-// E/W strip segments the patch pass recomputed and (50) those whose walk never met within the
-// strip (u32), and (u64 words at 52, 54) the external cost-volume cells clamped by the
-// quantisation window / NaN cells
-constexpr int ERR_EW_REPAIRS = 49, ERR_EW_OPEN = 50, ERR_VOL_CLAMPED = 52, ERR_VOL_NAN = 54;
+// (u64 words at 52, 54) the external cost-volume cells clamped by the quantisation window / NaN
+// cells, and (u64 words at 56, 58) the E/W strip segments the patch pass recomputed and those
+// whose walk never met within the strip (64-bit: a service repairs hundreds of segments per pair)
+constexpr int ERR_VOL_CLAMPED = 52, ERR_VOL_NAN = 54, ERR_EW_REPAIRS = 56, ERR_EW_OPEN = 58;
 // timing ablation: no guarded fallback launches after the sweeps
 constexpr int DBG_NO_FALLBACK = (int)0x80000000u;
 // flags only the ablation build (SM_ABLATIONS) accepts: timing switches whose results are
@@ -1137,7 +1137,7 @@ int run_lines(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs, hipStream_t 
         pa.P1 = n.P1;
         pa.P2 = n.P2;
         pa.guard = gflag;
-        pa.fixes = (uint32_t*)ctx->sweep_err.p + ERR_EW_REPAIRS;
+        pa.fixes = reinterpret_cast<unsigned long long*>((uint32_t*)ctx->sweep_err.p + ERR_EW_REPAIRS);
         const hipError_t e = smk::ew_patch_launch(n.D, (int)et, pa, G, ctx->stream);
         if (e == hipErrorInvalidValue) return fail(ctx, SM_E_UNSUPPORTED, "E/W patch: numDisparities %d not built", n.D);
         HIP_TRY(ctx, e);
@@ -1590,7 +1590,7 @@ int run_group(sm_ctx* ctx, const Src& src, const Geo& g, const Norm& n, int16_t*
             if ((rc = ensure(ctx, bs.cost, (size_t)G * g.vol * 2)) != SM_OK) return rc;
             if ((rc = ensure_sweep_err(ctx)) != SM_OK) return rc;  // (holds the clamp / NaN counters)
             const float* win = nullptr;
-            if (!(src.scale != 0.f)) {  // scale 0 (or NaN): the window from the volume's own range
+            if (src.scale == 0.f || std::isnan(src.scale)) {  // scale 0 or NaN: the window from the volume's own range
                 if ((rc = ensure(ctx, ctx->volwin, (size_t)G * 16)) != SM_OK) return rc;
                 smk::VolWinArgs wa{};
                 wa.vol = src.vol;
@@ -2922,17 +2922,17 @@ int sm_get_counter(sm_ctx* ctx, int which, long long* value)
         HIP_TRY(ctx, hipSetDevice(ctx->device));
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
         HIP_TRY(ctx, hipStreamSynchronize(ctx->side));
-        if (which == SM_COUNTER_VOLUME_CLAMPED || which == SM_COUNTER_VOLUME_NAN) {
+        if (which != SM_COUNTER_SWEEP_FALLBACKS) {  // u64 words
             unsigned long long u = 0;
-            const int word = which == SM_COUNTER_VOLUME_CLAMPED ? ERR_VOL_CLAMPED : ERR_VOL_NAN;
+            const int word = which == SM_COUNTER_VOLUME_CLAMPED ? ERR_VOL_CLAMPED
+                             : which == SM_COUNTER_VOLUME_NAN   ? ERR_VOL_NAN
+                             : which == SM_COUNTER_EW_OPEN      ? ERR_EW_OPEN
+                                                                : ERR_EW_REPAIRS;
             HIP_TRY(ctx, hipMemcpy(&u, (uint32_t*)ctx->sweep_err.p + word, 8, hipMemcpyDeviceToHost));
             v = (long long)u;
         } else {
             uint32_t u = 0;
-            const int word = which == SM_COUNTER_SWEEP_FALLBACKS ? ERR_FALLBACKS
-                             : which == SM_COUNTER_EW_OPEN         ? ERR_EW_OPEN
-                                                                   : ERR_EW_REPAIRS;
-            HIP_TRY(ctx, hipMemcpy(&u, (uint32_t*)ctx->sweep_err.p + word, 4, hipMemcpyDeviceToHost));
+            HIP_TRY(ctx, hipMemcpy(&u, (uint32_t*)ctx->sweep_err.p + ERR_FALLBACKS, 4, hipMemcpyDeviceToHost));
             v = u;
         }
     }

@@ -274,9 +274,9 @@ __global__ void __launch_bounds__(256) k_ew_patch(EwPatchArgs a)
                 mq[1] = mn[1];
             }
         }
-        if (!met) {
+        if (!met) {  // the true far-end state, in the min-0 form of the stored boundary states
 #pragma unroll
-            for (int q = 0; q < NP; q++) T[q] = Lq[1][q];
+            for (int q = 0; q < NP; q++) T[q] = pk_sub(Lq[1][q], mq[1]);
         }
         return met ? 1 : 0;
     };
@@ -378,9 +378,9 @@ __global__ void __launch_bounds__(256) k_ew_patch(EwPatchArgs a)
                 mq[1] = mn[1];
             }
         }
-        if (!met) {
+        if (!met) {  // (min-0 form, as above)
 #pragma unroll
-            for (int q = 0; q < NPW; q++) T[q] = Lq[1][q];
+            for (int q = 0; q < NPW; q++) T[q] = pk_sub(Lq[1][q], mq[1]);
         }
         return met ? 1 : 0;
     };
@@ -502,8 +502,8 @@ __global__ void __launch_bounds__(256) k_ew_patch(EwPatchArgs a)
     }
     if (a.fixes) {
         nfix = group_sum_u32_wave(g == 0 ? nfix : 0u);  // every line's walks
-        if (lane == 0 && nfix) atomicAdd(a.fixes, nfix);
-        if (lane == 0 && nopen) atomicAdd(a.fixes + 1, nopen);  // (the next counter word)
+        if (lane == 0 && nfix) atomicAdd(a.fixes, (unsigned long long)nfix);
+        if (lane == 0 && nopen) atomicAdd(a.fixes + 1, (unsigned long long)nopen);  // (the next counter)
     }
 }
 

@@ -170,11 +170,12 @@ __device__ __forceinline__ uint32_t sweep_step_h16(const uint32_t (&Lp)[NP], uin
 //  * 16-lane lines take the d - 1 / d + 1 neighbours across lanes with zero-filling DPP
 //    moves OR'ed with the per-lane edge constants eL / eR (EDGE on the line's first /
 //    last lane, 0 elsewhere), which the compiler fuses into one v_or_b32_dpp each.
-template <int VL, int NP, bool H16>
+template <int VL, int NP, bool H16, bool DS = false>
 __device__ __forceinline__ uint32_t sweep_step2(const uint32_t (&Lp)[NP], uint32_t mmp, const uint32_t (&C)[NP],
                                                 uint32_t P1p, uint32_t P2p, uint32_t eL, uint32_t eR,
                                                 uint32_t (&Ln)[NP])
 {
+    static_assert(!DS || H16, "deferred subtraction (sweep_step2n): census f16 form only");
     constexpr uint32_t EDGE = H16 ? 0x7BFF7BFFu : (kBig | (kBig << 16));
     uint32_t lm, lq;
     if constexpr (VL == 16) {
@@ -201,7 +202,7 @@ __device__ __forceinline__ uint32_t sweep_step2(const uint32_t (&Lp)[NP], uint32
         const uint32_t a2 = __builtin_amdgcn_alignbit(k + 1 < NP ? Lp[k + 1] : lq, Lp[k], 16);
         if constexpr (H16) {
             const uint32_t v = h2min3(h2add(h2min(a1, a2), P1p), Lp[k], dl);
-            Ln[k] = h2add(h2sub(v, mmp), C[k]);
+            Ln[k] = DS ? h2add(v, C[k]) : h2add(h2sub(v, mmp), C[k]);
         } else {
             uint32_t v = pk_min(pk_add(pk_min(a1, a2), P1p), Lp[k]);
             v = pk_min(v, dl);
@@ -262,11 +263,18 @@ __device__ __forceinline__ void group_min_n(uint32_t (&v)[ND])
     }
 }
 
-template <int VL, int NP, bool H16, int ND>
+// DS (deferred subtraction, census f16 form only): the step leaves out "- minLp", so the new
+// state is R = L + minLp (every later step is shift-invariant: min3(R, R_d+-1 + P1, minR + P2)
+// moves with a constant shift of its input, so the true value of any state's successor is
+// R_next - minR of that state).  The caller subtracts the input minima once per sum of paths
+// instead of once per word and path, and renormalises the state (R - minR) often enough that
+// every value stays below the f16 form's 2^11 (sm_sweep.hpp SWEEP_DS).
+template <int VL, int NP, bool H16, int ND, bool DS = false>
 __device__ __forceinline__ void sweep_step2n(const uint32_t (&Lp)[ND][NP], const uint32_t (&mmp)[ND],
                                              const uint32_t (&C)[ND][NP], uint32_t P1p, uint32_t P2p, uint32_t eL,
                                              uint32_t eR, uint32_t (&Ln)[ND][NP], uint32_t (&mn)[ND])
 {
+    static_assert(!DS || H16, "deferred subtraction: census f16 form only");
     constexpr uint32_t EDGE = H16 ? 0x7BFF7BFFu : (kBig | (kBig << 16));
     uint32_t lm[ND], lq[ND], dl[ND], a1[ND];
 #pragma unroll
@@ -320,10 +328,12 @@ __device__ __forceinline__ void sweep_step2n(const uint32_t (&Lp)[ND][NP], const
         for (int k = 0; k < NP; k++)
 #pragma unroll
             for (int n = 0; n < ND; n++) v[n][k] = h2min3(v[n][k], Lp[n][k], dl[n]);
+        if constexpr (!DS) {
 #pragma unroll
-        for (int k = 0; k < NP; k++)
+            for (int k = 0; k < NP; k++)
 #pragma unroll
-            for (int n = 0; n < ND; n++) v[n][k] = h2sub(v[n][k], mmp[n]);
+                for (int n = 0; n < ND; n++) v[n][k] = h2sub(v[n][k], mmp[n]);
+        }
 #pragma unroll
         for (int k = 0; k < NP; k++)
 #pragma unroll

@@ -81,7 +81,7 @@ constexpr bool unit_built()
     if constexpr (NCW == 0) return false;
     else if constexpr (MODE < 3) return true;
     else if constexpr (DPL % 2 != 0 || SWEEP_U32) return false;
-    else if constexpr (MODE == 3) return LineGeo<VL, DPL, NCW, 3>::BUILT;
+    else if constexpr (MODE == 3) return LineGeo<VL, DPL, NCW, 3, (int)sizeof(CT)>::BUILT;
     else return true;
 }
 

@@ -95,6 +95,22 @@ constexpr uint32_t SW_SPIN_LIMIT = 1u << 19;
 #ifndef SWEEP_H16
 #define SWEEP_H16 1
 #endif
+// census (f16 form): deferred subtraction of the previous row's minimum (sm_pk.hpp
+// sweep_step2n DS): the path states run unnormalised, each sum of paths subtracts the input
+// minima once, and every state is renormalised (R - min R) at least every SWEEP_DS_RN rows /
+// line steps, which keeps every value below 2^11: after k steps R <= 62 k + 62 + P2 and the
+// step's largest intermediate adds P1 (P2 <= 193, P1 < P2: k <= 25)
+#ifndef SWEEP_DS
+#define SWEEP_DS 1
+#endif
+#ifndef SWEEP_DS_LINES
+#define SWEEP_DS_LINES 1  // the MODE 3 line waves too (their ring offsets beside the ring)
+#endif
+#ifndef SWEEP_DS_LANE0
+#define SWEEP_DS_LANE0 0
+#endif
+#define SWEEP_DS_RN 16
+static_assert(62 * SWEEP_DS_RN + 62 + 193 + 192 < 2048, "DS renormalisation interval too long for the f16 form");
 // packed row loops: the recurrences that wait on the LDS row (A and B of an own wave, the
 // column sets of a halo wave) issued interleaved (sm_pk.hpp sweep_step2n: no wait states
 // between dependent VOP3P operations)
@@ -254,18 +270,21 @@ constexpr bool sweep_nobar()
 }
 template <int DPL, int MODE>
 constexpr bool sweep_halo_poll() { return sweep_nobar<DPL, MODE>() && SWEEP_HALO_POLL; }
-template <int VL, int DPL, int NCW_, int MODE>
+template <int VL, int DPL, int NCW_, int MODE, int CTB = 1>
 struct LineGeo {
     using G = SweepGeo<VL, DPL, NCW_>;
     static constexpr bool ON = MODE == 3;
+    // census lines with deferred subtraction (SWEEP_DS): each ring cell's E and W offsets (the
+    // lines' input minima at that column) beside the ring, 8 bytes per own column and row
+    static constexpr bool DSO = CTB == 1 && SWEEP_DS && SWEEP_DS_LINES && SWEEP_H16 && VL != 8;  // (8-lane lines: spills)
     static constexpr bool HPOLL = sweep_halo_poll<DPL, MODE>();
     static constexpr int POLLER = HPOLL ? 0 : 1;  // poller waves
     // at most 16 waves per workgroup (1024 threads): compute waves + poller + lines
     static constexpr int NLW = !ON ? 0 : (SWEEP_NLW < 16 - POLLER - NCW_ ? SWEEP_NLW : 16 - POLLER - NCW_);
     static constexpr int RPW = G::LPW / 2;  // rows per line wave and batch
     // LDS besides the ring: lv, lmin, the counters, a margin
-    static constexpr int BASE = 8 * G::COLS * G::D + 16 * G::COLS + 4 * NCW_ + 4 * 16 + 512;
-    static constexpr int ROWB = G::CW * G::D * 2;  // ring row: u16 E + W sums of the own columns
+    static constexpr int BASE = 8 * G::COLS * G::D + 16 * G::COLS + 4 * NCW_ + 4 * 16 + 512 + 4 * G::D;  // (+ ring padding)
+    static constexpr int ROWB = G::CW * G::D * 2 + (DSO ? G::CW * 8 : 0);  // ring row: u16 E + W sums of the own columns (+ offsets)
     static constexpr int FIT = (kMaxLds - BASE) / ROWB;
     static constexpr int LEAD0 = SWEEP_LEAD_BLOCKS * G::HB;
     static constexpr int LEAD = LEAD0 + RPW <= FIT ? LEAD0 : (FIT > RPW ? (FIT - RPW) / RPW * RPW : 0);
@@ -459,7 +478,7 @@ template <int VL, int DPL, typename CT, int MODE, int NCW_ = kNarrowNcw>
 __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_sweep(SweepArgs a)
 {
     using G = SweepGeo<VL, DPL, NCW_>;
-    using LG = LineGeo<VL, DPL, NCW_, MODE>;
+    using LG = LineGeo<VL, DPL, NCW_, MODE, (int)sizeof(CT)>;
     constexpr bool UP = MODE == 2 || MODE == 4;
     constexpr bool WTA = MODE == 1 || MODE == 2 || MODE == 4;
     constexpr bool EWIN = MODE == 1 || MODE == 2;   // E / W path volumes read (k_ew)
@@ -500,7 +519,13 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
     __shared__ uint32_t rowcnt[NCW];
     // MODE 3: E + W of the own columns for LR rows; batches each line wave has completed;
     // rows each own wave has consumed from the ring
-    __shared__ __attribute__((aligned(16))) uint16_t ring[LINES ? LG::LR : 1][LINES ? CW : 1][LINES ? D : 2];
+    // (one D-slice of padding on each side: a line's last step prefetches the column past the
+    // strip, which is never used; the padding keeps that read inside the declared array)
+    constexpr int RING_D = LINES ? D : 2;
+    __shared__ __attribute__((aligned(16))) uint16_t ring_pad[(LINES ? LG::LR : 1) * (LINES ? CW : 1) * RING_D + 2 * RING_D];
+    auto& ring = *reinterpret_cast<uint16_t(*)[LINES ? LG::LR : 1][LINES ? CW : 1][RING_D]>(ring_pad + RING_D);
+    // DS census lines: [ring row][own column][E, W] input minima (the offsets of the ring's sums)
+    __shared__ __attribute__((aligned(8))) uint32_t roff[LINES && LG::DSO ? LG::LR : 1][LINES && LG::DSO ? CW : 1][2];
     __shared__ uint32_t linecnt[LINES ? LG::NLW : 1], conscnt[NCW];
     __shared__ uint32_t pollcnt;  // NOBAR: blocks whose halo snapshot the poller has written
 
@@ -654,8 +679,10 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
             constexpr int NP = DPL / 2;
             constexpr int CB = DPL * (int)sizeof(CT);
             constexpr bool H16 = sizeof(CT) == 1 && SWEEP_H16;
+            constexpr bool DSL = LG::DSO;  // deferred subtraction (census): renormalised at every chunk end
             constexpr uint32_t EDGE2 = H16 ? 0x7BFF7BFFu : (kBig | (kBig << 16));
             constexpr int LPF = LG::template lpf<CT>();  // cost loads in flight per lane (a divisor of CW / 2)
+            static_assert(!DSL || LPF <= SWEEP_DS_RN, "DS lines renormalise once per chunk");
             const int li = wave - NCW - LG::POLLER;
             const int kl = lane / VL, g = lane % VL;
             const int dir = kl & 1, r = kl >> 1;
@@ -733,6 +760,9 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
                 // ring row of y (a row >= H reuses a slot whose row every own wave has consumed
                 // and no later row needs); own column o = h (E) or CW - 1 - h (W) at step w + h
                 uint16_t* rp = &ring[y % LR][dir ? CW - 1 : 0][g * DPL];
+                // (DS) this line's offset slot of own column o: rop + (j - w) * ostep
+                uint32_t* rop = &roff[DSL ? y % LR : 0][DSL && dir ? CW - 1 : 0][DSL ? dir : 0];
+                const int ostep = cs * 2;
                 // boundary states of (y, strip, dir): [0] entering the strip, [1] at its far end
                 const uint32_t so = yl ? ((((uint32_t)y * (uint32_t)a.nwg + (uint32_t)wg) * 2u + (uint32_t)dir) * 2u *
                                               (uint32_t)D + (uint32_t)(g * DPL)) * (uint32_t)sizeof(CT)
@@ -782,9 +812,16 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
                         uint32_t Lq[1][NP], mq[1] = {mm}, Ln[1][NP], mn[1];
 #pragma unroll
                         for (int i = 0; i < NP; i++) Lq[0][i] = Lp[i];
-                        sweep_step2n<VL, NP, H16, 1>(Lq, mq, C, P1p, P2p, eL, eR, Ln, mn);
+                        sweep_step2n<VL, NP, H16, 1, DSL>(Lq, mq, C, P1p, P2p, eL, eR, Ln, mn);
 #pragma unroll
                         for (int i = 0; i < NP; i++) Lp[i] = Ln[0][i];
+                        if constexpr (DSL && RING != 0) {  // the column's value is Lp - (input minimum)
+#if SWEEP_DS_LANE0
+                            if (g == 0) rop[(j - w) * ostep] = mq[0];
+#else
+                            rop[(j - w) * ostep] = mq[0];  // every lane of the line: the same word, no exec mask
+#endif
+                        }
                         mm = mn[0];
                         if constexpr (RING != 0) {
                             uint16_t* p = rp + (j - w) * rstep;
@@ -793,21 +830,40 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
 #pragma unroll
                                 for (int i = 0; i < NP; i++) v[i] = pk_add(old[i], Lp[i]);
                                 lds_put_pk<NP>(p, v);
-                                lds_get_pk<NP>(p + rstep, old);  // the next column (the other line wrote it)
+                                // the next column (the other line wrote it; past the strip's last
+                                // column: the ring's padding, never used)
+                                lds_get_pk<NP>(p + rstep, old);
                             } else {
                                 lds_put_pk<NP>(p, Lp);
+                            }
+                        }
+                        if constexpr (DSL) {
+                            if (k == LPF - 1) {  // chunk end (after the ring write): renormalise
+#pragma unroll
+                                for (int i = 0; i < NP; i++) Lp[i] = pk_sub(Lp[i], mm);
+                                mm = 0;
                             }
                         }
                     }
                 };
                 const int half = CW / 2 / LPF;  // chunks per half strip
+                // boundary states in the min-0 form (state - its minimum: every later output is
+                // invariant to a constant shift of the state, so k_ew_patch compares and
+                // recomputes on this form; DS lines are renormalised at every chunk end already)
+                auto min0 = [&](uint32_t (&v)[NP]) {
+#pragma unroll
+                    for (int i = 0; i < NP; i++) v[i] = DSL ? Lp[i] : pk_sub(Lp[i], mm);
+                };
+                uint32_t sv[NP];
                 for (int c = 0; c < wch; c++) chunk(c * LPF, std::integral_constant<int, 0>{});
-                store_pk<CT, NP>(rs, so, Lp);  // the state entering the strip
+                min0(sv);
+                store_pk<CT, NP>(rs, so, sv);  // the state entering the strip
                 for (int c = 0; c < half; c++) chunk(w + c * LPF, std::integral_constant<int, 1>{});
                 // the first far-half column: the other line wrote it in the last step of the loop above
                 lds_get_pk<NP>(rp + (CW / 2) * rstep, old);
                 for (int c = 0; c < half; c++) chunk(w + (half + c) * LPF, std::integral_constant<int, 2>{});
-                store_pk<CT, NP>(rs, yl ? so + (uint32_t)(D * sizeof(CT)) : kOOB, Lp);  // the far end
+                min0(sv);
+                store_pk<CT, NP>(rs, yl ? so + (uint32_t)(D * sizeof(CT)) : kOOB, sv);  // the far end
                 // the batch's ring rows are complete (LDS only: the state stores need no ordering)
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
                 __hip_atomic_store(&linecnt[li], (uint32_t)(t + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -993,6 +1049,8 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
         // costs saturate in OpenCV's order (normalize's domain keeps L <= 16383)
         constexpr bool SAT = sizeof(CT) == 2;
         constexpr bool H16 = !SAT && SWEEP_H16;  // census: f16 form of the recurrence and the sums
+        constexpr bool DS = H16 && SWEEP_DS;     // deferred subtraction (SWEEP_DS)
+        static_assert(!DS || SWEEP_STEPN, "deferred subtraction runs the stage-wise steps");
         auto run = [&](auto role_c) {
             constexpr int ROLE = decltype(role_c)::value;  // 0 left halo (A), 1 own (A, B, V), 2 right halo (B)
             constexpr bool HAS_A = ROLE != 2, HAS_B = ROLE != 0, OWN = ROLE == 1;
@@ -1077,7 +1135,7 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
                     if constexpr (SWEEP_LDS_FIRST && MODE == 1) __builtin_amdgcn_sched_barrier(0);
                     uint32_t nV[NP], nA[NS][NP], nB[NS][NP], mnV = 0, mnA[NS], mnB[NS];
                     auto step = [&](const uint32_t(&Lp)[NP], uint32_t m, const uint32_t(&Ch)[NP], uint32_t(&Ln)[NP]) {
-                        return sweep_step2<VL, NP, H16>(Lp, m, Ch, P1p, P2p, eL, eR, Ln);
+                        return sweep_step2<VL, NP, H16, DS>(Lp, m, Ch, P1p, P2p, eL, eR, Ln);
                     };
                     if constexpr (OWN) {
                         if constexpr (SWEEP_STEPN) {  // stage-wise over the words (sweep_step2n)
@@ -1087,7 +1145,7 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
                                 Lp1[0][i] = LVp[i];
                                 C1[0][i] = C[0][i];
                             }
-                            sweep_step2n<VL, NP, H16, 1>(Lp1, m1, C1, P1p, P2p, eL, eR, Ln1, mn1);
+                            sweep_step2n<VL, NP, H16, 1, DS>(Lp1, m1, C1, P1p, P2p, eL, eR, Ln1, mn1);
 #pragma unroll
                             for (int i = 0; i < NP; i++) nV[i] = Ln1[0][i];
                             mnV = mn1[0];
@@ -1106,7 +1164,7 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
                         }
                         m2[0] = mA[0];
                         m2[1] = mB[0];
-                        sweep_step2n<VL, NP, H16, 2>(Lp2, m2, C2, P1p, P2p, eL, eR, Ln2, mn2);
+                        sweep_step2n<VL, NP, H16, 2, DS>(Lp2, m2, C2, P1p, P2p, eL, eR, Ln2, mn2);
 #pragma unroll
                         for (int i = 0; i < NP; i++) {
                             nA[0][i] = Ln2[0][i];
@@ -1129,7 +1187,7 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
                                 mn_in[h] = mB[h];
                             }
                         }
-                        sweep_step2n<VL, NP, H16, NS>(Lpn, mn_in, C, P1p, P2p, eL, eR, Lnn, mnn);
+                        sweep_step2n<VL, NP, H16, NS, DS>(Lpn, mn_in, C, P1p, P2p, eL, eR, Lnn, mnn);
 #pragma unroll
                         for (int h = 0; h < NS; h++) {
 #pragma unroll
@@ -1145,6 +1203,33 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
                         for (int h = 0; h < NS; h++) {
                             if constexpr (HAS_A) mnA[h] = step(LA[h], mA[h], C[h], nA[h]);
                             if constexpr (HAS_B) mnB[h] = step(LB[h], mB[h], C[h], nB[h]);
+                        }
+                    }
+                    // DS: the own wave's outputs are n - (input minimum) per path, summed first and
+                    // corrected once (offs); the state passed on (LDS row, snapshot, next row) is
+                    // renormalised at the block's last row and every SWEEP_DS_RN rows, the outputs'
+                    // offsets then shrink by the removed minima (u16 arithmetic mod 2^16: the
+                    // corrected sums are exact)
+                    [[maybe_unused]] uint32_t offs = 0;
+                    if constexpr (DS) {
+                        if constexpr (OWN) offs = pk_add(pk_add(mVl, mA[0]), mB[0]);
+                        if (j == HB - 1 || j % SWEEP_DS_RN == SWEEP_DS_RN - 1) {
+                            if constexpr (OWN) {
+                                offs = pk_sub(offs, pk_add(pk_add(mnV, mnA[0]), mnB[0]));
+#pragma unroll
+                                for (int i = 0; i < NP; i++) nV[i] = pk_sub(nV[i], mnV);
+                                mnV = 0;
+                            }
+#pragma unroll
+                            for (int h = 0; h < NS; h++) {
+#pragma unroll
+                                for (int i = 0; i < NP; i++) {
+                                    if constexpr (HAS_A) nA[h][i] = pk_sub(nA[h][i], mnA[h]);
+                                    if constexpr (HAS_B) nB[h][i] = pk_sub(nB[h][i], mnB[h]);
+                                }
+                                if constexpr (HAS_A) mnA[h] = 0;
+                                if constexpr (HAS_B) mnB[h] = 0;
+                            }
                         }
                     }
                     // snapshot of the block's last row for the neighbouring strips' halos: the
@@ -1248,6 +1333,10 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
                             for (int i = 0; i < NP; i++) out[i] = pk_add(nV[i], nA[0][i]);
 #pragma unroll
                             for (int i = 0; i < NP; i++) out[i] = pk_add(out[i], nB[0][i]);
+                            if constexpr (DS) {
+#pragma unroll
+                                for (int i = 0; i < NP; i++) out[i] = pk_sub(out[i], offs);
+                            }
                             bstore_n<uint32_t, NP, SWEEP_STREAM_AUX>(rp, boff(e, 2), out);
                         } else if constexpr (MODE == 3) {
                             // + E + W of this row from the line waves' ring (u16 costs: saturating,
@@ -1259,8 +1348,16 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
                             for (int i = 0; i < NP; i++) out[i] = pk_add(out[i], nB[0][i]);
                             if (live) wait_lines(s);
                             lds_get_pk<NP>(&ring[s % LG::LR][(wave - 1) * LPW + kl][g * DPL], ewl);
+                            if constexpr (DS && LG::DSO) {  // + the E and W lines' offsets of this column
+                                const uint2 ro = *reinterpret_cast<const uint2*>(&roff[s % LG::LR][(wave - 1) * LPW + kl][0]);
+                                offs = pk_add(offs, pk_add(ro.x, ro.y));
+                            }
 #pragma unroll
                             for (int i = 0; i < NP; i++) out[i] = SAT ? pk_adds(out[i], ewl[i]) : pk_add(out[i], ewl[i]);
+                            if constexpr (DS) {
+#pragma unroll
+                                for (int i = 0; i < NP; i++) out[i] = pk_sub(out[i], offs);
+                            }
                             bstore_n<uint32_t, NP, SWEEP_STREAM_AUX>(rp, boff(e, 2), out);
                             // the ring row is read (the fence waits for the LDS read): the lines may reuse it
                             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
@@ -1317,6 +1414,10 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
                                 for (int i = 0; i < NP; i++) ew[i] = pk_add(nB[0][i], ew[i]);
 #pragma unroll
                                 for (int i = 0; i < NP; i++) Sp[i] = pk_add(Sp[i], ew[i]);
+                                if constexpr (DS) {
+#pragma unroll
+                                    for (int i = 0; i < NP; i++) Sp[i] = pk_sub(Sp[i], offs);
+                                }
                             }
                             uint32_t key = 0xFFFFFFFFu;
 #pragma unroll

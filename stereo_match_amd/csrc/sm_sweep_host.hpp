@@ -158,11 +158,12 @@ struct EwPatchArgs {
     size_t cost_pair;     // bytes
     uint16_t* part;       // [pair][H][W1][D] u16 partial written by MODE 3
     size_t part_pair;     // bytes
-    const uint8_t* st;    // MODE 3 boundary states [pair][H][nwg][2][2][D] of CT
+    uint8_t* st;          // MODE 3 boundary states [pair][H][nwg][2][2][D] of CT; phase A overwrites the
+                          // s_k slot of a strip whose walk never met with its true far-end state c_k
     size_t st_pair;       // bytes
     int H, W1, nwg, cw, P1, P2;
     const uint32_t* guard;  // the group's give-up flag: nothing to patch when set (the fallback recomputes)
-    uint32_t* fixes;        // [0] strip segments recomputed, [1] of them never met within the strip (atomic)
+    unsigned long long* fixes;  // [0] strip segments recomputed, [1] of them never met within the strip (u64 atomics)
 };
 // chunks of LPW * 8 path positions per row and direction the patch pass handles (its open-strip
 // masks in LDS): strips of a pair it accepts (16-lane lines where D % 32 == 0, else 8-lane)

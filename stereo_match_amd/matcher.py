@@ -111,7 +111,7 @@ class StereoSGBM:
             return disparity
         return out
 
-    def computeFromCost(self, cost, offset: float = 0.0, scale=None):
+    def computeFromCost(self, cost, offset: float = 0.0, scale=1.0):
         """SGM over an external matching-cost volume (mc-cnn).
 
         ``cost``: float32 ``(1, D, H, W)`` or ``(D, H, W)``, d-major — the
@@ -120,14 +120,19 @@ class StereoSGBM:
         right x − (minDisparity + d).  Costs are quantised
         ``rint((c + offset) * scale)`` to [0, 4095] (NaN → 4095), then the
         same paths / WTA / LR / median as :meth:`compute` run (``mode`` picks
-        5 or 8 paths; ``blockSize``/``preFilterCap`` are unused).  ``scale``
-        None (the default) derives the window from the volume's own finite
-        range on the device (offset = -min, scale = 4095 / (max - min)), so
-        nothing is clamped whatever range the volume has; P1 / P2 are in the
-        quantised units either way.  Cells that were clamped or NaN are counted
-        (``_lib.engine().counters()``).  numpy in → int16 numpy out; a torch
-        CUDA float32 tensor in → int16 CUDA tensor (torch's current stream)."""
-        scale = 0.0 if scale is None else float(scale)
+        5 or 8 paths; ``blockSize``/``preFilterCap`` are unused).  The window
+        is explicit by default (``offset`` 0, ``scale`` 1).  ``scale="auto"``
+        (opt-in) derives it per pair on the device from the volume's own finite
+        range (offset = -min, scale = 4095 / (max - min)), so nothing is
+        clamped; P1 / P2 are in the quantised units either way, so under
+        "auto" the smoothing strength follows each frame's own cost range (it
+        differs between the pairs of a batch and along a video, and one large
+        finite outlier compresses every other cost into a few levels): pass a
+        fixed window for consistent smoothing.  Cells that were clamped or NaN
+        are counted (``_lib.engine().counters()``).  numpy in → int16 numpy
+        out; a torch CUDA float32 tensor in → int16 CUDA tensor (torch's
+        current stream)."""
+        scale = _lib.volume_scale(scale)
         prm = self.params()
         prm.cost_kind = _lib.SM_COST_VOLUME
         if _is_torch_cuda(cost):

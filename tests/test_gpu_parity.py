@@ -585,7 +585,7 @@ def test_sweep_strip_widths_agree_on_a_kitti_batch(eng, cost, mode):
     """8 KITTI pairs per call (the bench's launch group): the default sweeps (each
     pass picks narrow or wide strips by its model), narrow (1 << 19) and wide
     (1 << 21) strips forced, and the per-direction engine (4096) return the same
-    maps; pair 0 equals the C oracle."""
+    maps, and every pair of every engine equals the C oracle."""
     import torch
 
     H, W, D = synthetic.CONFIGS["kitti"]
@@ -607,6 +607,7 @@ def test_sweep_strip_widths_agree_on_a_kitti_batch(eng, cost, mode):
         finally:
             eng.set_stream(None)
             eng.set_debug_flags(0)
+    exp = ref_c.compute_many(pairs, p)  # every pair against the oracle
     for flags, o in outs.items():
-        assert np.array_equal(o, outs[4096]), flags
-    assert np.array_equal(outs[0][0], ref_c.compute(pairs[0][0], pairs[0][1], p))
+        for i in range(n):
+            assert np.array_equal(o[i], exp[i]), (flags, i, int(np.sum(o[i] != exp[i])))

@@ -142,7 +142,7 @@ def test_lines_open_strips_carry_the_true_state(eng, name):
 
 def test_lines_match_classic_engine_kitti_batch(eng):
     """8 KITTI census pairs through one launch group: the in-sweep lines and the E/W volume
-    kernel (SM_TUNE_SWEEP_LINES -1) give identical maps, and both equal the oracle."""
+    kernel (SM_TUNE_SWEEP_LINES -1) give identical maps, and every pair equals the oracle."""
     import torch
 
     H, W, D = synthetic.CONFIGS["kitti"]
@@ -166,8 +166,10 @@ def test_lines_match_classic_engine_kitti_batch(eng):
             eng.set_tuning(eng.TUNE_SWEEP_LINES, 0)
         outs.append(out.cpu().numpy())
     assert np.array_equal(outs[0], outs[1])
-    for i in (0, 5):
-        _check(outs[0][i], ls[i], rs[i], p)
+    # every pair against the oracle (not only pairs 0 and 5)
+    exp = ref_c.compute_many(list(zip(ls, rs)), p)
+    for i in range(8):
+        assert np.array_equal(outs[0][i], exp[i]), f"pair {i}: {np.sum(outs[0][i] != exp[i])} px differ"
 
 
 @pytest.mark.parametrize("D,warm", [(192, 0), (192, 2), (64, 0)])
@@ -228,7 +230,7 @@ def test_volume_automatic_window(eng, D, mode):
     assert sc != 1.0 and off > 0  # a real window: the volume has negative costs
     clamped_exp, nan_exp = sgm_np.quantize_counts(vol, prm, off, sc)
     before = eng.counters()
-    out = eng.aggregate_cost_f32(vol, synthetic.to_sm_params(p))  # scale None: automatic
+    out = eng.aggregate_cost_f32(vol, synthetic.to_sm_params(p), scale="auto")  # opt-in automatic window
     after = eng.counters()
     exp = ref_c.compute_volume(vol, p, off, sc)
     assert np.array_equal(out, exp), f"{np.sum(out != exp)} px differ"
@@ -236,6 +238,38 @@ def test_volume_automatic_window(eng, D, mode):
     assert after["volume_clamped"] - before["volume_clamped"] == clamped_exp
     assert clamped_exp == int(np.sum(np.isinf(vol[:, :, prm["minD"] + D:])))
     assert after["volume_nan"] - before["volume_nan"] == nan_exp > 0
+
+
+def test_volume_nan_scale_at_the_c_abi_derives_the_window(eng):
+    """a NaN scale at the C-ABI takes the automatic window (as the header says), not
+    a NaN quantisation; the Python surface refuses NaN outright."""
+    import ctypes
+
+    from oracle import sgm_np
+
+    D, H, W = 32, 23, 160
+    vol = _signed_volume(H, W, D, seed=11)
+    p = synthetic.cost_volume_params(D)
+    prm = sgm_np.normalize_params(dict(p, cost=2))
+    off, sc = sgm_np.volume_window(vol, prm)
+    v = np.ascontiguousarray(vol, np.float32)
+    out = np.empty((H, W), np.int16)
+    rc = eng._lib.sm_aggregate_cost_f32(eng.ctx, v.ctypes.data, D, H, W, ctypes.byref(synthetic.to_sm_params(p)),
+                                        0.0, float("nan"), out.ctypes.data)
+    assert rc == 0
+    assert np.array_equal(out, ref_c.compute_volume(vol, p, off, sc))
+    with pytest.raises(ValueError):
+        eng.aggregate_cost_f32(vol, synthetic.to_sm_params(p), 0.0, float("nan"))
+
+
+def test_volume_default_window_is_explicit(eng):
+    """omitting scale keeps the explicit window (offset 0, scale 1), the round-4
+    default; the automatic window is opt-in."""
+    D, H, W = 32, 21, 150
+    vol = (_signed_volume(H, W, D, seed=12) * np.float32(300)).astype(np.float32)
+    p = synthetic.cost_volume_params(D)
+    out = eng.aggregate_cost_f32(vol, synthetic.to_sm_params(p))
+    assert np.array_equal(out, ref_c.compute_volume(vol, p, 0.0, 1.0))
 
 
 def test_volume_explicit_window_counts_clamped_cells(eng):

@@ -173,3 +173,16 @@ def test_reproject_oracle_known_answer():
     assert np.isinf(p[0, 0, 2])
     pm = reproject_np.reproject_image_to_3d(d, Q, handle_missing=True)
     assert pm[0, 0, 2] == 10000.0 and pm[1, 2, 2] == p[1, 2, 2]
+
+
+def test_volume_scale_argument():
+    """the automatic quantisation window is opt-in ("auto" -> 0 at the C-ABI); NaN and
+    None are refused on the Python surface; numbers pass through."""
+    assert _lib.volume_scale("auto") == 0.0
+    assert _lib.volume_scale(4000) == 4000.0
+    assert _lib.volume_scale(1.0) == 1.0
+    for bad in (float("nan"), None, "automatic"):
+        with pytest.raises(ValueError):
+            _lib.volume_scale(bad)
+    import inspect
+    assert inspect.signature(sm.StereoSGBM.computeFromCost).parameters["scale"].default == 1.0
