@@ -277,13 +277,24 @@ int sm_get_counters(sm_ctx* ctx, long long* sweep_fallbacks);
  *                               sweep (host-side count of the engine's choice);
  *   SM_COUNTER_EW_OPEN          of the EW_REPAIRS segments, those whose recomputed values had
  *                               not met the speculative ones by the strip's far end (the true
- *                               state was carried into the next strip). */
+ *                               state was carried into the next strip);
+ *   SM_COUNTER_BAND_REPAIRS     vertical (S / SE / SW) chains of the row-band engine (5 paths,
+ *                               one or two pairs per launch group) whose speculative state
+ *                               entering a band differed from the true one and that the band
+ *                               patch recomputed;
+ *   SM_COUNTER_BAND_OPEN        of those, chains whose repair walk had not met the speculative
+ *                               trajectory by the band's last row (it continued into the next
+ *                               band);
+ *   SM_COUNTER_BAND_GROUPS      launch groups that ran with row bands (host-side count). */
 #define SM_COUNTER_SWEEP_FALLBACKS 0
 #define SM_COUNTER_EW_REPAIRS 1
 #define SM_COUNTER_VOLUME_CLAMPED 2
 #define SM_COUNTER_VOLUME_NAN 3
 #define SM_COUNTER_LINE_GROUPS 4
 #define SM_COUNTER_EW_OPEN 5
+#define SM_COUNTER_BAND_REPAIRS 6
+#define SM_COUNTER_BAND_OPEN 7
+#define SM_COUNTER_BAND_GROUPS 8
 int sm_get_counter(sm_ctx* ctx, int which, long long* value);
 
 /* Restrict the context's own streams (the default stream and its internal
@@ -382,6 +393,14 @@ int sm_set_debug_flags(sm_ctx* ctx, int flags);
  *   SM_TUNE_SWEEP_LINES the fused-sweep engine's horizontal paths: 0 automatic (inside the
  *                      down sweep wherever that instance is built), 1 the same, -1 the E/W
  *                      volume kernel (k_ew) before / beside the sweeps.
+ *   SM_TUNE_BANDS      row bands of the 5-path lines engine: 0 automatic (enough bands to
+ *                      occupy the CUs at one or two pairs per launch group), 1 none, 2..H that
+ *                      many (speculative vertical paths patched at the band boundaries,
+ *                      exact for any value).
+ *   SM_TUNE_BAND_WARMUP rows each band's vertical paths run above it (0 automatic: 16 census,
+ *                      24 u16 costs; 1..4096).  Any value is exact.
+ *   SM_TUNE_BAND_GUESS 0 the bands start from the zero state; 1 (tests) from a deliberately
+ *                      wrong state inside the domain, so that nearly every chain is repaired.
  * Returns SM_E_ARG for an unknown key or value. */
 #define SM_TUNE_EW_LANES 1
 #define SM_TUNE_SWEEP_NCW 2
@@ -390,6 +409,9 @@ int sm_set_debug_flags(sm_ctx* ctx, int flags);
 #define SM_TUNE_EW_WARMUP 5
 #define SM_TUNE_SWEEP_LINES 6
 #define SM_TUNE_EW_GUESS 7
+#define SM_TUNE_BANDS 8
+#define SM_TUNE_BAND_WARMUP 9
+#define SM_TUNE_BAND_GUESS 10
 int sm_set_tuning(sm_ctx* ctx, int key, int value);
 
 /* Last error text of ctx (or of the calling thread when ctx == NULL). */

@@ -445,7 +445,7 @@ class Engine:
         self._check(self._lib.sm_synchronize(self.ctx))
 
     COUNTERS = ("sweep_fallbacks", "ew_repairs", "volume_clamped", "volume_nan", "line_groups",
-                "ew_open")  # SM_COUNTER_*
+                "ew_open", "band_repairs", "band_open", "band_groups")  # SM_COUNTER_*
 
     def counters(self) -> dict:
         """Counters since the engine was created (include/stereo_match_amd.h SM_COUNTER_*):
@@ -504,6 +504,7 @@ class Engine:
 
     TUNE_EW_LANES, TUNE_SWEEP_NCW, TUNE_EW_WAVES, TUNE_EW_PRIO, TUNE_EW_WARMUP, TUNE_SWEEP_LINES = 1, 2, 3, 4, 5, 6
     TUNE_EW_GUESS = 7
+    TUNE_BANDS, TUNE_BAND_WARMUP, TUNE_BAND_GUESS = 8, 9, 10
 
     def set_tuning(self, key: int, value: int):
         """Launch-shape knob (include/stereo_match_amd.h sm_set_tuning); 0 = automatic."""

@@ -80,6 +80,7 @@ struct BufSet {
     DevBuf census[2], cost, L, raw;
     DevBuf part, key2, pre;  // sweep engine: u16 partial sums, WTA winner records, sub-pixel inputs
     DevBuf st;               // in-sweep E/W lines (MODE 3): the strip segments' boundary states
+    DevBuf vst;              // MODE 3 row bands: the vertical paths' boundary states
     hipEvent_t paths_done = nullptr, wta_done = nullptr;
     bool pending = false;  // wta_done recorded and not yet waited for by stream A
 };
@@ -114,6 +115,8 @@ constexpr int ERR_GROUP0 = 0, ERR_STICKY = 32, ERR_FALLBACKS = 48;
 // cells, and (u64 words at 56, 58) the E/W strip segments the patch pass recomputed and those
 // whose walk never met within the strip (64-bit: a service repairs hundreds of segments per pair)
 constexpr int ERR_VOL_CLAMPED = 52, ERR_VOL_NAN = 54, ERR_EW_REPAIRS = 56, ERR_EW_OPEN = 58;
+// (u64 words at 60, 62) the row bands' vertical chains the band patch repaired / carried on
+constexpr int ERR_BAND_REPAIRS = 60, ERR_BAND_OPEN = 62;
 // timing ablation: no guarded fallback launches after the sweeps
 constexpr int DBG_NO_FALLBACK = (int)0x80000000u;
 // flags only the ablation build (SM_ABLATIONS) accepts: timing switches whose results are
@@ -136,6 +139,7 @@ struct sm_ctx {
     hipEvent_t ev_wls_fork = nullptr, ev_wls_ready = nullptr;
     DevBuf hop, sweep_err;  // sweep engine: strip-boundary granules, device error word
     DevBuf volwin;          // external cost volumes, automatic window: [pair] min/max keys + offset/scale
+
     void* pin = nullptr;    // page-locked host staging of the host-pointer entry points (HostStage)
     size_t pin_n = 0;
     // compute_disparity: the right matcher runs on a twin context (own streams and
@@ -148,6 +152,7 @@ struct sm_ctx {
     hipEvent_t ev_fb_fork = nullptr, ev_fb_join = nullptr;  // sweep engine: fallback beside the LR pass
     const uint32_t* fb_guard = nullptr;  // set while enqueuing a group's guarded per-direction fallback
     hipStream_t wta_override = nullptr;  // stream of the WTA launch when it is not stream_b()
+    const uint32_t* wta_skip = nullptr;  // the WTA row kernel exits when this flag is set (WtaArgs::skip)
     int16_t* wta_dst = nullptr;  // integer WTA index of the current launch group (sm_compute_wta_*), or null
     BufSet set[2];
     int next_set = 0;
@@ -161,7 +166,9 @@ struct sm_ctx {
     int tune_ew_lanes = 0, tune_sweep_ncw = 0, tune_ew_waves = 0, tune_ew_prio = 0;
     int tune_ew_warmup = 0, tune_sweep_lines = 0;  // in-sweep E/W lines: warmup columns, -1 off / 1 on
     int tune_ew_guess = 0;                         // 1: the lines start from a wrong state (tests)
+    int tune_bands = 0, tune_band_warmup = 0, tune_band_guess = 0;  // MODE 3 row bands (SM_TUNE_BANDS ...)
     long long line_groups = 0;  // launch groups run with the in-sweep E/W lines (SM_COUNTER_LINE_GROUPS)
+    long long band_groups = 0;  // of them, with row bands (SM_COUNTER_BAND_GROUPS)
     std::vector<TimedEvent> pending;
     std::vector<hipEvent_t> free_events;
     double stage_ms[SM_NUM_STAGES] = {0};
@@ -598,6 +605,7 @@ int launch_wta_t(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs)
     wa.disp = (int16_t*)bs.raw.p;
     wa.wta = ctx->wta_dst;
     wa.lane8 = n.ndirs == 5;
+    wa.skip = ctx->fb_guard ? nullptr : ctx->wta_skip;
     dim3 grid(g.H, g.G);
     const size_t smem = (size_t)g.W * (ctx->wta_dst ? 10 : 8) + 16;
     if (smem > kRowLds)
@@ -711,6 +719,10 @@ struct SweepJob {
     size_t st_pair = 0;     // bytes
     int ewarm = 0;          // MODE 3: warmup columns of the E/W segments
     int ewguess = 0;        // MODE 3: 1 = a deliberately wrong start state (tests)
+    // MODE 3 row bands (nband > 1: the wide instance)
+    int nband = 1, band_h = 0, vwarm = 0, vguess = 0;
+    uint8_t* vst = nullptr;
+    size_t vst_pair = 0;
 };
 
 // CUs the stream may run on: its CU mask (sm_set_cu_mask), the whole device when unmasked
@@ -848,17 +860,20 @@ bool sweeps_fit(sm_ctx* ctx, const Norm& n, bool hybrid, bool lines = false)
 int sweep_pass(sm_ctx* ctx, const Norm& n, const Geo& g, const SweepJob& j, int mode)
 {
     SweepFit f;
-    if (!sweep_capacity(ctx, n, mode, j.G, f)) {
+    const bool banded = j.nband > 1;
+    if (banded ? !(sweep_fit_variant(ctx, n, mode, 0, f) && f.si.impl == 1) : !sweep_capacity(ctx, n, mode, j.G, f)) {
         if (f.nwg > f.cap)
             return fail(ctx, SM_E_UNSUPPORTED, "sweep: %d strips exceed %d resident workgroups", f.nwg, f.cap);
         return fail(ctx, SM_E_UNSUPPORTED, "sweep: numDisparities %d not built", n.D);
     }
     const smk::SweepInfo& si = f.si;
     const int nwg = f.nwg, cap = f.cap;
-    const int nblk = (g.H + si.hb - 1) / si.hb;
+    const int nb = banded ? j.nband : 1;
+    // halo blocks per strip record: every band's rows (own + warmup) fit
+    const int nblk = banded ? (j.band_h + j.vwarm + si.hb - 1) / si.hb : (g.H + si.hb - 1) / si.hb;
     // ablation / test flag 8192: one pair per sweep launch (exercises the chunked launches)
-    const int per_launch = (ctx->dbg_flags & DBG_SWEEP1) ? 1 : std::max(1, std::min(j.G, cap / nwg));
-    const size_t hop_pair = (size_t)nwg * 2 * nblk * si.ngr;
+    const int per_launch = (ctx->dbg_flags & DBG_SWEEP1) ? 1 : std::max(1, std::min(j.G, cap / (nwg * nb)));
+    const size_t hop_pair = (size_t)nwg * nb * 2 * nblk * si.ngr;
     const size_t hop_bytes = hop_pair * 8 * per_launch;
     if (hop_pair * 8 > smk::kMaxRecords) return fail(ctx, SM_E_UNSUPPORTED, "sweep: boundary buffer too large");
     int rc;
@@ -888,6 +903,13 @@ int sweep_pass(sm_ctx* ctx, const Norm& n, const Geo& g, const SweepJob& j, int 
         a.st_pair = j.st_pair;
         a.ewarm = j.ewarm;
         a.ewguess = j.ewguess;
+        a.nband = nb;
+        a.band_h = j.band_h;
+        a.vwarm = j.vwarm;
+        a.vguess = j.vguess;
+        a.hop_nblk = nblk;
+        a.vst = j.vst ? j.vst + (size_t)p0 * j.vst_pair : nullptr;
+        a.vst_pair = j.vst_pair;
         a.rec = j.key2 ? j.key2 + (size_t)p0 * g.H * g.W : nullptr;
         a.nb = j.pre ? j.pre + (size_t)p0 * g.H * g.W : nullptr;
         a.err = j.err;
@@ -1095,6 +1117,38 @@ int ew_warmup(const sm_ctx* ctx, const Norm& n)
     return elem_bytes(n) == 1 ? 16 : 24;
 }
 
+// largest value one path can take (normalize's domains): a 5-path sum of the banded engine must
+// stay below 2^16, where the band patch's atomic corrections are exact (no saturation)
+long long path_max(const Norm& n)
+{
+    if (n.cost == SM_COST_CENSUS) return 62 + n.P2;
+    if (n.cost == SM_COST_VOLUME) return smk::VOL_CMAX + n.P2;
+    const long long side = 2 * (n.bs / 2) + 1;
+    return side * side * (2 * n.ftzero + (255 >> 2)) + n.P2;
+}
+
+// row bands per pair of a 5-path lines launch group of G pairs (1: none): so many that the
+// strips of every band of the group are co-resident on the device's CUs (KITTI D = 160, one pair:
+// 31 wide strips -> 8 bands of 47 rows), each band at least 24 rows.  SM_TUNE_BANDS forces a count.
+int line_bands(const sm_ctx* ctx, const Norm& n, int H, int G)
+{
+    if (n.ndirs != 5 || ctx->tune_bands == 1 || 5 * path_max(n) > 65535) return 1;
+    SweepFit f;
+    if (!sweep_fit_variant(const_cast<sm_ctx*>(ctx), n, 3, 0, f) || f.si.impl != 1 || f.nwg <= 0) return 1;
+    int nb = ctx->tune_bands >= 2 ? ctx->tune_bands : std::min(f.cap / std::max(1, G * f.nwg), H / 24);
+    nb = std::min(nb, H);
+    if (nb < 2) return 1;
+    const int bh = (H + nb - 1) / nb;
+    return (H + bh - 1) / bh;  // no empty band
+}
+
+// rows each band's vertical paths run before its own rows (speculation warmup; SM_TUNE_BAND_WARMUP)
+int band_warmup(const sm_ctx* ctx, const Norm& n)
+{
+    if (ctx->tune_band_warmup > 0) return ctx->tune_band_warmup;
+    return elem_bytes(n) == 1 ? 16 : 24;
+}
+
 int run_lines(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs, hipStream_t ws, uint32_t* gflag)
 {
     const int G = g.G;
@@ -1109,18 +1163,50 @@ int run_lines(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs, hipStream_t 
     j.part = (uint16_t*)bs.part.p;
     j.part_pair = g.vol * 2;
     SweepFit f;
-    if (!sweep_capacity(ctx, n, 3, G, f)) return fail(ctx, SM_E_UNSUPPORTED, "sweep lines: no instance fits");
+    j.nband = line_bands(ctx, n, g.H, G);
+    if (j.nband > 1 ? !sweep_fit_variant(ctx, n, 3, 0, f) : !sweep_capacity(ctx, n, 3, G, f))
+        return fail(ctx, SM_E_UNSUPPORTED, "sweep lines: no instance fits");
     j.st_pair = ((size_t)g.H * f.nwg * 4 * n.D * et + 255) & ~size_t(255);
     if ((rc = ensure(ctx, bs.st, j.st_pair * G)) != SM_OK) return rc;
     j.st = (uint8_t*)bs.st.p;
     j.ewarm = ew_warmup(ctx, n);
     j.ewguess = ctx->tune_ew_guess;
+    if (j.nband > 1) {
+        j.band_h = (g.H + j.nband - 1) / j.nband;
+        j.vwarm = band_warmup(ctx, n);
+        j.vguess = ctx->tune_band_guess;
+        j.vst_pair = ((size_t)j.nband * 6 * n.width1 * n.D * et + 255) & ~size_t(255);
+        if ((rc = ensure(ctx, bs.vst, j.vst_pair * G)) != SM_OK) return rc;
+        j.vst = (uint8_t*)bs.vst.p;
+        ctx->band_groups++;
+    }
     ctx->line_groups++;
+    const bool fb_side = n.ndirs == 5 && ws == ctx->stream && !(ctx->dbg_flags & DBG_NO_FALLBACK);
     {
         StageTimer t(ctx, ctx->stream, SM_STAGE_PATHS, G);
         {
             StageTimer ts(ctx, ctx->stream, SM_STAGE_SWEEP, G);
             if ((rc = sweep_pass(ctx, n, g, j, 3)) != SM_OK) return rc;
+        }
+        if (fb_side) {
+            // 5 paths: the group flag is final after the sweep, so the guarded per-direction
+            // fallback (two launches that exit at once unless a strip gave up) runs on the side
+            // stream beside the patch passes and the WTA row kernel, which writes nothing when
+            // the flag is set: the fallback's launch latency leaves the critical path
+            if (ctx->dbg_flags & DBG_FORCE_FALLBACK) HIP_TRY(ctx, hipMemsetAsync(gflag, 1, 1, ctx->stream));
+            if ((rc = ensure_event(ctx, ctx->ev_fb_fork)) != SM_OK) return rc;
+            if ((rc = ensure_event(ctx, ctx->ev_fb_join)) != SM_OK) return rc;
+            HIP_TRY(ctx, hipEventRecord(ctx->ev_fb_fork, ctx->stream));
+            HIP_TRY(ctx, hipStreamWaitEvent(ctx->side, ctx->ev_fb_fork, 0));
+            StreamSwap sw(ctx, ctx->side);
+            ctx->wta_override = ctx->side;
+            ctx->fb_guard = gflag;
+            rc = dispatch(ctx, n, g, bs, DISPATCH_PATHS);
+            if (rc == SM_OK) rc = dispatch(ctx, n, g, bs, DISPATCH_WTA);
+            ctx->fb_guard = nullptr;
+            ctx->wta_override = nullptr;
+            if (rc != SM_OK) return rc;
+            HIP_TRY(ctx, hipEventRecord(ctx->ev_fb_join, ctx->side));
         }
         StageTimer th(ctx, ctx->stream, SM_STAGE_HORIZONTAL, G);
         smk::EwPatchArgs pa{};
@@ -1141,6 +1227,27 @@ int run_lines(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs, hipStream_t 
         const hipError_t e = smk::ew_patch_launch(n.D, (int)et, pa, G, ctx->stream);
         if (e == hipErrorInvalidValue) return fail(ctx, SM_E_UNSUPPORTED, "E/W patch: numDisparities %d not built", n.D);
         HIP_TRY(ctx, e);
+        if (j.nband > 1) {  // then the vertical chains at the band boundaries (after: both touch the partial)
+            smk::BandPatchArgs ba{};
+            ba.cost = j.cost;
+            ba.cost_pair = j.cost_pair;
+            ba.part = j.part;
+            ba.part_pair = j.part_pair;
+            ba.vst = j.vst;
+            ba.vst_pair = j.vst_pair;
+
+            ba.H = g.H;
+            ba.W1 = n.width1;
+            ba.nband = j.nband;
+            ba.band_h = j.band_h;
+            ba.P1 = n.P1;
+            ba.P2 = n.P2;
+            ba.guard = gflag;
+            ba.fixes = reinterpret_cast<unsigned long long*>((uint32_t*)ctx->sweep_err.p + ERR_BAND_REPAIRS);
+            const hipError_t eb = smk::band_patch_launch(n.D, (int)et, ba, G, ctx->stream);
+            if (eb == hipErrorInvalidValue) return fail(ctx, SM_E_UNSUPPORTED, "band patch: numDisparities %d not built", n.D);
+            HIP_TRY(ctx, eb);
+        }
     }
     if (ws != ctx->stream) {
         HIP_TRY(ctx, hipEventRecord(bs.paths_done, ctx->stream));
@@ -1166,9 +1273,13 @@ int run_lines(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs, hipStream_t 
     ctx->wta_override = ws;
     {
         StageTimer ts(ctx, ws, SM_STAGE_SWEEP_WTA, G);
+        ctx->wta_skip = fb_side ? gflag : nullptr;
         rc = dispatch(ctx, n, g, bs, DISPATCH_WTA);
+        ctx->wta_skip = nullptr;
     }
-    if (rc == SM_OK && !(ctx->dbg_flags & DBG_NO_FALLBACK)) {
+    if (fb_side) {
+        if (rc == SM_OK) HIP_TRY(ctx, hipStreamWaitEvent(ws, ctx->ev_fb_join, 0));
+    } else if (rc == SM_OK && !(ctx->dbg_flags & DBG_NO_FALLBACK)) {
         if (ctx->dbg_flags & DBG_FORCE_FALLBACK) HIP_TRY(ctx, hipMemsetAsync(gflag, 1, 1, ws));
         ctx->fb_guard = gflag;
         rc = dispatch(ctx, n, g, bs, DISPATCH_PATHS);
@@ -1747,8 +1858,9 @@ int run_pairs(sm_ctx* ctx, const Src& src, int npairs, int H, int W, int stride,
     // the sweeps' parallelism is (strips x pairs): below sweep_min_pairs pairs per launch
     // group the per-direction engine is faster; flag 16384 forces them, and so
     // does SM_TUNE_SWEEP_NCW (a forced instance is measured, never silently replaced)
+    // (5 paths with the in-sweep lines: the row bands fill the CUs instead)
     if (g.sweep && std::min(G, npairs) < sweep_min_pairs(ctx, n) && !(ctx->dbg_flags & DBG_SWEEP8) &&
-        !ctx->tune_sweep_ncw) {
+        !ctx->tune_sweep_ncw && !(g.lines && line_bands(ctx, n, H, std::min(G, npairs)) > 1)) {
         g.sweep = g.lines = false;
         G = group_size(ctx, n, H, npairs, false, false);
     }
@@ -2269,11 +2381,13 @@ void sm_destroy(sm_ctx* ctx)
                       &ctx->volbuf,  &ctx->wls_num, &ctx->wls_den,   &ctx->wls_inter,   &ctx->wls_disp[0], &ctx->wls_w,
                       &ctx->wls_disp[1], &ctx->wls_out, &ctx->sp_parent, &ctx->sp_count,
                       &ctx->rp_in,   &ctx->rp_out,  &ctx->rp_min,    &ctx->bm_pre[0],   &ctx->bm_pre[1],
-                      &ctx->bm_cost, &ctx->hop,     &ctx->sweep_err, &ctx->wls_R,      &ctx->wls_IT};
+                      &ctx->bm_cost, &ctx->hop,     &ctx->sweep_err, &ctx->wls_R,      &ctx->wls_IT,
+                      &ctx->volwin};
     for (DevBuf* b : bufs)
         if (b->p) (void)hipFree(b->p);
     for (auto& bs : ctx->set) {
-        DevBuf* sb[] = {&bs.census[0], &bs.census[1], &bs.cost, &bs.L, &bs.raw, &bs.part, &bs.key2, &bs.pre};
+        DevBuf* sb[] = {&bs.census[0], &bs.census[1], &bs.cost, &bs.L,  &bs.raw,
+                        &bs.part,      &bs.key2,      &bs.pre,  &bs.st, &bs.vst};
         for (DevBuf* b : sb)
             if (b->p) (void)hipFree(b->p);
         if (bs.paths_done) (void)hipEventDestroy(bs.paths_done);
@@ -2580,6 +2694,9 @@ int sm_compute_disparity_batch_device(sm_ctx* ctx, const uint8_t* dL, const uint
         ctx->twin->tune_ew_warmup = ctx->tune_ew_warmup;
         ctx->twin->tune_sweep_lines = ctx->tune_sweep_lines;
         ctx->twin->tune_ew_guess = ctx->tune_ew_guess;
+        ctx->twin->tune_bands = ctx->tune_bands;
+        ctx->twin->tune_band_warmup = ctx->tune_band_warmup;
+        ctx->twin->tune_band_guess = ctx->tune_band_guess;
         if (!ctx->cu_mask.empty() &&
             (rc = sm_set_cu_mask(ctx->twin, ctx->cu_mask.data(), (int)ctx->cu_mask.size())) != SM_OK)
             return fail(ctx, rc, "%s", ctx->twin->err.c_str());
@@ -2913,11 +3030,11 @@ int sm_get_counter(sm_ctx* ctx, int which, long long* value)
 {
     if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
     if (!value) return fail(ctx, SM_E_ARG, "value is NULL");
-    if (which < SM_COUNTER_SWEEP_FALLBACKS || which > SM_COUNTER_EW_OPEN)
+    if (which < SM_COUNTER_SWEEP_FALLBACKS || which > SM_COUNTER_BAND_GROUPS)
         return fail(ctx, SM_E_ARG, "unknown counter %d", which);
     long long v = 0;
-    if (which == SM_COUNTER_LINE_GROUPS) {
-        v = ctx->line_groups;
+    if (which == SM_COUNTER_LINE_GROUPS || which == SM_COUNTER_BAND_GROUPS) {
+        v = which == SM_COUNTER_LINE_GROUPS ? ctx->line_groups : ctx->band_groups;
     } else if (ctx->sweep_err.p) {
         HIP_TRY(ctx, hipSetDevice(ctx->device));
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
@@ -2927,6 +3044,8 @@ int sm_get_counter(sm_ctx* ctx, int which, long long* value)
             const int word = which == SM_COUNTER_VOLUME_CLAMPED ? ERR_VOL_CLAMPED
                              : which == SM_COUNTER_VOLUME_NAN   ? ERR_VOL_NAN
                              : which == SM_COUNTER_EW_OPEN      ? ERR_EW_OPEN
+                             : which == SM_COUNTER_BAND_REPAIRS ? ERR_BAND_REPAIRS
+                             : which == SM_COUNTER_BAND_OPEN    ? ERR_BAND_OPEN
                                                                 : ERR_EW_REPAIRS;
             HIP_TRY(ctx, hipMemcpy(&u, (uint32_t*)ctx->sweep_err.p + word, 8, hipMemcpyDeviceToHost));
             v = (long long)u;
@@ -3045,6 +3164,18 @@ int sm_set_tuning(sm_ctx* ctx, int key, int value)
     case SM_TUNE_SWEEP_LINES:
         if (value < -1 || value > 1) return fail(ctx, SM_E_ARG, "sweep lines %d: -1, 0 or 1", value);
         ctx->tune_sweep_lines = value;
+        break;
+    case SM_TUNE_BANDS:
+        if (value < 0 || value > 65535) return fail(ctx, SM_E_ARG, "row bands %d: 0..65535", value);
+        ctx->tune_bands = value;
+        break;
+    case SM_TUNE_BAND_WARMUP:
+        if (value < 0 || value > 4096) return fail(ctx, SM_E_ARG, "band warmup %d: 0..4096", value);
+        ctx->tune_band_warmup = value;
+        break;
+    case SM_TUNE_BAND_GUESS:
+        if (value < 0 || value > 1) return fail(ctx, SM_E_ARG, "band guess %d: 0 or 1", value);
+        ctx->tune_band_guess = value;
         break;
     default: return fail(ctx, SM_E_ARG, "unknown tuning key %d", key);
     }

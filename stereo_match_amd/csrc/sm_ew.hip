@@ -92,7 +92,38 @@ hipError_t patch_d(int D, const EwPatchArgs& a, int npairs, hipStream_t stream)
     }
 }
 
+template <int VL, int NP, typename CT>
+hipError_t run_band_patch(BandPatchArgs a, int npairs, hipStream_t stream)
+{
+    constexpr int LPW = 64 / VL;
+    a.nbx = (3 * a.W1 + 4 * LPW - 1) / (4 * LPW);  // 4 waves of LPW chains per workgroup
+    if (a.nband < 2) return hipSuccess;
+    hipLaunchKernelGGL((k_band_patch<VL, NP, CT>), dim3(a.nbx, a.nband - 1, npairs), dim3(256), 0, stream, a);
+    return hipGetLastError();
+}
+
+template <typename CT>
+hipError_t band_patch_d(int D, const BandPatchArgs& a, int npairs, hipStream_t stream)
+{
+    switch (D) {  // the lines of k_ew_patch: 16 lanes where D % 32 == 0, else 8
+#define P16(d) \
+    case d: return run_band_patch<16, d / 32, CT>(a, npairs, stream);
+#define P8(d) \
+    case d: return run_band_patch<8, d / 16, CT>(a, npairs, stream);
+        P8(16) P16(32) P8(48) P16(64) P8(80) P16(96) P8(112) P16(128)
+        P8(144) P16(160) P8(176) P16(192) P8(208) P16(224) P8(240) P16(256)
+#undef P16
+#undef P8
+    default: return hipErrorInvalidValue;
+    }
+}
+
 }  // namespace
+
+hipError_t band_patch_launch(int D, int ct_bytes, const BandPatchArgs& a, int npairs, hipStream_t stream)
+{
+    return ct_bytes == 1 ? band_patch_d<uint8_t>(D, a, npairs, stream) : band_patch_d<uint16_t>(D, a, npairs, stream);
+}
 
 hipError_t ew_patch_launch(int D, int ct_bytes, const EwPatchArgs& a, int npairs, hipStream_t stream)
 {

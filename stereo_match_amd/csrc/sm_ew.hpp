@@ -507,4 +507,127 @@ __global__ void __launch_bounds__(256) k_ew_patch(EwPatchArgs a)
     }
 }
 
+// ---- row-band patch (BandPatchArgs): grid (nbx, nband - 1, pairs), 256 threads.
+// Line kl of wave w takes chain id = (blockIdx.x * 4 + w) * LPW + kl of boundary bi = blockIdx.y
+// + 1: direction dir = id / W1 (0 S, 1 SE = +x, 2 SW = -x) entering band bi at column x = id % W1
+// of the row above it, i.e. steps r = 0, 1, ... at column x + dx (r + 1) of row bi * band_h + r.
+// Where the speculative entering state (band bi's warmup) differs from the band above's stored end
+// state, the two trajectories are stepped side by side and (second - first) is added to the
+// partial until they meet — across later band boundaries too, with no hand-off between walks:
+// past a boundary the first trajectory continues as well, and there it is exactly the values that
+// boundary's own walk (or none) left, so the contributions of all walks telescope to
+// (true - speculative) in every band (u32 atomics on u16 pairs: exact whatever their order while
+// no half leaves 0..65535, which the host guarantees).
+template <int VL, int NP, typename CT>
+__global__ void __launch_bounds__(256) k_band_patch(BandPatchArgs a)
+{
+    constexpr int LPW = 64 / VL, DPL = 2 * NP, D = VL * DPL, CB = DPL * (int)sizeof(CT);
+    constexpr bool H16 = sizeof(CT) == 1 && EW_H16;
+    constexpr uint32_t EDGE = H16 ? 0x7BFF7BFFu : (kBig | (kBig << 16));
+    constexpr int RC = 8;  // chain steps whose costs load together
+    if (a.guard && __hip_atomic_load(a.guard, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int g = lane % VL, kl = lane / VL;
+    const int bi = (int)blockIdx.y + 1;
+    const size_t pair = blockIdx.z;
+    const int H = a.H, W1 = a.W1;
+    const int y0 = bi * a.band_h;
+    const int id = ((int)blockIdx.x * 4 + wave) * LPW + kl;
+    const bool on = id < 3 * W1 && y0 < H;
+    const int dir = on ? id / W1 : 0, x = on ? id % W1 : 0;
+    const int dx = dir == 0 ? 0 : dir == 1 ? 1 : -1;
+    // steps inside the image and the domain
+    const int nr = !on ? 0 : dx == 0 ? H - y0 : dx > 0 ? min(H - y0, W1 - 1 - x) : min(H - y0, x);
+    const uint64_t cells = (uint64_t)H * W1 * D;
+    const rsrc_t rc = make_rsrc(a.cost + pair * a.cost_pair, cells * sizeof(CT));
+    const rsrc_t rv = make_rsrc(a.vst + pair * a.vst_pair, a.vst_pair);
+    uint32_t* part = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(a.part) + pair * a.part_pair);
+    const uint32_t P1p = (uint32_t)a.P1 * 0x10001u, P2p = (uint32_t)a.P2 * 0x10001u;
+    const uint32_t eL = g == 0 ? EDGE : 0u, eR = g == VL - 1 ? EDGE : 0u;
+    auto voff = [&](int band, int which, int col) -> uint32_t {
+        return (((((uint32_t)band * 2u + (uint32_t)which) * 3u + (uint32_t)dir) * (uint32_t)W1 + (uint32_t)col) *
+                    (uint32_t)D + (uint32_t)(g * DPL)) * (uint32_t)sizeof(CT);
+    };
+    auto cost_off = [&](int r) -> uint32_t {
+        return r < nr ? (((uint32_t)(y0 + r) * (uint32_t)W1 + (uint32_t)(x + dx * (r + 1))) * (uint32_t)D +
+                         (uint32_t)(g * DPL)) * (uint32_t)sizeof(CT)
+                      : kOOB;
+    };
+    auto line_all = [&](bool ok) -> bool { return group_min<VL>(ok ? 1u : 0u) != 0u; };
+    auto state_min = [&](const uint32_t (&v)[NP]) -> uint32_t {
+        uint32_t m = v[0];
+#pragma unroll
+        for (int i = 1; i < NP; i++) m = pk_min(m, v[i]);
+        m = ::min(m & 0xFFFFu, m >> 16);
+        return group_min<VL>(m) * 0x10001u;
+    };
+    RawBytes<CB> sb, tb, cc[RC];
+    sb.load(rv, on ? voff(bi, 0, x) : kOOB);      // speculative: band bi's warmup
+    tb.load(rv, on ? voff(bi - 1, 1, x) : kOOB);  // the band above's end
+#pragma unroll
+    for (int u = 0; u < RC; u++) cc[u].load(rc, cost_off(u));
+    uint32_t Lq[2][NP], mq[2];
+    unpack_ct_pk<CT, DPL>(sb, Lq[0]);
+    unpack_ct_pk<CT, DPL>(tb, Lq[1]);
+    bool same = true;
+#pragma unroll
+    for (int i = 0; i < NP; i++) same &= Lq[0][i] == Lq[1][i];
+    same = line_all(same);
+    uint32_t nfix = 0, nlong = 0;
+    if (on && !same && nr > 0) {
+        nfix++;
+        mq[0] = state_min(Lq[0]);
+        mq[1] = state_min(Lq[1]);
+        const int rb = min(H, y0 + a.band_h) - y0;  // steps inside band bi
+        bool met = false;
+        int r0 = 0;
+        for (; r0 < nr && !met; r0 += RC) {
+            if (r0 > 0) {
+#pragma unroll
+                for (int u = 0; u < RC; u++) cc[u].load(rc, cost_off(r0 + u));
+            }
+#pragma unroll
+            for (int u = 0; u < RC; u++) {  // (no break: the loop must unroll)
+                const int r = r0 + u;
+                if (r >= nr || met) continue;
+                uint32_t C2[2][NP], Ln[2][NP], mn[2];
+                unpack_ct_pk<CT, DPL>(cc[u], C2[0]);
+#pragma unroll
+                for (int q = 0; q < NP; q++) C2[1][q] = C2[0][q];
+                sweep_step2n<VL, NP, H16, 2>(Lq, mq, C2, P1p, P2p, eL, eR, Ln, mn);
+                bool eq = true;
+#pragma unroll
+                for (int q = 0; q < NP; q++) eq &= Ln[0][q] == Ln[1][q];
+                if (line_all(eq)) {
+                    met = true;
+                    continue;
+                }
+                nlong |= r >= rb ? 1u : 0u;  // (a walk that crossed the next boundary)
+                // (second - first) per u16 half as one signed 32-bit addend
+                const size_t w0 = (((size_t)(y0 + r) * (size_t)W1 + (size_t)(x + dx * (r + 1))) * D + g * DPL) / 2;
+#pragma unroll
+                for (int q = 0; q < NP; q++) {
+                    const int lo = (int)(Ln[1][q] & 0xFFFFu) - (int)(Ln[0][q] & 0xFFFFu);
+                    const int hi = (int)(Ln[1][q] >> 16) - (int)(Ln[0][q] >> 16);
+                    const uint32_t add = (uint32_t)(hi * 65536 + lo);
+                    if (add) __hip_atomic_fetch_add(part + w0 + q, add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+#pragma unroll
+                for (int q = 0; q < NP; q++) {
+                    Lq[0][q] = Ln[0][q];
+                    Lq[1][q] = Ln[1][q];
+                }
+                mq[0] = mn[0];
+                mq[1] = mn[1];
+            }
+        }
+    }
+    if (a.fixes) {
+        nfix = group_sum_u32_wave(g == 0 ? nfix : 0u);
+        nlong = group_sum_u32_wave(g == 0 ? nlong : 0u);
+        if (lane == 0 && nfix) atomicAdd(a.fixes, (unsigned long long)nfix);
+        if (lane == 0 && nlong) atomicAdd(a.fixes + 1, (unsigned long long)nlong);
+    }
+}
+
 }  // namespace smk

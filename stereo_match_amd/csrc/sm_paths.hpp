@@ -510,6 +510,9 @@ struct WtaArgs {
     const uint32_t* guard;
     uint32_t* fallbacks;
     int npairs;
+    // (not the fallback) the group's give-up flag: set, the row kernel writes nothing (the guarded
+    // fallback, running beside it on another stream, writes the maps); null: always run
+    const uint32_t* skip;
 };
 
 // The row's columns from u16 sums (the MODE 3 lines' patched partial with every path, or the
@@ -795,6 +798,7 @@ __global__ void __launch_bounds__(NT) k_wta(WtaArgs a)
             __syncthreads();  // the next row reuses the shared row buffers
         }
     } else {
+        if (a.skip && __hip_atomic_load(a.skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;
         wta_row<DPL, LT, NT, PART_ONLY>(a, blockIdx.x, blockIdx.y, smem);
     }
 }

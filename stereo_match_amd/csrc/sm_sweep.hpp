@@ -529,23 +529,49 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
     __shared__ uint32_t linecnt[LINES ? LG::NLW : 1], conscnt[NCW];
     __shared__ uint32_t pollcnt;  // NOBAR: blocks whose halo snapshot the poller has written
 
-    for (int i = threadIdx.x; i < 2 * 2 * COLS * D / 2; i += NTH)
-        reinterpret_cast<uint32_t*>(&lv[0][0][0][0])[i] = 0;
-    for (int i = threadIdx.x; i < 2 * 2 * COLS; i += NTH) (&lmin[0][0][0])[i] = 0;
+    // row band of this workgroup (MODE 3 with a.nband > 1: blockIdx.x = band * nwg + strip)
+    const int nband = LINES && a.nband > 1 ? a.nband : 1;
+    const int band = nband > 1 ? (int)blockIdx.x / a.nwg : 0;
+    const int wg = (int)blockIdx.x - band * a.nwg, pair = blockIdx.y;
+    const int H = a.H, W1 = a.W1;
+    // rows: own [y0b, y1b), computed from ys (vertical warmup rows above the band: the zero state,
+    // or the test's wrong state, enters at ys); step s is row ys + s (down sweeps), s < nrow
+    const int y0b = nband > 1 ? band * a.band_h : 0;
+    const int y1b = nband > 1 ? min(H, y0b + a.band_h) : H;
+    const int ys = band > 0 ? max(0, y0b - a.vwarm) : 0;
+    const int nrow = y1b - ys, wrows = y0b - ys;  // steps, warmup steps (wave-uniform)
+    const int nblk = (nrow + HB - 1) / HB;
+    const int nblk_rec = nband > 1 ? a.hop_nblk : nblk;  // record stride of the hop buffer
+    const bool vguess = a.vguess && band > 0;  // tests: a wrong entering state
+    // the wrong state of a column slot inside the domain: (d % 5) + 3 (slot & 1), minimum 3 (slot & 1)
+    auto in_domain_slot = [&](int q) { const int x = wg * CW + (q - 1) - HW; return x >= 0 && x < W1; };
+
+    for (int i = threadIdx.x; i < 2 * 2 * COLS * D / 2; i += NTH) {
+        uint32_t v = 0;
+        if (vguess) {
+            const int q = (i / (D / 2)) % COLS, d0 = 2 * (i % (D / 2));
+            if (in_domain_slot(q)) v = (uint32_t)(d0 % 5 + 3 * (q & 1)) | ((uint32_t)((d0 + 1) % 5 + 3 * (q & 1)) << 16);
+        }
+        reinterpret_cast<uint32_t*>(&lv[0][0][0][0])[i] = v;
+    }
+    for (int i = threadIdx.x; i < 2 * 2 * COLS; i += NTH) {
+        const int q = i % COLS;
+        (&lmin[0][0][0])[i] = vguess && in_domain_slot(q) ? (uint32_t)(3 * (q & 1)) * 0x10001u : 0u;
+    }
     for (int i = threadIdx.x; i < NCW; i += NTH) rowcnt[i] = conscnt[i] = 0;
     if (threadIdx.x == 0) pollcnt = 0;
+
     if constexpr (LINES)
         for (int i = threadIdx.x; i < LG::NLW; i += NTH) linecnt[i] = 0;
     __syncthreads();
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int wg = blockIdx.x, pair = blockIdx.y;
-    const int H = a.H, W1 = a.W1;
-    const int nblk = (H + HB - 1) / HB;
     const bool has_left = wg > 0, has_right = wg + 1 < a.nwg;
     const uint32_t tag0 = a.epoch << 16;
     unsigned long long* hopp = a.hop + (size_t)pair * a.hop_pair;
-    auto gbase = [&](int strip, int dir, int b) -> size_t { return ((size_t)(strip * 2 + dir) * nblk + b) * SNG; };
+    auto gbase = [&](int strip, int dir, int b) -> size_t {
+        return ((size_t)((band * a.nwg + strip) * 2 + dir) * nblk_rec + b) * SNG;
+    };
 
     if (!HPOLL && wave == NCW) {
         // ---- poller: halo snapshots of the neighbouring strips, once per block.  Granule
@@ -746,22 +772,23 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
             const int jhi = min(nsteps, dir ? c0 + 1 : W1 - c0);
             const int cstep = cs * D * (int)sizeof(CT);  // byte step of the cost offset
             const int rstep = cs * D;                     // u16 step of the ring pointer (own column o)
+            // batch t: the band's own rows u0 .. u0 + RPW - 1 (row y0b + u), ring row u % LR
             for (int t = 0;; t++) {
-                const int y0 = (t * NLW + li) * RPW;
-                if (y0 >= H) break;
-                barriers_to(y0);
-                wait_cons(y0 + RPW - LR);
-                const int y = y0 + r;
-                const bool yl = y < H;
+                const int u0 = (t * NLW + li) * RPW;
+                if (u0 >= y1b - y0b) break;
+                barriers_to(u0);
+                wait_cons(u0 + RPW - LR);
+                const int y = y0b + u0 + r;
+                const bool yl = y < y1b;
                 const uint32_t jspan = yl && jhi > jlo ? (uint32_t)(jhi - jlo) : 0u;
                 // byte offset of step 0's cost slice (wraps for columns left of 0; never used there)
                 const uint32_t coff = (((uint32_t)y * (uint32_t)W1 + (uint32_t)c0) * (uint32_t)D + (uint32_t)(g * DPL)) *
                                       (uint32_t)sizeof(CT);
                 // ring row of y (a row >= H reuses a slot whose row every own wave has consumed
                 // and no later row needs); own column o = h (E) or CW - 1 - h (W) at step w + h
-                uint16_t* rp = &ring[y % LR][dir ? CW - 1 : 0][g * DPL];
+                uint16_t* rp = &ring[(u0 + r) % LR][dir ? CW - 1 : 0][g * DPL];
                 // (DS) this line's offset slot of own column o: rop + (j - w) * ostep
-                uint32_t* rop = &roff[DSL ? y % LR : 0][DSL && dir ? CW - 1 : 0][DSL ? dir : 0];
+                uint32_t* rop = &roff[DSL ? (u0 + r) % LR : 0][DSL && dir ? CW - 1 : 0][DSL ? dir : 0];
                 const int ostep = cs * 2;
                 // boundary states of (y, strip, dir): [0] entering the strip, [1] at its far end
                 const uint32_t so = yl ? ((((uint32_t)y * (uint32_t)a.nwg + (uint32_t)wg) * 2u + (uint32_t)dir) * 2u *
@@ -1063,16 +1090,16 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
             };
             RawBytes<CB> rcs[PF][NS];
             auto issue_r = [&](int k, int s) {
-                const int yy = UP ? H - 1 - s : s;
+                const int yy = UP ? H - 1 - s : ys + s;
 #pragma unroll
                 for (int h = 0; h < NS; h++)
-                    rcs[k][h].template load<WTA ? SWEEP_COST_AUX : 0>(rc, boff(s < H ? cell_h(h, yy) : NONE, sizeof(CT)));
+                    rcs[k][h].template load<WTA ? SWEEP_COST_AUX : 0>(rc, boff(s < nrow ? cell_h(h, yy) : NONE, sizeof(CT)));
                 if constexpr (OWN && EWIN) {
-                    const uint32_t en = s < H ? cell(yy) : NONE;
+                    const uint32_t en = s < nrow ? cell(yy) : NONE;
                     re_[k].template load<SWEEP_STREAM_AUX>(re, boff(en, sizeof(CT)));
                     rw_[k].template load<SWEEP_STREAM_AUX>(rw, boff(en, sizeof(CT)));
                 }
-                if constexpr (OWN && PARTR) rp_[k].template load<SWEEP_STREAM_AUX>(rp, boff(s < H ? cell(yy) : NONE, 2));
+                if constexpr (OWN && PARTR) rp_[k].template load<SWEEP_STREAM_AUX>(rp, boff(s < nrow ? cell(yy) : NONE, 2));
             };
 #pragma unroll
             for (int k = 0; k < PF; k++) issue_r(k, k);
@@ -1080,6 +1107,38 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
 #pragma unroll
             for (int i = 0; i < NP; i++) LVp[i] = 0;
             uint32_t mVl = 0;
+            if (vguess && OWN && active) {  // (tests) the wrong entering state of the LDS rows, slot c + 1
+                const uint32_t o = (uint32_t)(3 * ((c + 1) & 1));
+#pragma unroll
+                for (int i = 0; i < NP; i++) {
+                    const int d0 = g * DPL + 2 * i;
+                    LVp[i] = ((uint32_t)(d0 % 5) + o) | (((uint32_t)((d0 + 1) % 5) + o) << 16);
+                }
+                mVl = o * 0x10001u;
+            }
+            // MODE 3 with row bands: the own columns' S / SE / SW states (min-0 form) at the row
+            // above the band (which 0, speculative) and at the band's last row (which 1)
+            auto vstore = [&](int which, const uint32_t (&sV)[NP], uint32_t mV_, const uint32_t (&sA)[NP], uint32_t mA_,
+                              const uint32_t (&sB)[NP], uint32_t mB_) {
+                if constexpr (LINES && OWN) {
+                    const rsrc_t rv = make_rsrc(a.vst + (size_t)pair * a.vst_pair, a.vst_pair);
+                    auto off = [&](int dir) -> uint32_t {
+                        return active ? (((((uint32_t)band * 2u + (uint32_t)which) * 3u + (uint32_t)dir) * (uint32_t)W1 +
+                                          (uint32_t)x1) * (uint32_t)D + (uint32_t)(g * DPL)) * (uint32_t)sizeof(CT)
+                                      : kOOB;
+                    };
+                    uint32_t v[NP];
+#pragma unroll
+                    for (int i = 0; i < NP; i++) v[i] = pk_sub(sV[i], mV_);
+                    store_pk<CT, NP>(rv, off(0), v);
+#pragma unroll
+                    for (int i = 0; i < NP; i++) v[i] = pk_sub(sA[i], mA_);
+                    store_pk<CT, NP>(rv, off(1), v);
+#pragma unroll
+                    for (int i = 0; i < NP; i++) v[i] = pk_sub(sB[i], mB_);
+                    store_pk<CT, NP>(rv, off(2), v);
+                }
+            };
             // d + 1 of each packed half of this lane (uniqueness window test)
             uint32_t dpk[NP];
 #pragma unroll
@@ -1091,8 +1150,8 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
                     const int k = j % PF;
                     const int s = b * HB + j;
                     if constexpr (SWEEP_DYNPRIO && OWN) __builtin_amdgcn_s_setprio(PRIO_HI);
-                    const bool live = s < H;
-                    const int y = UP ? H - 1 - s : s;
+                    const bool live = s < nrow;
+                    const int y = UP ? H - 1 - s : ys + s;
                     const int rb = (s + 1) & 1, wb = s & 1;
                     const uint32_t e = live ? cell(y) : NONE;
                     uint32_t C[NS][NP], Ein[NP], Win[NP], Pin[NP];
@@ -1232,6 +1291,10 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
                             }
                         }
                     }
+                    if constexpr (LINES && OWN) {  // row bands: the vertical paths' boundary states
+                        if (nband > 1 && (s == wrows - 1 || (s == nrow - 1 && band + 1 < nband)))
+                            vstore(s == wrows - 1 ? 0 : 1, nV, mnV, nA[0], mnA[0], nB[0], mnB[0]);
+                    }
                     // snapshot of the block's last row for the neighbouring strips' halos: the
                     // strip's HM boundary own waves on each side (before the block-end barrier
                     // with SWEEP_EARLY_XCHG, so no wave of the strip waits for the others first)
@@ -1339,6 +1402,8 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
                             }
                             bstore_n<uint32_t, NP, SWEEP_STREAM_AUX>(rp, boff(e, 2), out);
                         } else if constexpr (MODE == 3) {
+                          const int u = s - wrows;  // the band's own row index (< 0: a vertical warmup row)
+                          if (u >= 0) {
                             // + E + W of this row from the line waves' ring (u16 costs: saturating,
                             // the WTA clamps at 32767 anyway; three paths alone stay below 2^16)
                             uint32_t out[NP], ewl[NP];
@@ -1346,10 +1411,10 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
                             for (int i = 0; i < NP; i++) out[i] = pk_add(nV[i], nA[0][i]);
 #pragma unroll
                             for (int i = 0; i < NP; i++) out[i] = pk_add(out[i], nB[0][i]);
-                            if (live) wait_lines(s);
-                            lds_get_pk<NP>(&ring[s % LG::LR][(wave - 1) * LPW + kl][g * DPL], ewl);
+                            if (live) wait_lines(u);
+                            lds_get_pk<NP>(&ring[u % LG::LR][(wave - 1) * LPW + kl][g * DPL], ewl);
                             if constexpr (DS && LG::DSO) {  // + the E and W lines' offsets of this column
-                                const uint2 ro = *reinterpret_cast<const uint2*>(&roff[s % LG::LR][(wave - 1) * LPW + kl][0]);
+                                const uint2 ro = *reinterpret_cast<const uint2*>(&roff[u % LG::LR][(wave - 1) * LPW + kl][0]);
                                 offs = pk_add(offs, pk_add(ro.x, ro.y));
                             }
 #pragma unroll
@@ -1361,8 +1426,9 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
                             bstore_n<uint32_t, NP, SWEEP_STREAM_AUX>(rp, boff(e, 2), out);
                             // the ring row is read (the fence waits for the LDS read): the lines may reuse it
                             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-                            __hip_atomic_store(&conscnt[wave], (uint32_t)(s + 1), __ATOMIC_RELAXED,
+                            __hip_atomic_store(&conscnt[wave], (uint32_t)(u + 1), __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_WORKGROUP);
+                          }
                         } else {
                             uint32_t Sp[NP], ew[NP];
                             // a padded cost volume (u16 costs only): its pad planes d >= Dv take

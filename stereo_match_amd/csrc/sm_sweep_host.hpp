@@ -41,6 +41,17 @@ struct SweepArgs {
     size_t st_pair;  // bytes
     int ewarm;
     int ewguess;  // 0: the zero state; 1 (tests): a deliberately wrong start state, every segment repaired
+    // MODE 3 row bands (one or two pairs per call: DESIGN.md §4.5): workgroup blockIdx.x =
+    // band * nwg + strip; band b owns rows [b * band_h, (b + 1) * band_h) and starts vwarm rows
+    // above them from the zero state (a speculation: k_band_patch repairs the vertical paths
+    // where it did not meet the true state).  The own columns' S / SE / SW states at the row
+    // above the band (speculative) and at its last row go to
+    // vst[pair][band][0 / 1][3][W1][D] (CT, min-0 form).  nband <= 1: one band of all rows.
+    int nband, band_h, vwarm;
+    int vguess;    // tests: bands > 0 start from a deliberately wrong state inside the domain
+    int hop_nblk;  // halo blocks per strip record in the hop buffer (>= every band's block count)
+    uint8_t* vst;
+    size_t vst_pair;  // bytes
 };
 
 
@@ -165,6 +176,26 @@ struct EwPatchArgs {
     const uint32_t* guard;  // the group's give-up flag: nothing to patch when set (the fallback recomputes)
     unsigned long long* fixes;  // [0] strip segments recomputed, [1] of them never met within the strip (u64 atomics)
 };
+// Vertical patch after a banded MODE 3 sweep (sm_ew.hpp k_band_patch): each
+// column's S / SE / SW state entering a band (speculative, from the band's warmup rows) is checked
+// against the band above's stored end state; where they differ both trajectories are stepped down
+// the chain and (second - first) added to the partial until they meet, across later boundaries
+// too (the contributions telescope to true - speculative; no hand-off between walks).
+struct BandPatchArgs {
+    const uint8_t* cost;  // [pair][H][W1][D] of CT
+    size_t cost_pair;     // bytes
+    uint16_t* part;       // [pair][H][W1][D] u16 partial (u32 atomics on u16 pairs: exact while no
+                          // cell saturates, which the host guarantees)
+    size_t part_pair;     // bytes
+    const uint8_t* vst;   // [pair][band][2][3][W1][D] of CT (SweepArgs::vst), min-0 form
+    size_t vst_pair;      // bytes
+    int H, W1, nband, band_h, P1, P2;
+    int nbx;              // workgroups per boundary (blockIdx.x)
+    const uint32_t* guard;  // the group's give-up flag: nothing to patch when set
+    unsigned long long* fixes;  // [0] chains repaired, [1] of them still apart past the next boundary (u64 atomics)
+};
+hipError_t band_patch_launch(int D, int ct_bytes, const BandPatchArgs& a, int npairs, hipStream_t stream);
+
 // chunks of LPW * 8 path positions per row and direction the patch pass handles (its open-strip
 // masks in LDS): strips of a pair it accepts (16-lane lines where D % 32 == 0, else 8-lane)
 constexpr int kPatchMaxChunks = 8;

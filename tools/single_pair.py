@@ -2,7 +2,8 @@
 stereo_vision.py:178-182 runs it): stage breakdown of sm_compute_disparity at
 settings.ini values (D=160) for each engine flag set.
     python tools/single_pair.py [--flags 0,4096] [--calls 20] [--runs "0/ew=16;16384/ncw=5"]
-A run is debug flags, then /knob=value items (ew: SM_TUNE_EW_LANES, ncw: SM_TUNE_SWEEP_NCW);
+A run is debug flags, then /knob=value items (ew: SM_TUNE_EW_LANES, ncw: SM_TUNE_SWEEP_NCW,
+bands: SM_TUNE_BANDS, bw: SM_TUNE_BAND_WARMUP);
 --runs replaces --flags."""
 import argparse
 import json
@@ -37,7 +38,7 @@ def main():
     wp = wf.params(H, W)
     e = _lib.Engine(0)
     ref = None
-    knobs = {"ew": e.TUNE_EW_LANES, "ncw": e.TUNE_SWEEP_NCW}
+    knobs = {"ew": e.TUNE_EW_LANES, "ncw": e.TUNE_SWEEP_NCW, "bands": e.TUNE_BANDS, "bw": e.TUNE_BAND_WARMUP}
     runs = args.runs.split(";") if args.runs else args.flags.split(",")
     for run in runs:
         parts = run.split("/")
@@ -52,6 +53,7 @@ def main():
         same = bool(np.array_equal(d, ref[0]) and np.array_equal(fl, ref[1]))
         e.set_timing(True)
         e.reset_timing()
+        c0 = e.counters()
         ts = []
         for _ in range(args.calls):
             t0 = time.perf_counter()
@@ -59,7 +61,9 @@ def main():
             ts.append(time.perf_counter() - t0)
         st = e.timing()
         e.set_timing(False)
+        c1 = e.counters()
         print(json.dumps({"run": run, "same_as_first": same, "ms_per_call": round(float(np.median(ts)) * 1e3, 3),
+                          "counters_per_call": {k: (c1[k] - c0[k]) / args.calls for k in c1 if c1[k] != c0[k]},
                           "stage_us_per_call": {k: round(v[0] * 1e3 / args.calls, 1) for k, v in st.items() if v[0] > 0}}))
 
 
