@@ -401,6 +401,11 @@ int sm_set_debug_flags(sm_ctx* ctx, int flags);
  *                      24 u16 costs; 1..4096).  Any value is exact.
  *   SM_TUNE_BAND_GUESS 0 the bands start from the zero state; 1 (tests) from a deliberately
  *                      wrong state inside the domain, so that nearly every chain is repaired.
+ *   SM_TUNE_COST_WGS   workgroups the SGBM cost kernel aims for per launch (0 automatic:
+ *                      2048; its row bands are sized from it).
+ *   SM_TUNE_LR_STAGGER sm_compute_disparity*: 0 automatic / 1 the left matcher starts on a
+ *                      second stream once the right one's down sweep is done (overlapping its
+ *                      patch passes and WTA); -1 the matchers strictly one after the other.
  * Returns SM_E_ARG for an unknown key or value. */
 #define SM_TUNE_EW_LANES 1
 #define SM_TUNE_SWEEP_NCW 2
@@ -412,6 +417,8 @@ int sm_set_debug_flags(sm_ctx* ctx, int flags);
 #define SM_TUNE_BANDS 8
 #define SM_TUNE_BAND_WARMUP 9
 #define SM_TUNE_BAND_GUESS 10
+#define SM_TUNE_COST_WGS 11
+#define SM_TUNE_LR_STAGGER 12
 int sm_set_tuning(sm_ctx* ctx, int key, int value);
 
 /* Last error text of ctx (or of the calling thread when ctx == NULL). */

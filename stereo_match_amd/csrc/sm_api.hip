@@ -136,6 +136,13 @@ struct sm_ctx {
     DevBuf wls_num, wls_den, wls_inter, wls_w, wls_disp[2], wls_out;  // WLS scratch
     DevBuf wls_R, wls_IT;         // WLS: Thomas pivots / elimination factors of every pass
     hipStream_t wls_stream = nullptr;  // compute_disparity: WLS weights + pivots beside the matchers
+    hipStream_t lr_stream = nullptr;   // compute_disparity: the left matcher, staggered behind the right one
+    hipEvent_t ev_stagger = nullptr;
+    // (set by the caller for one call) recorded on the stream right after a MODE 3 down sweep;
+    // sweep_done_hit tells the caller it was
+    hipEvent_t sweep_done_ev = nullptr;
+    bool sweep_done_hit = false;
+    int tune_lr_stagger = 0;  // SM_TUNE_LR_STAGGER: 0 automatic (on), -1 off
     hipEvent_t ev_wls_fork = nullptr, ev_wls_ready = nullptr;
     DevBuf hop, sweep_err;  // sweep engine: strip-boundary granules, device error word
     DevBuf volwin;          // external cost volumes, automatic window: [pair] min/max keys + offset/scale
@@ -167,6 +174,7 @@ struct sm_ctx {
     int tune_ew_warmup = 0, tune_sweep_lines = 0;  // in-sweep E/W lines: warmup columns, -1 off / 1 on
     int tune_ew_guess = 0;                         // 1: the lines start from a wrong state (tests)
     int tune_bands = 0, tune_band_warmup = 0, tune_band_guess = 0;  // MODE 3 row bands (SM_TUNE_BANDS ...)
+    int tune_cost_wgs = 0;  // k_sgbm_cost2 workgroups a launch aims for (SM_TUNE_COST_WGS; 0: SGBM_COST2_WGS)
     long long line_groups = 0;  // launch groups run with the in-sweep E/W lines (SM_COUNTER_LINE_GROUPS)
     long long band_groups = 0;  // of them, with row bands (SM_COUNTER_BAND_GROUPS)
     std::vector<TimedEvent> pending;
@@ -1171,6 +1179,10 @@ int run_lines(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs, hipStream_t 
     j.st = (uint8_t*)bs.st.p;
     j.ewarm = ew_warmup(ctx, n);
     j.ewguess = ctx->tune_ew_guess;
+    // one or two pairs (row bands): the patch passes' longest walks are the call's critical
+    // path, so the u16 segments warm up longer (settings.ini D = 160, one pair: 24 -> 54 columns,
+    // E/W repairs 551 -> 26 per matcher, device time per call 1114 -> 1058 us)
+    if (j.nband > 1 && ctx->tune_ew_warmup <= 0 && et == 2) j.ewarm = 54;
     if (j.nband > 1) {
         j.band_h = (g.H + j.nband - 1) / j.nband;
         j.vwarm = band_warmup(ctx, n);
@@ -1187,6 +1199,10 @@ int run_lines(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs, hipStream_t 
         {
             StageTimer ts(ctx, ctx->stream, SM_STAGE_SWEEP, G);
             if ((rc = sweep_pass(ctx, n, g, j, 3)) != SM_OK) return rc;
+        }
+        if (ctx->sweep_done_ev) {  // compute_disparity's stagger: the other matcher may start now
+            HIP_TRY(ctx, hipEventRecord(ctx->sweep_done_ev, ctx->stream));
+            ctx->sweep_done_hit = true;
         }
         if (fb_side) {
             // 5 paths: the group flag is final after the sweep, so the guarded per-direction
@@ -1382,7 +1398,8 @@ int launch_cost2_s(sm_ctx* ctx, const Norm& n, const Geo& g, const smk::SgbmCost
     c2.nt = cost_nt(g, 2);
     const int strips = (n.width1 + TX - 1) / TX;
     // enough workgroups to fill the chip; bands at least 8 rows (warm-up 2S rows each)
-    const int want = std::max(1, SGBM_COST2_WGS / std::max(1, strips * g.G));
+    const int wgs = ctx->tune_cost_wgs > 0 ? ctx->tune_cost_wgs : SGBM_COST2_WGS;
+    const int want = std::max(1, wgs / std::max(1, strips * g.G));
     c2.band = std::max({(sc.Yc + want - 1) / want, 8, 4 * S});
     const int bands = (sc.Yc + c2.band - 1) / c2.band;
     if (one)
@@ -2329,6 +2346,18 @@ int run_bm(sm_ctx* ctx, const uint8_t* dL, const uint8_t* dR, size_t pair_stride
 }
 
 // the third stream of compute_disparity (WLS guide-only work), on the context's CU mask
+int ensure_lr_stream(sm_ctx* ctx)
+{
+    int rc;
+    if ((rc = ensure_event(ctx, ctx->ev_stagger)) != SM_OK) return rc;
+    if (ctx->lr_stream) return SM_OK;
+    if (!ctx->cu_mask.empty())
+        HIP_TRY(ctx, hipExtStreamCreateWithCUMask(&ctx->lr_stream, (uint32_t)ctx->cu_mask.size(), ctx->cu_mask.data()));
+    else
+        HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->lr_stream, hipStreamNonBlocking));
+    return SM_OK;
+}
+
 int ensure_wls_stream(sm_ctx* ctx)
 {
     int rc;
@@ -2406,6 +2435,8 @@ void sm_destroy(sm_ctx* ctx)
     if (ctx->ev_wls_fork) (void)hipEventDestroy(ctx->ev_wls_fork);
     if (ctx->ev_wls_ready) (void)hipEventDestroy(ctx->ev_wls_ready);
     if (ctx->wls_stream) (void)hipStreamDestroy(ctx->wls_stream);
+    if (ctx->lr_stream) (void)hipStreamDestroy(ctx->lr_stream);
+    if (ctx->ev_stagger) (void)hipEventDestroy(ctx->ev_stagger);
     if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
     if (ctx->ev_fb_fork) (void)hipEventDestroy(ctx->ev_fb_fork);
     if (ctx->ev_fb_join) (void)hipEventDestroy(ctx->ev_fb_join);
@@ -2697,6 +2728,7 @@ int sm_compute_disparity_batch_device(sm_ctx* ctx, const uint8_t* dL, const uint
         ctx->twin->tune_bands = ctx->tune_bands;
         ctx->twin->tune_band_warmup = ctx->tune_band_warmup;
         ctx->twin->tune_band_guess = ctx->tune_band_guess;
+        ctx->twin->tune_cost_wgs = ctx->tune_cost_wgs;
         if (!ctx->cu_mask.empty() &&
             (rc = sm_set_cu_mask(ctx->twin, ctx->cu_mask.data(), (int)ctx->cu_mask.size())) != SM_OK)
             return fail(ctx, rc, "%s", ctx->twin->err.c_str());
@@ -2725,16 +2757,37 @@ int sm_compute_disparity_batch_device(sm_ctx* ctx, const uint8_t* dL, const uint
     // D = 160, one pair: matchers 1.32 ms concurrent, 1.22 ms in sequence; per matcher the
     // per-direction path kernel took 665 vs 332 us)
     const bool serial = (ctx->dbg_flags & DBG_CONCURRENT_LR) == 0;
+    // staggered: the left matcher starts on a second stream as soon as the right
+    // one's MODE 3 sweep is done, so its cost volume and sweep overlap the right one's
+    // latency-bound patch passes and WTA (with no MODE 3 sweep: after the whole right matcher)
+    const bool stagger = serial && ctx->tune_lr_stagger >= 0;
+    if (stagger && (rc = ensure_lr_stream(ctx)) != SM_OK) return rc;
     {
         // serial: the twin enqueues on the caller's stream for this call only (restored on
         // every exit path, so the twin never keeps a stream it does not own)
         StreamSwap sw(tw, serial ? ctx->stream : tw->stream);
         HIP_TRY(ctx, hipStreamWaitEvent(tw->stream, ctx->ev_lr_fork, 0));
+        tw->sweep_done_ev = stagger ? ctx->ev_stagger : nullptr;
+        tw->sweep_done_hit = false;
         rc = sm_compute_batch_device(tw, dR, dL, npairs, pair_stride, H, W, stride, &rm, d_dispr);
+        tw->sweep_done_ev = nullptr;
     }
     if (rc != SM_OK) return fail(ctx, rc, "right matcher: %s", tw->err.c_str());
-    HIP_TRY(ctx, hipEventRecord(ctx->ev_lr_join, serial ? ctx->stream : tw->stream));
-    rc = sm_compute_batch_device(ctx, dL, dR, npairs, pair_stride, H, W, stride, &lm, d_displ);
+    if (stagger) {
+        if (!tw->sweep_done_hit) HIP_TRY(ctx, hipEventRecord(ctx->ev_stagger, ctx->stream));
+        HIP_TRY(ctx, hipEventRecord(ctx->ev_lr_join, ctx->stream));  // the right matcher's end
+        HIP_TRY(ctx, hipStreamWaitEvent(ctx->lr_stream, ctx->ev_stagger, 0));
+        {
+            StreamSwap sw(ctx, ctx->lr_stream);
+            rc = sm_compute_batch_device(ctx, dL, dR, npairs, pair_stride, H, W, stride, &lm, d_displ);
+        }
+        // the caller's stream has the right matcher; it joins the left one (every path)
+        HIP_TRY(ctx, hipEventRecord(ctx->ev_stagger, ctx->lr_stream));
+        HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_stagger, 0));
+    } else {
+        HIP_TRY(ctx, hipEventRecord(ctx->ev_lr_join, serial ? ctx->stream : tw->stream));
+        rc = sm_compute_batch_device(ctx, dL, dR, npairs, pair_stride, H, W, stride, &lm, d_displ);
+    }
     HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_lr_join, 0));  // joined on every path
     if (prep) HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_wls_ready, 0));
     if (rc != SM_OK) return rc;
@@ -3075,6 +3128,7 @@ int sm_set_cu_mask(sm_ctx* ctx, const uint32_t* mask, int nwords)
     HIP_TRY(ctx, hipStreamSynchronize(ctx->own_stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->side));
     if (ctx->wls_stream) HIP_TRY(ctx, hipStreamSynchronize(ctx->wls_stream));
+    if (ctx->lr_stream) HIP_TRY(ctx, hipStreamSynchronize(ctx->lr_stream));
     hipStream_t a = nullptr, b = nullptr;
     if (nwords > 0) {
         HIP_TRY(ctx, hipExtStreamCreateWithCUMask(&a, (uint32_t)nwords, mask));
@@ -3096,6 +3150,10 @@ int sm_set_cu_mask(sm_ctx* ctx, const uint32_t* mask, int nwords)
     if (ctx->wls_stream) {  // recreated on the new mask when next needed
         (void)hipStreamDestroy(ctx->wls_stream);
         ctx->wls_stream = nullptr;
+    }
+    if (ctx->lr_stream) {
+        (void)hipStreamDestroy(ctx->lr_stream);
+        ctx->lr_stream = nullptr;
     }
     ctx->own_stream = a;
     ctx->side = b;
@@ -3176,6 +3234,14 @@ int sm_set_tuning(sm_ctx* ctx, int key, int value)
     case SM_TUNE_BAND_GUESS:
         if (value < 0 || value > 1) return fail(ctx, SM_E_ARG, "band guess %d: 0 or 1", value);
         ctx->tune_band_guess = value;
+        break;
+    case SM_TUNE_COST_WGS:
+        if (value < 0 || value > 65536) return fail(ctx, SM_E_ARG, "cost workgroups %d: 0..65536", value);
+        ctx->tune_cost_wgs = value;
+        break;
+    case SM_TUNE_LR_STAGGER:
+        if (value < -1 || value > 1) return fail(ctx, SM_E_ARG, "matcher stagger %d: -1, 0 or 1", value);
+        ctx->tune_lr_stagger = value;
         break;
     default: return fail(ctx, SM_E_ARG, "unknown tuning key %d", key);
     }

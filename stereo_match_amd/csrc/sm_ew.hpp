@@ -211,14 +211,14 @@ __global__ void __launch_bounds__(256) k_ew_patch(EwPatchArgs a)
         // first chunk's beside the state loads: one memory round trip for both)
         RawBytes<CB> cc[RC];
         RawBytes<DPL * 2> pb[RC];
+        auto issue1 = [&](int u, int o) {  // slot u <- column o of the walk
+            const int c = dir ? x0 + CW - 1 - o : x0 + o;
+            cc[u].load(rc, o < ncol ? cell(c) * (uint32_t)sizeof(CT) : kOOB);
+            pb[u].load(rp, o < ncol ? cell(c) * 2u : kOOB);
+        };
         auto issue = [&](int o0) {
 #pragma unroll
-            for (int u = 0; u < RC; u++) {
-                const int o = o0 + u;
-                const int c = dir ? x0 + CW - 1 - o : x0 + o;
-                cc[u].load(rc, o < ncol ? cell(c) * (uint32_t)sizeof(CT) : kOOB);
-                pb[u].load(rp, o < ncol ? cell(c) * 2u : kOOB);
-            }
+            for (int u = 0; u < RC; u++) issue1(u, o0 + u);
         };
         issue(0);
         uint32_t A[NP];
@@ -235,14 +235,20 @@ __global__ void __launch_bounds__(256) k_ew_patch(EwPatchArgs a)
         mq[1] = state_min(Lq[1]);
         bool met = false;
         for (int o0 = 0; o0 < ncol && !met; o0 += RC) {
-            if (o0 > 0) issue(o0);
 #pragma unroll
             for (int u = 0; u < RC; u++) {  // (no break: the loop must unroll)
                 const int o = o0 + u;
                 if (o >= ncol || met) continue;
                 const int c = dir ? x0 + CW - 1 - o : x0 + o;
-                uint32_t C2[2][NP], Ln[2][NP], mn[2];
+                uint32_t C2[2][NP], Ln[2][NP], mn[2], pv_[NP];
                 unpack_ct_pk<CT, DPL>(cc[u], C2[0]);
+                // slot u refilled with column o + RC once read (loads RC columns ahead)
+#pragma unroll
+                for (int q = 0; q < NP; q++) {
+                    pv_[q] = pb[u].w[q];
+                    asm volatile("" : "+v"(C2[0][q]), "+v"(pv_[q])::"memory");
+                }
+                issue1(u, o + RC);
 #pragma unroll
                 for (int q = 0; q < NP; q++) C2[1][q] = C2[0][q];
                 sweep_step2n<VL, NP, H16, 2>(Lq, mq, C2, P1p, P2p, eL, eR, Ln, mn);
@@ -256,12 +262,12 @@ __global__ void __launch_bounds__(256) k_ew_patch(EwPatchArgs a)
                     if constexpr (SAT) {
                         // a half pv < 0xFFFF is the exact sum, pv >= sv: (pv - sv) + tv saturating;
                         // pv == 0xFFFF stays (sat: 0xFFFF exactly there, from pv + 1 wrapping to 0)
-                        const uint32_t pv = pb[u].w[q];
+                        const uint32_t pv = pv_[q];
                         const uint32_t x = pk_adds(pk_sub(pv, Ln[0][q]), Ln[1][q]);
                         const uint32_t sat = pk_sub(pk_min(pk_add(pv, 0x00010001u), 0x00010001u), 0x00010001u);
                         P[q] = pkw(__builtin_elementwise_max(pkv(x), pkv(sat)));
                     } else {  // census: every sum < 2^11, the u16 wrap is exact
-                        P[q] = pk_add(pk_sub(pb[u].w[q], Ln[0][q]), Ln[1][q]);
+                        P[q] = pk_add(pk_sub(pv_[q], Ln[0][q]), Ln[1][q]);
                     }
                 }
                 bstore_n<uint32_t, NP>(rp, cell(c) * 2u, P);
@@ -315,14 +321,14 @@ __global__ void __launch_bounds__(256) k_ew_patch(EwPatchArgs a)
         // first chunk's beside the state loads: one memory round trip for both)
         RawBytes<CBW> cc[RC];
         RawBytes<DPLW * 2> pb[RC];
+        auto issue1 = [&](int u, int o) {  // slot u <- column o of the walk
+            const int c = dir ? x0 + CW - 1 - o : x0 + o;
+            cc[u].load(rc, o < ncol ? cell64(c) * (uint32_t)sizeof(CT) : kOOB);
+            pb[u].load(rp, o < ncol ? cell64(c) * 2u : kOOB);
+        };
         auto issue = [&](int o0) {
 #pragma unroll
-            for (int u = 0; u < RC; u++) {
-                const int o = o0 + u;
-                const int c = dir ? x0 + CW - 1 - o : x0 + o;
-                cc[u].load(rc, o < ncol ? cell64(c) * (uint32_t)sizeof(CT) : kOOB);
-                pb[u].load(rp, o < ncol ? cell64(c) * 2u : kOOB);
-            }
+            for (int u = 0; u < RC; u++) issue1(u, o0 + u);
         };
         issue(0);
         uint32_t A[NPW];
@@ -339,14 +345,20 @@ __global__ void __launch_bounds__(256) k_ew_patch(EwPatchArgs a)
         mq[1] = state_min64(Lq[1]);
         bool met = false;
         for (int o0 = 0; o0 < ncol && !met; o0 += RC) {
-            if (o0 > 0) issue(o0);
 #pragma unroll
             for (int u = 0; u < RC; u++) {  // (no break: the loop must unroll)
                 const int o = o0 + u;
                 if (o >= ncol || met) continue;
                 const int c = dir ? x0 + CW - 1 - o : x0 + o;
-                uint32_t C2[2][NPW], Ln[2][NPW], mn[2];
+                uint32_t C2[2][NPW], Ln[2][NPW], mn[2], pv_[NPW];
                 unpack_ct_pk<CT, DPLW>(cc[u], C2[0]);
+                // slot u refilled with column o + RC once read (loads RC columns ahead)
+#pragma unroll
+                for (int q = 0; q < NPW; q++) {
+                    pv_[q] = pb[u].w[q];
+                    asm volatile("" : "+v"(C2[0][q]), "+v"(pv_[q])::"memory");
+                }
+                issue1(u, o + RC);
 #pragma unroll
                 for (int q = 0; q < NPW; q++) C2[1][q] = C2[0][q];
                 sweep_step2n<64, NPW, H16, 2>(Lq, mq, C2, P1p, P2p, 0u, 0u, Ln, mn);
@@ -360,12 +372,12 @@ __global__ void __launch_bounds__(256) k_ew_patch(EwPatchArgs a)
                     if constexpr (SAT) {
                         // a half pv < 0xFFFF is the exact sum, pv >= sv: (pv - sv) + tv saturating;
                         // pv == 0xFFFF stays (sat: 0xFFFF exactly there, from pv + 1 wrapping to 0)
-                        const uint32_t pv = pb[u].w[q];
+                        const uint32_t pv = pv_[q];
                         const uint32_t x = pk_adds(pk_sub(pv, Ln[0][q]), Ln[1][q]);
                         const uint32_t sat = pk_sub(pk_min(pk_add(pv, 0x00010001u), 0x00010001u), 0x00010001u);
                         P[q] = pkw(__builtin_elementwise_max(pkv(x), pkv(sat)));
                     } else {  // census: every sum < 2^11, the u16 wrap is exact
-                        P[q] = pk_add(pk_sub(pb[u].w[q], Ln[0][q]), Ln[1][q]);
+                        P[q] = pk_add(pk_sub(pv_[q], Ln[0][q]), Ln[1][q]);
                     }
                 }
                 bstore_n<uint32_t, NPW>(rp, cell64(c) * 2u, P);
@@ -581,17 +593,18 @@ __global__ void __launch_bounds__(256) k_band_patch(BandPatchArgs a)
         const int rb = min(H, y0 + a.band_h) - y0;  // steps inside band bi
         bool met = false;
         int r0 = 0;
+        // cost loads RC steps ahead: slot u holds step r0 + u; it is refilled with step r0 + u + RC
+        // as soon as it is unpacked, so the chain never waits for a whole chunk's round trip
         for (; r0 < nr && !met; r0 += RC) {
-            if (r0 > 0) {
-#pragma unroll
-                for (int u = 0; u < RC; u++) cc[u].load(rc, cost_off(r0 + u));
-            }
 #pragma unroll
             for (int u = 0; u < RC; u++) {  // (no break: the loop must unroll)
                 const int r = r0 + u;
                 if (r >= nr || met) continue;
                 uint32_t C2[2][NP], Ln[2][NP], mn[2];
                 unpack_ct_pk<CT, DPL>(cc[u], C2[0]);
+#pragma unroll
+                for (int q = 0; q < NP; q++) asm volatile("" : "+v"(C2[0][q])::"memory");
+                cc[u].load(rc, cost_off(r + RC));
 #pragma unroll
                 for (int q = 0; q < NP; q++) C2[1][q] = C2[0][q];
                 sweep_step2n<VL, NP, H16, 2>(Lq, mq, C2, P1p, P2p, eL, eR, Ln, mn);

@@ -67,11 +67,13 @@ def test_lines_random_shapes(eng, c):
 
 
 @pytest.mark.parametrize("cost,mode,D", [(1, 8, 128), (0, 5, 128), (0, 8, 128), (0, 5, 160), (1, 5, 64)])
-@pytest.mark.parametrize("warm,guess", [(0, 0), (1, 0), (0, 1)])
+@pytest.mark.parametrize("warm,guess", [(0, 0), (1, 0), (1, 1)])
 def test_lines_full_kitti(eng, cost, mode, D, warm, guess):
     """Full KITTI frames: default warmup, the shortest warmup, and a deliberately wrong start
     state (SM_TUNE_EW_GUESS: every segment that does not meet the truth inside its warmup is
-    repaired): bit-exact, and the repair counter counts the repairs."""
+    repaired; with the shortest warmup, so that they are): bit-exact, and the repair counter
+    counts the repairs.  (One pair of 5 paths runs on the row bands, whose default u16 warmup
+    is long enough for even a wrong guess to meet the truth.)"""
     H, W, _ = synthetic.CONFIGS["kitti"]
     left, right, _ = synthetic.random_dot_pair(H, W, D, seed=D + mode + cost)
     p = _params(cost, D, mode)
@@ -198,7 +200,8 @@ def test_lines_tuning_arguments(eng):
     with pytest.raises(ValueError):
         eng.set_tuning(eng.TUNE_EW_GUESS, 2)
     c = eng.counters()
-    assert set(c) == {"sweep_fallbacks", "ew_repairs", "volume_clamped", "volume_nan", "line_groups", "ew_open"}
+    assert set(c) == {"sweep_fallbacks", "ew_repairs", "volume_clamped", "volume_nan", "line_groups", "ew_open",
+                      "band_repairs", "band_open", "band_groups"}
 
 
 # ------------------------------------------------------------------ mc-cnn quantisation window

@@ -193,3 +193,46 @@ def test_bands_off_matches_bands_on_full_kitti_census(eng):
     b = _run(eng, left, right, p)
     exp = ref_c.compute(left, right, p)
     assert np.array_equal(a, exp) and np.array_equal(b, exp)
+
+
+def test_band_tuning_arguments(eng):
+    for key, bad in ((eng.TUNE_BANDS, -1), (eng.TUNE_BAND_WARMUP, -1), (eng.TUNE_BAND_GUESS, 2),
+                     (eng.TUNE_COST_WGS, -1), (eng.TUNE_LR_STAGGER, 2)):
+        with pytest.raises(ValueError):
+            eng.set_tuning(key, bad)
+
+
+@pytest.mark.parametrize("stagger", [0, -1])
+def test_compute_disparity_stagger_matches_serial(stagger):
+    """sm_compute_disparity with the left matcher staggered behind the right one's sweep (the
+    default) and strictly after it: the same maps, equal to the C oracle's left matcher + the
+    numpy WLS restatement (settings.ini, one KITTI pair, D = 160)."""
+    from oracle import sgm_np, wls_np
+    from stereo_match_amd import settings, wls
+    from stereo_match_amd.stereo_vision import matcher_from_settings
+
+    s = dict(settings.DEFAULT_SETTINGS, window_size=5)
+    H, W, _ = synthetic.CONFIGS["kitti"]
+    D = s["num_disparities"]
+    gl, gr, _ = synthetic.random_dot_pair(H, W, D, seed=66)
+    lm = matcher_from_settings(s)
+    prm = lm.params()
+    wf = wls.createDisparityWLSFilter(lm)
+    wf.setLambda(s["lmbda"])
+    wf.setSigmaColor(s["sigma"])
+    wp = wf.params(H, W)
+    e = _lib.Engine(0)
+    try:
+        e.set_tuning(e.TUNE_LR_STAGGER, stagger)
+        d, f = e.compute_disparity(gl, gr, prm, wp)
+        d2, f2 = e.compute_disparity(gl, gr, prm, wp)  # buffers reused
+    finally:
+        e.close()
+    assert np.array_equal(d, d2) and np.array_equal(f, f2)
+    hp = synthetic.parity_params(D, 5)
+    lp = dict(hp, uniquenessRatio=0, disp12MaxDiff=1000000)
+    dl = ref_c.compute(gl, gr, lp)
+    assert np.array_equal(d, dl)
+    dr = ref_c.compute(gr, gl, sgm_np.right_matcher_params(hp))
+    wpar = dict(lmbda=80000.0, sigma=1.2, radius=(hp["blockSize"] + 1) // 2, min_disp=0, left_offset=D, right_offset=0)
+    assert np.array_equal(f, wls_np.wls_filter(dl, gl, dr, wpar))

@@ -3,7 +3,7 @@ stereo_vision.py:178-182 runs it): stage breakdown of sm_compute_disparity at
 settings.ini values (D=160) for each engine flag set.
     python tools/single_pair.py [--flags 0,4096] [--calls 20] [--runs "0/ew=16;16384/ncw=5"]
 A run is debug flags, then /knob=value items (ew: SM_TUNE_EW_LANES, ncw: SM_TUNE_SWEEP_NCW,
-bands: SM_TUNE_BANDS, bw: SM_TUNE_BAND_WARMUP);
+bands: SM_TUNE_BANDS, bw: SM_TUNE_BAND_WARMUP, eww: SM_TUNE_EW_WARMUP, cw: SM_TUNE_COST_WGS);
 --runs replaces --flags."""
 import argparse
 import json
@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--calls", type=int, default=20)
     ap.add_argument("--D", type=int, default=160)
     ap.add_argument("--runs", default="")
+    ap.add_argument("--stages", default="", help="comma list: time only these stages (e.g. call); default all")
     args = ap.parse_args()
     import stereo_match_amd as sm
     from stereo_match_amd import _lib, synthetic, wls
@@ -38,7 +39,8 @@ def main():
     wp = wf.params(H, W)
     e = _lib.Engine(0)
     ref = None
-    knobs = {"ew": e.TUNE_EW_LANES, "ncw": e.TUNE_SWEEP_NCW, "bands": e.TUNE_BANDS, "bw": e.TUNE_BAND_WARMUP}
+    knobs = {"ew": e.TUNE_EW_LANES, "ncw": e.TUNE_SWEEP_NCW, "bands": e.TUNE_BANDS, "bw": e.TUNE_BAND_WARMUP,
+             "eww": e.TUNE_EW_WARMUP, "cw": e.TUNE_COST_WGS, "stag": e.TUNE_LR_STAGGER}
     runs = args.runs.split(";") if args.runs else args.flags.split(",")
     for run in runs:
         parts = run.split("/")
@@ -51,7 +53,7 @@ def main():
         if ref is None:
             ref = (d, fl)
         same = bool(np.array_equal(d, ref[0]) and np.array_equal(fl, ref[1]))
-        e.set_timing(True)
+        e.set_timing(True, stages=args.stages.split(",") if args.stages else None)
         e.reset_timing()
         c0 = e.counters()
         ts = []
