@@ -609,8 +609,7 @@ __device__ __forceinline__ void wta_packed_cols(const WtaArgs& a, const int y, c
         for (int j = 0; j < NP; j++) {
             uint32_t t = pk_sub(dpk[j], bm1p);  // d + 1 - best: 0, 1, 2 inside the window
             t = pkw(__builtin_elementwise_sub_sat(pkv(0x00030003u), pkv(t)));
-            t = pkw(pkv(t) * pkv(0xFFFFFFFFu));
-            m2p = pk_min(m2p, pk_adds(Sp[j], t));
+            m2p = pk_min(m2p, pk_window_push(t, Sp[j]));
         }
         const uint32_t m2 = row16_min(::min(m2p & 0xFFFFu, m2p >> 16));
         const bool bad = (int)m2 * ku < (int)minS * 100 && (!pad || m2 <= 32767u);

@@ -92,6 +92,17 @@ __device__ __forceinline__ uint32_t pk_adds(uint32_t a, uint32_t b)
     return pkw(__builtin_elementwise_add_sat(pkv(a), pkv(b)));
 }
 
+// min(s + u * 0xFFFF, 0xFFFF) per u16 half (v_pk_mad_u16 with clamp; with the product
+// truncated to 16 bits it is still >= 0xFFFD for u in 1..3): the uniqueness test's window
+// entries (u = 3 - t > 0) pushed above every sum, the others (u = 0) unchanged, in one
+// instruction instead of the negate + saturating add the compiler emits for it
+__device__ __forceinline__ uint32_t pk_window_push(uint32_t u, uint32_t s)
+{
+    uint32_t r;
+    asm("v_pk_mad_u16 %0, %1, -1, %2 clamp" : "=v"(r) : "v"(u), "v"(s));
+    return r;
+}
+
 template <int VL, int NP>
 __device__ __forceinline__ uint32_t sweep_step_pk(const uint32_t (&Lp)[NP], uint32_t minLp, const uint32_t (&C)[NP],
                                                   uint32_t P1p, uint32_t P2, uint32_t (&Ln)[NP])

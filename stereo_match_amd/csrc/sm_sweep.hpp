@@ -1512,9 +1512,7 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
 #pragma unroll
                             for (int i = 0; i < NP; i++) tw[i] = pkw(__builtin_elementwise_sub_sat(pkv(0x00030003u), pkv(tw[i])));
 #pragma unroll
-                            for (int i = 0; i < NP; i++) tw[i] = pkw(pkv(tw[i]) * pkv(0xFFFFFFFFu));
-#pragma unroll
-                            for (int i = 0; i < NP; i++) tw[i] = pk_adds(Sp[i], tw[i]);
+                            for (int i = 0; i < NP; i++) tw[i] = pk_window_push(tw[i], Sp[i]);
                             uint32_t m2p = tw[0];
 #pragma unroll
                             for (int i = 1; i < NP; i++) m2p = pk_min(m2p, tw[i]);

@@ -236,3 +236,25 @@ def test_compute_disparity_stagger_matches_serial(stagger):
     dr = ref_c.compute(gr, gl, sgm_np.right_matcher_params(hp))
     wpar = dict(lmbda=80000.0, sigma=1.2, radius=(hp["blockSize"] + 1) // 2, min_disp=0, left_offset=D, right_offset=0)
     assert np.array_equal(f, wls_np.wls_filter(dl, gl, dr, wpar))
+
+
+def test_compute_disparity_one_call_equals_three_calls():
+    """The Python compute_disparity (one-call ABI for 2-D uint8 numpy pairs) against the
+    reference's three calls made separately through the matcher / WLS objects: identical maps."""
+    import stereo_match_amd as sm
+    from stereo_match_amd import settings, wls
+    from stereo_match_amd.stereo_vision import matcher_from_settings
+
+    s = dict(settings.DEFAULT_SETTINGS, window_size=5)
+    H, W = 200, 640
+    gl, gr, _ = synthetic.random_dot_pair(H, W, s["num_disparities"], seed=67)
+    d1, f1 = sm.compute_disparity(gl, gr, s)
+    lm = matcher_from_settings(s)
+    rmatch = sm.createRightMatcher(lm)
+    wf = wls.createDisparityWLSFilter(lm)
+    wf.setLambda(s["lmbda"])
+    wf.setSigmaColor(s["sigma"])
+    d2 = lm.compute(gl, gr)
+    dr = rmatch.compute(gr, gl)
+    f2 = wf.filter(d2, gl, None, dr)
+    assert np.array_equal(d1, d2) and np.array_equal(f1, f2)

@@ -4,6 +4,7 @@
 #       traffic (separate FETCH/WRITE passes) + SQ counters for the headline (census8), the
 #       parity mode (sgbm5) and Middlebury -> their benches with those files
 #   bash tools/gpu_round.sh <tag> T : part A without smoke, tests and kernel stats
+#   bash tools/gpu_round.sh <tag> P : part A without smoke, tests, valu_rate and the single-pair run
 #   bash tools/gpu_round.sh <tag> B : the other bench modes / engines / configs
 # Each GPU step is time-limited; a failure (other than pytest's rc 1) stops the script.
 set -u
@@ -13,7 +14,7 @@ OUT=gpurun_out/$TAG; mkdir -p "$OUT"
 export TMPDIR=/tmp
 step() { local name=$1 t=$2; shift 2; echo "== $name"; timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1; local rc=$?
          echo "== $name rc=$rc"; tail -n 2 "$OUT/$name.log" | cut -c1-400; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi; }
-if [ "$PART" = A ] || [ "$PART" = T ]; then
+if [ "$PART" = A ] || [ "$PART" = T ] || [ "$PART" = P ]; then
   if [ "$PART" = A ]; then
   step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()"
   step pytest_gpu 600 python -u -m pytest tests -m gpu -q -x --timeout 240 --timeout-method thread -p no:cacheprovider
@@ -31,8 +32,8 @@ if [ "$PART" = A ] || [ "$PART" = T ]; then
   done
   cp "$OUT/census8_traffic.json" profiles/traffic_latest.json
   cp "$OUT/census8_valu.json" profiles/valu_latest.json
-  [ "$PART" = T ] || step valu_rate 120 ./tools/ubench/valu_rate
-  [ "$PART" = T ] || FLAGS=0 step single 400 bash tools/gpu_single.sh $TAG
+  [ "$PART" = A ] && step valu_rate 120 ./tools/ubench/valu_rate
+  [ "$PART" = A ] && FLAGS=0 step single 400 bash tools/gpu_single.sh $TAG
   step bench 400 python -u bench.py --traffic-file "$OUT/census8_traffic.json"
   step bench_sgbm5 400 python -u bench.py --mode sgbm5 --traffic-file "$OUT/sgbm5_traffic.json" --valu-file "$OUT/sgbm5_valu.json"
   step bench_middlebury 400 python -u bench.py --config middlebury --pairs-per-gpu 4 --steps 40 --warmup 4 --cpu-baseline-pairs 0 --host-surface-calls 0 --traffic-file "$OUT/middlebury_traffic.json" --valu-file "$OUT/middlebury_valu.json"
