@@ -403,6 +403,8 @@ int sm_set_debug_flags(sm_ctx* ctx, int flags);
  *                      wrong state inside the domain, so that nearly every chain is repaired.
  *   SM_TUNE_COST_WGS   workgroups the SGBM cost kernel aims for per launch (0 automatic:
  *                      2048; its row bands are sized from it).
+ *   SM_TUNE_SWEEP_XCD  fused sweeps: 1 place each XCD's workgroups on a run of adjacent strips
+ *                      (their cost rows shared in its L2), 0 / -1 the plain grid order.
  *   SM_TUNE_LR_STAGGER sm_compute_disparity*: 0 automatic / 1 the left matcher starts on a
  *                      second stream once the right one's down sweep is done (overlapping its
  *                      patch passes and WTA); -1 the matchers strictly one after the other.
@@ -419,6 +421,7 @@ int sm_set_debug_flags(sm_ctx* ctx, int flags);
 #define SM_TUNE_BAND_GUESS 10
 #define SM_TUNE_COST_WGS 11
 #define SM_TUNE_LR_STAGGER 12
+#define SM_TUNE_SWEEP_XCD 13
 int sm_set_tuning(sm_ctx* ctx, int key, int value);
 
 /* Last error text of ctx (or of the calling thread when ctx == NULL). */

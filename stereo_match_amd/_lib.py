@@ -504,7 +504,7 @@ class Engine:
 
     TUNE_EW_LANES, TUNE_SWEEP_NCW, TUNE_EW_WAVES, TUNE_EW_PRIO, TUNE_EW_WARMUP, TUNE_SWEEP_LINES = 1, 2, 3, 4, 5, 6
     TUNE_EW_GUESS = 7
-    TUNE_BANDS, TUNE_BAND_WARMUP, TUNE_BAND_GUESS, TUNE_COST_WGS, TUNE_LR_STAGGER = 8, 9, 10, 11, 12
+    TUNE_BANDS, TUNE_BAND_WARMUP, TUNE_BAND_GUESS, TUNE_COST_WGS, TUNE_LR_STAGGER, TUNE_SWEEP_XCD = 8, 9, 10, 11, 12, 13
 
     def set_tuning(self, key: int, value: int):
         """Launch-shape knob (include/stereo_match_amd.h sm_set_tuning); 0 = automatic."""

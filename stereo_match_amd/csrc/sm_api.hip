@@ -175,6 +175,7 @@ struct sm_ctx {
     int tune_ew_guess = 0;                         // 1: the lines start from a wrong state (tests)
     int tune_bands = 0, tune_band_warmup = 0, tune_band_guess = 0;  // MODE 3 row bands (SM_TUNE_BANDS ...)
     int tune_cost_wgs = 0;  // k_sgbm_cost2 workgroups a launch aims for (SM_TUNE_COST_WGS; 0: SGBM_COST2_WGS)
+    int tune_sweep_xcd = 0;  // SM_TUNE_SWEEP_XCD: 1 the XCD-aware strip placement, -1 / 0 off
     long long line_groups = 0;  // launch groups run with the in-sweep E/W lines (SM_COUNTER_LINE_GROUPS)
     long long band_groups = 0;  // of them, with row bands (SM_COUNTER_BAND_GROUPS)
     std::vector<TimedEvent> pending;
@@ -918,6 +919,10 @@ int sweep_pass(sm_ctx* ctx, const Norm& n, const Geo& g, const SweepJob& j, int 
         a.hop_nblk = nblk;
         a.vst = j.vst ? j.vst + (size_t)p0 * j.vst_pair : nullptr;
         a.vst_pair = j.vst_pair;
+        if (ctx->tune_sweep_xcd > 0) {  // XCD-aware placement (SweepArgs::xcd_per)
+            a.xcd_total = np * nwg * nb;
+            a.xcd_per = (a.xcd_total + 7) / 8;
+        }
         a.rec = j.key2 ? j.key2 + (size_t)p0 * g.H * g.W : nullptr;
         a.nb = j.pre ? j.pre + (size_t)p0 * g.H * g.W : nullptr;
         a.err = j.err;
@@ -2729,6 +2734,7 @@ int sm_compute_disparity_batch_device(sm_ctx* ctx, const uint8_t* dL, const uint
         ctx->twin->tune_band_warmup = ctx->tune_band_warmup;
         ctx->twin->tune_band_guess = ctx->tune_band_guess;
         ctx->twin->tune_cost_wgs = ctx->tune_cost_wgs;
+        ctx->twin->tune_sweep_xcd = ctx->tune_sweep_xcd;
         if (!ctx->cu_mask.empty() &&
             (rc = sm_set_cu_mask(ctx->twin, ctx->cu_mask.data(), (int)ctx->cu_mask.size())) != SM_OK)
             return fail(ctx, rc, "%s", ctx->twin->err.c_str());
@@ -3238,6 +3244,10 @@ int sm_set_tuning(sm_ctx* ctx, int key, int value)
     case SM_TUNE_COST_WGS:
         if (value < 0 || value > 65536) return fail(ctx, SM_E_ARG, "cost workgroups %d: 0..65536", value);
         ctx->tune_cost_wgs = value;
+        break;
+    case SM_TUNE_SWEEP_XCD:
+        if (value < -1 || value > 1) return fail(ctx, SM_E_ARG, "sweep XCD placement %d: -1, 0 or 1", value);
+        ctx->tune_sweep_xcd = value;
         break;
     case SM_TUNE_LR_STAGGER:
         if (value < -1 || value > 1) return fail(ctx, SM_E_ARG, "matcher stagger %d: -1, 0 or 1", value);

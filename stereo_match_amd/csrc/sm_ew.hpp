@@ -235,6 +235,7 @@ __global__ void __launch_bounds__(256) k_ew_patch(EwPatchArgs a)
         mq[1] = state_min(Lq[1]);
         bool met = false;
         for (int o0 = 0; o0 < ncol && !met; o0 += RC) {
+            if (o0 > 0) issue(o0);
 #pragma unroll
             for (int u = 0; u < RC; u++) {  // (no break: the loop must unroll)
                 const int o = o0 + u;
@@ -242,13 +243,8 @@ __global__ void __launch_bounds__(256) k_ew_patch(EwPatchArgs a)
                 const int c = dir ? x0 + CW - 1 - o : x0 + o;
                 uint32_t C2[2][NP], Ln[2][NP], mn[2], pv_[NP];
                 unpack_ct_pk<CT, DPL>(cc[u], C2[0]);
-                // slot u refilled with column o + RC once read (loads RC columns ahead)
 #pragma unroll
-                for (int q = 0; q < NP; q++) {
-                    pv_[q] = pb[u].w[q];
-                    asm volatile("" : "+v"(C2[0][q]), "+v"(pv_[q])::"memory");
-                }
-                issue1(u, o + RC);
+                for (int q = 0; q < NP; q++) pv_[q] = pb[u].w[q];
 #pragma unroll
                 for (int q = 0; q < NP; q++) C2[1][q] = C2[0][q];
                 sweep_step2n<VL, NP, H16, 2>(Lq, mq, C2, P1p, P2p, eL, eR, Ln, mn);
@@ -345,6 +341,7 @@ __global__ void __launch_bounds__(256) k_ew_patch(EwPatchArgs a)
         mq[1] = state_min64(Lq[1]);
         bool met = false;
         for (int o0 = 0; o0 < ncol && !met; o0 += RC) {
+            if (o0 > 0) issue(o0);
 #pragma unroll
             for (int u = 0; u < RC; u++) {  // (no break: the loop must unroll)
                 const int o = o0 + u;
@@ -352,13 +349,8 @@ __global__ void __launch_bounds__(256) k_ew_patch(EwPatchArgs a)
                 const int c = dir ? x0 + CW - 1 - o : x0 + o;
                 uint32_t C2[2][NPW], Ln[2][NPW], mn[2], pv_[NPW];
                 unpack_ct_pk<CT, DPLW>(cc[u], C2[0]);
-                // slot u refilled with column o + RC once read (loads RC columns ahead)
 #pragma unroll
-                for (int q = 0; q < NPW; q++) {
-                    pv_[q] = pb[u].w[q];
-                    asm volatile("" : "+v"(C2[0][q]), "+v"(pv_[q])::"memory");
-                }
-                issue1(u, o + RC);
+                for (int q = 0; q < NPW; q++) pv_[q] = pb[u].w[q];
 #pragma unroll
                 for (int q = 0; q < NPW; q++) C2[1][q] = C2[0][q];
                 sweep_step2n<64, NPW, H16, 2>(Lq, mq, C2, P1p, P2p, 0u, 0u, Ln, mn);
@@ -593,18 +585,17 @@ __global__ void __launch_bounds__(256) k_band_patch(BandPatchArgs a)
         const int rb = min(H, y0 + a.band_h) - y0;  // steps inside band bi
         bool met = false;
         int r0 = 0;
-        // cost loads RC steps ahead: slot u holds step r0 + u; it is refilled with step r0 + u + RC
-        // as soon as it is unpacked, so the chain never waits for a whole chunk's round trip
         for (; r0 < nr && !met; r0 += RC) {
+            if (r0 > 0) {
+#pragma unroll
+                for (int u = 0; u < RC; u++) cc[u].load(rc, cost_off(r0 + u));
+            }
 #pragma unroll
             for (int u = 0; u < RC; u++) {  // (no break: the loop must unroll)
                 const int r = r0 + u;
                 if (r >= nr || met) continue;
                 uint32_t C2[2][NP], Ln[2][NP], mn[2];
                 unpack_ct_pk<CT, DPL>(cc[u], C2[0]);
-#pragma unroll
-                for (int q = 0; q < NP; q++) asm volatile("" : "+v"(C2[0][q])::"memory");
-                cc[u].load(rc, cost_off(r + RC));
 #pragma unroll
                 for (int q = 0; q < NP; q++) C2[1][q] = C2[0][q];
                 sweep_step2n<VL, NP, H16, 2>(Lq, mq, C2, P1p, P2p, eL, eR, Ln, mn);

@@ -208,7 +208,7 @@ hipError_t SW_CAT(sweep_info_lat_m, SWEEP_MODE)(int D, int ct_bytes, int device,
 hipError_t SW_CAT(sweep_launch_lat_m, SWEEP_MODE)(int D, int ct_bytes, const SweepArgs& a, int npairs,
                                                   hipStream_t stream)
 {
-    LaunchF f{&a, dim3(a.nwg * (a.nband > 1 ? a.nband : 1), npairs), stream};
+    LaunchF f{&a, a.xcd_per > 0 ? dim3(8 * a.xcd_per, 1) : dim3(a.nwg * (a.nband > 1 ? a.nband : 1), npairs), stream};
     return with_sweep(D, ct_bytes, f);
 }
 #elif SWEEP_WIDE
@@ -221,7 +221,7 @@ hipError_t SW_CAT(sweep_info_wide_m, SWEEP_MODE)(int D, int ct_bytes, int device
 hipError_t SW_CAT(sweep_launch_wide_m, SWEEP_MODE)(int D, int ct_bytes, const SweepArgs& a, int npairs,
                                                    hipStream_t stream)
 {
-    LaunchF f{&a, dim3(a.nwg * (a.nband > 1 ? a.nband : 1), npairs), stream};
+    LaunchF f{&a, a.xcd_per > 0 ? dim3(8 * a.xcd_per, 1) : dim3(a.nwg * (a.nband > 1 ? a.nband : 1), npairs), stream};
     return with_sweep(D, ct_bytes, f);
 }
 #else
@@ -248,7 +248,7 @@ hipError_t SW_CAT(sweep_launch_m, SWEEP_MODE)(int D, int ct_bytes, int variant, 
 #else
     (void)variant;
 #endif
-    LaunchF f{&a, dim3(a.nwg * (a.nband > 1 ? a.nband : 1), npairs), stream};
+    LaunchF f{&a, a.xcd_per > 0 ? dim3(8 * a.xcd_per, 1) : dim3(a.nwg * (a.nband > 1 ? a.nband : 1), npairs), stream};
     return with_sweep(D, ct_bytes, f);
 }
 #endif

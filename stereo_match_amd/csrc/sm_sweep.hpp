@@ -529,10 +529,20 @@ __global__ void __launch_bounds__((sweep_threads<VL, DPL, NCW_, MODE>())) k_swee
     __shared__ uint32_t linecnt[LINES ? LG::NLW : 1], conscnt[NCW];
     __shared__ uint32_t pollcnt;  // NOBAR: blocks whose halo snapshot the poller has written
 
-    // row band of this workgroup (MODE 3 with a.nband > 1: blockIdx.x = band * nwg + strip)
+    // the workgroup's (pair, band, strip) item: blockIdx (x = band * nwg + strip, y = pair), or
+    // the XCD-aware 1-D placement (SweepArgs::xcd_per)
+    int bx = blockIdx.x, by = blockIdx.y;
+    if (a.xcd_per > 0) {
+        const int item = (int)(blockIdx.x & 7u) * a.xcd_per + (int)(blockIdx.x >> 3);
+        if (item >= a.xcd_total) return;  // padding workgroup: no strip, nothing to wait for
+        const int per_pair = a.nwg * (a.nband > 1 ? a.nband : 1);
+        by = item / per_pair;
+        bx = item - by * per_pair;
+    }
+    // row band of this workgroup (MODE 3 with a.nband > 1: bx = band * nwg + strip)
     const int nband = LINES && a.nband > 1 ? a.nband : 1;
-    const int band = nband > 1 ? (int)blockIdx.x / a.nwg : 0;
-    const int wg = (int)blockIdx.x - band * a.nwg, pair = blockIdx.y;
+    const int band = nband > 1 ? bx / a.nwg : 0;
+    const int wg = bx - band * a.nwg, pair = by;
     const int H = a.H, W1 = a.W1;
     // rows: own [y0b, y1b), computed from ys (vertical warmup rows above the band: the zero state,
     // or the test's wrong state, enters at ys); step s is row ys + s (down sweeps), s < nrow

@@ -52,6 +52,10 @@ struct SweepArgs {
     int hop_nblk;  // halo blocks per strip record in the hop buffer (>= every band's block count)
     uint8_t* vst;
     size_t vst_pair;  // bytes
+    // XCD-aware placement (xcd_per > 0): a 1-D grid of 8 * xcd_per workgroups; workgroup i runs
+    // item (i % 8) * xcd_per + i / 8 of the (pair, band, strip) list (items >= xcd_total exit at
+    // once), so each XCD holds a run of adjacent strips that share cost rows in its L2
+    int xcd_per, xcd_total;
 };
 
 

@@ -258,3 +258,33 @@ def test_compute_disparity_one_call_equals_three_calls():
     dr = rmatch.compute(gr, gl)
     f2 = wf.filter(d2, gl, None, dr)
     assert np.array_equal(d1, d2) and np.array_equal(f1, f2)
+
+
+@pytest.mark.parametrize("cost,mode,n", [(1, 8, 8), (0, 5, 7), (1, 5, 3)])
+def test_sweep_xcd_placement(eng, cost, mode, n):
+    """The XCD-aware strip placement (SM_TUNE_SWEEP_XCD 1: a 1-D grid whose workgroups on one XCD
+    hold adjacent strips, padding workgroups exiting at once): every pair equals the oracle."""
+    import torch
+
+    H, W, _ = synthetic.CONFIGS["kitti"]
+    D = 128
+    pairs = [synthetic.random_dot_pair(H, W, D, seed=3100 + 7 * cost + i)[:2] for i in range(n)]
+    p = dict(_params(cost, D), mode=mode)
+    L = torch.tensor(np.stack([a for a, _ in pairs]), device="cuda")
+    R = torch.tensor(np.stack([b for _, b in pairs]), device="cuda")
+    out = torch.empty((n, H, W), dtype=torch.int16, device="cuda")
+    eng.set_stream(torch.cuda.current_stream().cuda_stream)
+    eng.set_tuning(eng.TUNE_SWEEP_XCD, 1)
+    eng.set_debug_flags(SWEEP8)
+    try:
+        eng.compute_batch_device(L.data_ptr(), R.data_ptr(), n, H * W, H, W, W, synthetic.to_sm_params(p),
+                                 out.data_ptr())
+        eng.synchronize()
+    finally:
+        eng.set_tuning(eng.TUNE_SWEEP_XCD, 0)
+        eng.set_debug_flags(0)
+        eng.set_stream(None)
+    got = out.cpu().numpy()
+    exp = ref_c.compute_many(pairs, p)
+    for i in range(n):
+        assert np.array_equal(got[i], exp[i]), (i, int(np.sum(got[i] != exp[i])))
