@@ -1388,7 +1388,7 @@ int launch_cost2_s(sm_ctx* ctx, const Norm& n, const Geo& g, const smk::SgbmCost
         return fail(ctx, SM_E_UNSUPPORTED, "sgbm cost: numDisparities %d not built", n.D);
     const bool one = NHC <= bd && rpairs <= bd;  // one prefetch slot per thread (fewer VGPRs)
     const int rph = (rpairs + 1) / 2;
-    const size_t lds = (size_t)NHC * 16 + (size_t)((NHC + 1) & ~1) * 8 + (size_t)2 * rph * 24 + (size_t)2 * (NHC | 1) * NP * 4;
+    const size_t lds = (size_t)NHC * 16 + (size_t)((NHC + 1) & ~1) * 8 + (size_t)2 * rph * 24 + (size_t)2 * ((CG * ((NHC + CG - 1) / CG)) | 1) * NP * 4;
     smk::SgbmCost2Args c2{};
     c2.planes = sc.planes;
     c2.C = sc.C;

@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "sm_common.hpp"
 
 namespace smk {
@@ -45,10 +47,21 @@ __global__ void __launch_bounds__(256) k_census9x7(CensusArgs a)
     const uint8_t* img = a.img[which] + (size_t)pair * a.in_pair;
     const int x0 = blockIdx.x * CT_W, y0 = blockIdx.y * CT_H;
     uint8_t* tb = reinterpret_cast<uint8_t*>(&tile[0][0]);
-    for (int i = threadIdx.x; i < (CT_H + 6) * CT_LW; i += 256) {
+    // every byte load in flight before the first LDS write (a load -> wait -> write loop
+    // serialises ~7 memory round trips per workgroup)
+    constexpr int NT = (CT_H + 6) * CT_LW, NST = (NT + 255) / 256;
+    uint32_t st[NST];
+#pragma unroll
+    for (int k = 0; k < NST; k++) {
+        const int i = threadIdx.x + 256 * k;
         const int ty = i / CT_LW, tx = i % CT_LW;
         const int y = min(max(y0 + ty - 3, 0), a.H - 1), x = min(max(x0 + tx - 4, 0), a.W - 1);
-        tb[ty * CT_LW + tx] = img[(size_t)y * a.stride + x];
+        if (i < NT) st[k] = img[(size_t)y * a.stride + x];
+    }
+#pragma unroll
+    for (int k = 0; k < NST; k++) {
+        const int i = threadIdx.x + 256 * k;
+        if (i < NT) tb[i] = (uint8_t)st[k];
     }
     __syncthreads();
     const int tx = threadIdx.x % CT_W, ty0 = (threadIdx.x / CT_W) * CT_PY;
@@ -127,13 +140,24 @@ __global__ void __launch_bounds__(256) k_census_cost8(Cost8Args a)
     // i / chunks for i < 64 * 16 as a multiply-shift (exact: the error stays below 1/64)
     const uint32_t M = (65536u + (uint32_t)chunks - 1) / (uint32_t)chunks;
     const int xl = tid & 63, c0 = tid >> 6;
+    const int nr = nx + D - 1;  // <= 319: two right codes per thread
+    // the next row's codes are fetched into registers while this row computes
+    uint64_t pl = 0, pr0 = 0, pr1 = 0;
+    auto fetch = [&](int y) {
+        const uint64_t* cl = a.cl + pair * a.census_pair + (size_t)y * a.W;
+        const uint64_t* cr = a.cr + pair * a.census_pair + (size_t)y * a.W;
+        if (tid < nx) pl = cl[X0 + tid];
+        if (tid < nr) pr0 = cr[rlo + tid];
+        if (tid + 256 < nr) pr1 = cr[rlo + 256 + tid];
+    };
+    if (blockIdx.y * C8_RY < a.H) fetch(blockIdx.y * C8_RY);
     for (int r = 0; r < C8_RY; r++) {
         const int y = blockIdx.y * C8_RY + r;
         if (y >= a.H) break;  // workgroup-uniform
-        const uint64_t* cl = a.cl + pair * a.census_pair + (size_t)y * a.W;
-        const uint64_t* cr = a.cr + pair * a.census_pair + (size_t)y * a.W;
-        if (tid < nx) lc[tid] = cl[X0 + tid];
-        for (int i = tid; i < nx + D - 1; i += 256) rc[i] = cr[rlo + i];
+        if (tid < nx) lc[tid] = pl;
+        if (tid < nr) rc[tid] = pr0;
+        if (tid + 256 < nr) rc[256 + tid] = pr1;
+        if (r + 1 < C8_RY && y + 1 < a.H) fetch(y + 1);
         __syncthreads();  // also: the previous row's stores have read the tile
         if (xl < nx) {
             const uint64_t l = lc[xl];
@@ -491,7 +515,7 @@ __global__ void __launch_bounds__(256) k_sgbm_cost2(SgbmCost2Args a)
     uint2* Ub = reinterpret_cast<uint2*>(Ua + NHC);
     uint4* Qa = reinterpret_cast<uint4*>(Ub + ((NHC + 1) & ~1));
     uint2* Qb = reinterpret_cast<uint2*>(Qa + 2 * rph);
-    const int PP = NHC | 1;
+    const int PP = (CG * ((NHC + CG - 1) / CG)) | 1;  // odd, >= every thread's run end
     // two row buffers: BT of row r+1 may start while slower threads still sum row r
     uint32_t* const pix2 = reinterpret_cast<uint32_t*>(Qb + 2 * rph) + p * PP;
     const uint2* Lp = a.planes + (size_t)(pair * 2) * a.H * W;
@@ -560,7 +584,9 @@ __global__ void __launch_bounds__(256) k_sgbm_cost2(SgbmCost2Args a)
     const bool edge = hlo > 0 || hhi < NHC - 1;
     // BT work split: thread cg computes halo columns [hb0, hb1) of its pair p
     const int per = (NHC + CG - 1) / CG;
-    const int hb0 = max(cg * per, hlo), hb1 = min(cg * per + per, hhi + 1);
+    // (every thread computes its whole run: halo columns outside [hlo, hhi] hold clamped-edge
+    // garbage that the edge path of the horizontal sum never reads)
+    const int hb0 = cg * per;
     // right pair index of column hb0 (and hb0 + 1) -> parity-split LDS slots
     const int kk0 = (x0 - S + hb0) - xlo + D - 2 - 2 * p;
     const int q0 = (kk0 & 1) * rph + (kk0 >> 1), q1 = ((kk0 + 1) & 1) * rph + ((kk0 + 1) >> 1);
@@ -597,20 +623,42 @@ __global__ void __launch_bounds__(256) k_sgbm_cost2(SgbmCost2Args a)
                                                                    __builtin_elementwise_max(subsat(V3, U5), subsat(U4, V3)));
                         return as_u32(g + (rr >> (u16x2)2));
                     };
-                    // consecutive columns alternate the parity of their right pair index
-                    for (; hc + 1 < hb1; hc += 2) {
-                        const uint32_t e0 = bt(ua[0], ub[0], *qa0, *qb0);
-                        const uint32_t e1 = bt(ua[1], ub[1], *qa1, *qb1);
-                        pix[hc] = e0;
-                        pix[hc + 1] = e1;
-                        ua += 2;
-                        ub += 2;
-                        qa0++;
-                        qb0++;
-                        qa1++;
-                        qb1++;
+                    // consecutive columns alternate the parity of their right pair index;
+                    // unrolled to the longest run (immediate LDS offsets from six bases: the
+                    // rolled loop spent 17 address / counter ops per 32 BT ops)
+                    // a run of N = per columns, N known at compile time for per = CPT + 1 or
+                    // CPT + 2: groups of KG columns issue all their loads, then the BT ops, then
+                    // the stores (the compiler cannot move a load above a pix store: one LDS array)
+                    auto bt_run = [&](auto nc) {
+                        constexpr int N = decltype(nc)::value, KG = 2;
+#pragma unroll
+                        for (int j0 = 0; j0 < N; j0 += KG) {
+                            uint4 A[KG], Q[KG];
+                            uint2 B[KG], R[KG];
+#pragma unroll
+                            for (int k = 0; k < KG; k++) {
+                                const int j = j0 + k;
+                                if (j < N) {
+                                    A[k] = ua[j];
+                                    B[k] = ub[j];
+                                    Q[k] = (j & 1) ? qa1[j >> 1] : qa0[j >> 1];
+                                    R[k] = (j & 1) ? qb1[j >> 1] : qb0[j >> 1];
+                                }
+                            }
+#pragma unroll
+                            for (int k = 0; k < KG; k++)
+                                if (j0 + k < N) pix[hc + j0 + k] = bt(A[k], B[k], Q[k], R[k]);
+                        }
+                    };
+                    if (per == CPT + 1) {
+                        bt_run(std::integral_constant<int, CPT + 1>{});
+                    } else if (per == CPT + 2) {
+                        bt_run(std::integral_constant<int, CPT + 2>{});
+                    } else {
+                        for (int j = 0; j < per; j++)
+                            pix[hc + j] = (j & 1) ? bt(ua[j], ub[j], qa1[j >> 1], qb1[j >> 1])
+                                                  : bt(ua[j], ub[j], qa0[j >> 1], qb0[j >> 1]);
                     }
-                    if (hc < hb1) pix[hc] = bt(ua[0], ub[0], *qa0, *qb0);
                 }
                 __syncthreads();
                 // running horizontal sum along the thread's CPT columns (halo columns past
