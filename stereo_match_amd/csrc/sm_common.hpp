@@ -38,6 +38,22 @@ enum : int {
     DPP_ROW_BCAST31 = 0x143      // rows 2..3 <- lane 31
 };
 
+// OpenCV's sub-pixel step trunc(((Sm - Sq) * 16 + den) / (2 * den)), den = max(Sm + Sq - 2 minS, 1),
+// for Sm, Sq in [minS, minS + 65535]: the quotient lies in [-8, 8] and n, d < 2^24, so the f32
+// product n * rcp(d) is within 2.5e-6 of n / d (v_rcp_f32: 1 ulp), closer than any non-integer
+// quotient lies to an integer (1 / d >= 3.8e-6); an exact integer quotient may land one below
+// (toward zero), which the 24-bit remainder check corrects.  ~8 VALU ops instead of the ~25 of
+// the integer division; exhaustive over every (Sm - minS, Sq - minS) pair:
+// tools/ubench/subpix_exact.hip.
+__device__ __forceinline__ int subpix_step(int Sm, int Sq, int minS)
+{
+    const int den = max(Sm + Sq - 2 * minS, 1);
+    const int n = (Sm - Sq) * 16 + den, d = den * 2;
+    int q = (int)((float)n * __builtin_amdgcn_rcpf((float)d));  // v_cvt_i32_f32 truncates
+    const int rem = n - __mul24(q, d);
+    return q + (rem >= d ? 1 : 0) - (rem <= -d ? 1 : 0);
+}
+
 template <int CTRL>
 __device__ __forceinline__ uint32_t dpp(uint32_t old, uint32_t src)
 {

@@ -620,8 +620,7 @@ __device__ __forceinline__ void wta_packed_cols(const WtaArgs& a, const int y, c
             int d16;
             if (best > 0 && best < Dv - 1) {
                 const int Sm = sr[best - 1], Sq = sr[best + 1];
-                const int den = max(Sm + Sq - 2 * (int)minS, 1);
-                d16 = best * 16 + ((Sm - Sq) * 16 + den) / (den * 2);  // C truncation
+                d16 = best * 16 + subpix_step(Sm, Sq, (int)minS);  // C truncation
             } else {
                 d16 = best * 16;
             }
@@ -748,8 +747,7 @@ __device__ __forceinline__ void wta_row(const WtaArgs& a, const int y, const int
             int d16;
             if (best > 0 && best < a.Dv - 1) {
                 const int Sm = (int)(nb & 0xFFFF), Sq = (int)(nb >> 16);
-                const int den = max(Sm + Sq - 2 * minS, 1);
-                d16 = best * 16 + ((Sm - Sq) * 16 + den) / (den * 2);  // C truncation
+                d16 = best * 16 + subpix_step(Sm, Sq, minS);  // C truncation
             } else {
                 d16 = best * 16;
             }

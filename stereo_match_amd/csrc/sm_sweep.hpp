@@ -1753,8 +1753,7 @@ __global__ void __launch_bounds__(256) k_lr_rows(const uint32_t* __restrict__ re
             if (best > 0 && best < D - 1) {
                 const uint32_t nb = nbs[row + X];
                 const int Sm = (int)(nb & 0xFFFF), Sq = (int)(nb >> 16);
-                const int den = max(Sm + Sq - 2 * minS, 1);
-                d16 += ((Sm - Sq) * 16 + den) / (den * 2);  // C truncation
+                d16 += subpix_step(Sm, Sq, minS);  // C truncation
             }
             drow[X] = (int16_t)(d16 + minD * 16);
         }

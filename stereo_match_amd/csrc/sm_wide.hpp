@@ -279,8 +279,7 @@ __global__ void __launch_bounds__(NT) k_wide_wta(WideWtaArgs a)
             int d16 = best * 16;
             if (best > 0 && best < D - 1) {
                 const int Sm = (int)(nb & 0xFFFF) - 32768, Sq = (int)(nb >> 16) - 32768;
-                const int den = max(Sm + Sq - 2 * minS, 1);
-                d16 += ((Sm - Sq) * 16 + den) / (den * 2);  // C truncation
+                d16 += subpix_step(Sm, Sq, minS);  // C truncation
             }
             drow[X] = d16 + minD * 16;
             if (a.wta) brow[X] = (int16_t)best;
