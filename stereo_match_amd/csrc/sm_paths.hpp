@@ -520,15 +520,22 @@ struct WtaArgs {
 // and the uniqueness window (the fused sweep's form, sm_sweep.hpp), S[best -+ 1] from a row of
 // S in LDS.  Same decisions as wta_row's scalar loop (sgbm5 KITTI: 26 VALU lane-ops per cell
 // there, the kernel at full VALU issue).
-template <int DPL, typename LT, int NT, bool PART_ONLY>
+// the packed loop's row of S per 16-lane group (one LDS array for both PAD instances)
+template <int DPL, int NT>
+__device__ __forceinline__ uint16_t* wta_packed_srow(int grp)
+{
+    __shared__ __attribute__((aligned(16))) uint16_t srow[NT / 16][16 * DPL];
+    return &srow[grp][0];
+}
+
+template <int DPL, typename LT, int NT, bool PART_ONLY, bool PAD>
 __device__ __forceinline__ void wta_packed_cols(const WtaArgs& a, const int y, const int pair, uint32_t* key2, int* drow,
                                               int16_t* brow)
 {
     constexpr int NP = DPL / 2;
-    __shared__ __attribute__((aligned(16))) uint16_t srow[NT / 16][16 * DPL];
     const int D = a.D, minD = a.minD, minX1 = a.minX1, Dv = a.Dv;
     const int g = threadIdx.x & 15, grp = threadIdx.x >> 4;
-    const bool pad = Dv < D;
+    constexpr bool pad = PAD;  // Dv < D (a padded cost volume); a template parameter: no selects per word
     const int ku = 100 - a.uniq;
     uint32_t rk[DPL], padm[NP], dpk[NP];
 #pragma unroll
@@ -547,7 +554,7 @@ __device__ __forceinline__ void wta_packed_cols(const WtaArgs& a, const int y, c
     const size_t slot = a.slot_bytes / 2;
     const int nslots = sizeof(LT) == 2 && !PART_ONLY ? a.nslots : 0;
     constexpr int MS = PART_ONLY ? 1 : 4;  // slots in flight (the partial-only kernel keeps none)
-    uint16_t* sr = &srow[grp][0];
+    uint16_t* sr = wta_packed_srow<DPL, NT>(grp);
     auto ldw = [&](const uint16_t* src, uint32_t (&w)[NP]) {
         if constexpr (NP % 4 == 0) {
 #pragma unroll
@@ -566,9 +573,17 @@ __device__ __forceinline__ void wta_packed_cols(const WtaArgs& a, const int y, c
             for (int k = 0; k < NP; k++) w[k] = reinterpret_cast<const uint32_t*>(src)[k];
         }
     };
+    uint32_t tq[NP];  // partial-only: the next column's words, loaded one column ahead
+    if (PART_ONLY && grp < a.width1) ldw(P + (size_t)grp * D, tq);
     for (int x = grp; x < a.width1; x += NT / 16) {
         uint32_t Sp[NP], t[MS][NP], tp[NP];
-        if (P) ldw(P + (size_t)x * D, tp);
+        if constexpr (PART_ONLY) {
+#pragma unroll
+            for (int j = 0; j < NP; j++) tp[j] = tq[j];
+            if (x + NT / 16 < a.width1) ldw(P + (size_t)(x + NT / 16) * D, tq);
+        } else if (P) {
+            ldw(P + (size_t)x * D, tp);
+        }
 #pragma unroll
         for (int j = 0; j < NP; j++) Sp[j] = 0u;
         for (int k0 = 0; k0 < nslots; k0 += MS) {  // MS slots' loads in flight before their adds
@@ -653,10 +668,16 @@ __device__ __forceinline__ void wta_row(const WtaArgs& a, const int y, const int
     if constexpr (DPL % 2 == 0) {
         // the in-sweep lines' patched partial (PART_ONLY), or u16 direction volumes (+ partial)
         if constexpr (PART_ONLY) {
-            wta_packed_cols<DPL, LT, NT, true>(a, y, pair, key2, drow, brow);
+            if (a.Dv < a.D)
+                wta_packed_cols<DPL, LT, NT, true, true>(a, y, pair, key2, drow, brow);
+            else
+                wta_packed_cols<DPL, LT, NT, true, false>(a, y, pair, key2, drow, brow);
             goto tail;
         } else if (sizeof(LT) == 2 && DPL <= 12) {  // (block-uniform; DPL 14, 16: the scalar loop's registers)
-            wta_packed_cols<DPL, LT, NT, false>(a, y, pair, key2, drow, brow);
+            if (a.Dv < a.D)
+                wta_packed_cols<DPL, LT, NT, false, true>(a, y, pair, key2, drow, brow);
+            else
+                wta_packed_cols<DPL, LT, NT, false, false>(a, y, pair, key2, drow, brow);
             goto tail;
         }
     }
