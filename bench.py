@@ -359,8 +359,11 @@ class GpuWorkload:
         # ... with the horizontal paths inside the down sweep (sm_get_counter SM_COUNTER_LINE_GROUPS)
         self.lines = self.sweep and self.eng.counters()["line_groups"] > self._c0["line_groups"]
         self.P_dirs = 5 if args.mode in ("sgbm5", "disparity5") else 8
+        # strips per pair of the lines engine (SM_COUNTER_LINE_STRIPS over the profiled pairs)
+        c1 = self.eng.counters()
+        self.strips = (c1["line_strips"] - self._c0["line_strips"]) / max(1, n_prof * self.P) if self.lines else 0
         self.kern, cands = design_kernels(args, self.profile, self.H, self.W, self.D, self.p, self.P_dirs, self.sweep,
-                                          self.bm, self.lines)
+                                          self.bm, self.lines, self.strips)
         self.cands = cands
         # the dominant kernel is fixed per engine (the stage that moves the most bytes by design:
         # the WTA sweep, the per-direction path kernel), not picked by a timing race between
@@ -686,7 +689,7 @@ def run_rank(args, wl, world, rank):
         dist.destroy_process_group()
 
 
-def design_kernels(args, stages, H, W, D, p, P_dirs, sweep, bm, lines=False):
+def design_kernels(args, stages, H, W, D, p, P_dirs, sweep, bm, lines=False, strips=0):
     """The engine's own bytes per pair for each timed stage (what the kernels
     move by design), and the stages that can be the dominant kernel."""
     width1 = W - D  # minDisparity 0
@@ -697,7 +700,9 @@ def design_kernels(args, stages, H, W, D, p, P_dirs, sweep, bm, lines=False):
                 "wta": ("k_bm_sad (column sums in LDS + WTA)", H * W * (2 + 2 + 4))}, ("wta",)
     if sweep and lines:
         rec_b = 8 * H * width1
-        st = 4 * D * eb * H * ((width1 + 35) // 36)  # boundary states of the E/W segments (36-column strips)
+        # boundary states of the E/W segments: 2 directions x (entering, far end) per strip and row
+        # (strips per pair from SM_COUNTER_LINE_STRIPS; 36-column strips when not reported)
+        st = 4 * D * eb * H * (round(strips) if strips else (width1 + 35) // 36)
         kern = {"sweep": ("k_sweep MODE 3 (S+SE+SW + in-kernel E/W lines -> partial)", vol * eb + 2 * vol + st),
                 "horizontal": ("k_ew_patch (segment check + repairs)", st),
                 "sweep_wta": ("k_sweep MODE 4 (N+NE+NW + partial + WTA)", vol * eb + 2 * vol + rec_b) if P_dirs == 8

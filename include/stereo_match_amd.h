@@ -285,7 +285,10 @@ int sm_get_counters(sm_ctx* ctx, long long* sweep_fallbacks);
  *   SM_COUNTER_BAND_OPEN        of those, chains whose repair walk had not met the speculative
  *                               trajectory by the band's last row (it continued into the next
  *                               band);
- *   SM_COUNTER_BAND_GROUPS      launch groups that ran with row bands (host-side count). */
+ *   SM_COUNTER_BAND_GROUPS      launch groups that ran with row bands (host-side count);
+ *   SM_COUNTER_LINE_STRIPS      sweep strips x pairs of the LINE_GROUPS launch groups (host-side:
+ *                               divided by the pairs, the strips per pair, whose boundary states
+ *                               the patch pass reads). */
 #define SM_COUNTER_SWEEP_FALLBACKS 0
 #define SM_COUNTER_EW_REPAIRS 1
 #define SM_COUNTER_VOLUME_CLAMPED 2
@@ -295,6 +298,7 @@ int sm_get_counters(sm_ctx* ctx, long long* sweep_fallbacks);
 #define SM_COUNTER_BAND_REPAIRS 6
 #define SM_COUNTER_BAND_OPEN 7
 #define SM_COUNTER_BAND_GROUPS 8
+#define SM_COUNTER_LINE_STRIPS 9
 int sm_get_counter(sm_ctx* ctx, int which, long long* value);
 
 /* Restrict the context's own streams (the default stream and its internal
@@ -385,9 +389,9 @@ int sm_set_debug_flags(sm_ctx* ctx, int flags);
  *   SM_TUNE_EW_WAVES   waves per workgroup of the packed E/W lines: 0 automatic, 1..4.
  *   SM_TUNE_EW_PRIO    issue priority (s_setprio 0..3) of the packed E/W lines' waves.
  *   SM_TUNE_EW_WARMUP  columns each in-sweep E/W strip segment runs before its strip
- *                      (0 automatic: 16 census, 24 u16 costs; 1..4096; rounded up to the
- *                      line loop's load chunk).  Any value is exact (the patch pass repairs
- *                      segments that started wrong); large values cost line work.
+ *                      (0 automatic: 16; 54 for u16 costs in row bands; 1..4096; rounded up
+ *                      to the line loop's load chunk).  Any value is exact (the patch pass
+ *                      repairs segments that started wrong); large values cost line work.
  *   SM_TUNE_EW_GUESS   0 the segments start from the zero state; 1 (tests) from a
  *                      deliberately wrong state, so that nearly every segment is repaired.
  *   SM_TUNE_SWEEP_LINES the fused-sweep engine's horizontal paths: 0 automatic (inside the

@@ -445,7 +445,7 @@ class Engine:
         self._check(self._lib.sm_synchronize(self.ctx))
 
     COUNTERS = ("sweep_fallbacks", "ew_repairs", "volume_clamped", "volume_nan", "line_groups",
-                "ew_open", "band_repairs", "band_open", "band_groups")  # SM_COUNTER_*
+                "ew_open", "band_repairs", "band_open", "band_groups", "line_strips")  # SM_COUNTER_*
 
     def counters(self) -> dict:
         """Counters since the engine was created (include/stereo_match_amd.h SM_COUNTER_*):
@@ -453,7 +453,9 @@ class Engine:
         E/W strip segments the patch pass recomputed), volume_clamped / volume_nan (external
         cost-volume cells clamped by the quantisation window / NaN), line_groups (launch groups
         whose E/W paths ran inside the down sweep), ew_open (of the ew_repairs, segments whose
-        recomputation had not met the speculative values by the strip's end)."""
+        recomputation had not met the speculative values by the strip's end), band_repairs /
+        band_open / band_groups (the row-band engine's repaired chains, chains that crossed a
+        boundary, launch groups), line_strips (strips x pairs of the line_groups)."""
         out = {}
         n = ctypes.c_longlong()
         for i, name in enumerate(self.COUNTERS):

@@ -178,6 +178,7 @@ struct sm_ctx {
     int tune_sweep_xcd = 0;  // SM_TUNE_SWEEP_XCD: 1 the XCD-aware strip placement, -1 / 0 off
     long long line_groups = 0;  // launch groups run with the in-sweep E/W lines (SM_COUNTER_LINE_GROUPS)
     long long band_groups = 0;  // of them, with row bands (SM_COUNTER_BAND_GROUPS)
+    long long line_strips = 0;  // strips x pairs of those groups (SM_COUNTER_LINE_STRIPS)
     std::vector<TimedEvent> pending;
     std::vector<hipEvent_t> free_events;
     double stage_ms[SM_NUM_STAGES] = {0};
@@ -1127,7 +1128,10 @@ bool use_lines(sm_ctx* ctx, const Norm& n)
 int ew_warmup(const sm_ctx* ctx, const Norm& n)
 {
     if (ctx->tune_ew_warmup > 0) return ctx->tune_ew_warmup;
-    return elem_bytes(n) == 1 ? 16 : 24;
+    // 16 columns for both cost types (sgbm5, 8 pairs: 6520-6535 pairs/s at 16 against 6444-6469
+    // at 24, the patch pass's extra 4.5 us per pair below the sweep's 6 us saved)
+    (void)n;
+    return 16;
 }
 
 // largest value one path can take (normalize's domains): a 5-path sum of the banded engine must
@@ -1198,6 +1202,7 @@ int run_lines(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs, hipStream_t 
         ctx->band_groups++;
     }
     ctx->line_groups++;
+    ctx->line_strips += (long long)f.nwg * G;
     const bool fb_side = n.ndirs == 5 && ws == ctx->stream && !(ctx->dbg_flags & DBG_NO_FALLBACK);
     {
         StageTimer t(ctx, ctx->stream, SM_STAGE_PATHS, G);
@@ -3089,11 +3094,12 @@ int sm_get_counter(sm_ctx* ctx, int which, long long* value)
 {
     if (!ctx) return fail(nullptr, SM_E_ARG, "ctx is NULL");
     if (!value) return fail(ctx, SM_E_ARG, "value is NULL");
-    if (which < SM_COUNTER_SWEEP_FALLBACKS || which > SM_COUNTER_BAND_GROUPS)
+    if (which < SM_COUNTER_SWEEP_FALLBACKS || which > SM_COUNTER_LINE_STRIPS)
         return fail(ctx, SM_E_ARG, "unknown counter %d", which);
     long long v = 0;
-    if (which == SM_COUNTER_LINE_GROUPS || which == SM_COUNTER_BAND_GROUPS) {
-        v = which == SM_COUNTER_LINE_GROUPS ? ctx->line_groups : ctx->band_groups;
+    if (which == SM_COUNTER_LINE_GROUPS || which == SM_COUNTER_BAND_GROUPS || which == SM_COUNTER_LINE_STRIPS) {
+        v = which == SM_COUNTER_LINE_GROUPS ? ctx->line_groups
+            : which == SM_COUNTER_BAND_GROUPS ? ctx->band_groups : ctx->line_strips;
     } else if (ctx->sweep_err.p) {
         HIP_TRY(ctx, hipSetDevice(ctx->device));
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));

@@ -201,7 +201,7 @@ def test_lines_tuning_arguments(eng):
         eng.set_tuning(eng.TUNE_EW_GUESS, 2)
     c = eng.counters()
     assert set(c) == {"sweep_fallbacks", "ew_repairs", "volume_clamped", "volume_nan", "line_groups", "ew_open",
-                      "band_repairs", "band_open", "band_groups"}
+                      "band_repairs", "band_open", "band_groups", "line_strips"}
 
 
 # ------------------------------------------------------------------ mc-cnn quantisation window

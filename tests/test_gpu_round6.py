@@ -288,3 +288,20 @@ def test_sweep_xcd_placement(eng, cost, mode, n):
     exp = ref_c.compute_many(pairs, p)
     for i in range(n):
         assert np.array_equal(got[i], exp[i]), (i, int(np.sum(got[i] != exp[i])))
+
+
+def test_line_strips_counter(eng):
+    """SM_COUNTER_LINE_STRIPS: a KITTI census8 call on the lines engine adds its strips x pairs
+    (the bench's boundary-state bytes use it), and nothing for a per-direction call."""
+    H, W, _ = synthetic.CONFIGS["kitti"]
+    left, right, _ = synthetic.random_dot_pair(H, W, 128, seed=3401)
+    p = synthetic.headline_params(128)
+    c0 = eng.counters()
+    _run(eng, left, right, p, flags=SWEEP8)
+    c1 = eng.counters()
+    assert c1["line_groups"] == c0["line_groups"] + 1
+    strips = c1["line_strips"] - c0["line_strips"]
+    # strips of a 1114-column domain: at most 36 columns wide (the wide instance), at least 8
+    assert 31 <= strips <= 140, strips
+    _run(eng, left, right, p, flags=4096)  # per-direction engine
+    assert eng.counters()["line_strips"] == c1["line_strips"]
