@@ -125,8 +125,10 @@ __global__ void __launch_bounds__(256) k_ew(EwArgs a)
 #ifndef EW_PATCH_B64
 #define EW_PATCH_B64 1  // phase B's carried walks on 64-lane lines where D % 128 == 0
 #endif
+// (0: by cost type — census 8, u16 16: census8 E/W patch 6.9 -> 6.4 us per pair at 8, 9.5 at 32;
+// sgbm5 17.6 at 16, 20.0 at 8, 21.5 at 32)
 #ifndef EW_PATCH_RC
-#define EW_PATCH_RC 16
+#define EW_PATCH_RC 0
 #endif
 // ---------------------------------------------------------------------------
 // Patch pass after a MODE 3 sweep (sm_sweep.hpp line waves).  Strip k's E line
@@ -161,7 +163,7 @@ __global__ void __launch_bounds__(256) k_ew_patch(EwPatchArgs a)
     // chunk of LPW * KU path positions, all loads of a chunk in flight together
     constexpr int KU = 8;
     constexpr int CHUNK = LPW * KU;
-    constexpr int RC = EW_PATCH_RC;  // columns of a repaired segment loaded together
+    constexpr int RC = EW_PATCH_RC ? EW_PATCH_RC : sizeof(CT) == 1 ? 8 : 16;  // columns of a repaired segment loaded together
     if (a.guard && __hip_atomic_load(a.guard, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int g = lane % VL, kl = lane / VL;
