@@ -85,6 +85,11 @@ struct BufSet {
     bool pending = false;  // wta_done recorded and not yet waited for by stream A
 };
 
+// the E/W patch pass with atomic corrections where no partial cell can saturate (k_ew_patch ATOM)
+#ifndef EW_PATCH_ATOM
+#define EW_PATCH_ATOM 1
+#endif
+
 // debug flags (sm_set_debug_flags); 1 skip horizontal, 2 skip vertical and 4 drop stores are read in-kernel
 constexpr int DBG_VL16 = 8, DBG_STORE_W = 16, DBG_ROW = 32, DBG_OVERLAP = 64, DBG_H64 = 512, DBG_NO_C8 = 1024;
 // 256: the sweep engine's E/W volumes from the per-direction engine's row lines instead of
@@ -157,6 +162,7 @@ struct sm_ctx {
     uint32_t hop_epoch = 0;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;  // sweep engine: E/W kernel on the side stream
     hipEvent_t ev_fb_fork = nullptr, ev_fb_join = nullptr;  // sweep engine: fallback beside the LR pass
+    hipEvent_t ev_ew_done = nullptr;  // banded lines: the E/W patch on the side stream (before the WTA)
     const uint32_t* fb_guard = nullptr;  // set while enqueuing a group's guarded per-direction fallback
     hipStream_t wta_override = nullptr;  // stream of the WTA launch when it is not stream_b()
     const uint32_t* wta_skip = nullptr;  // the WTA row kernel exits when this flag is set (WtaArgs::skip)
@@ -1214,27 +1220,6 @@ int run_lines(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs, hipStream_t 
             HIP_TRY(ctx, hipEventRecord(ctx->sweep_done_ev, ctx->stream));
             ctx->sweep_done_hit = true;
         }
-        if (fb_side) {
-            // 5 paths: the group flag is final after the sweep, so the guarded per-direction
-            // fallback (two launches that exit at once unless a strip gave up) runs on the side
-            // stream beside the patch passes and the WTA row kernel, which writes nothing when
-            // the flag is set: the fallback's launch latency leaves the critical path
-            if (ctx->dbg_flags & DBG_FORCE_FALLBACK) HIP_TRY(ctx, hipMemsetAsync(gflag, 1, 1, ctx->stream));
-            if ((rc = ensure_event(ctx, ctx->ev_fb_fork)) != SM_OK) return rc;
-            if ((rc = ensure_event(ctx, ctx->ev_fb_join)) != SM_OK) return rc;
-            HIP_TRY(ctx, hipEventRecord(ctx->ev_fb_fork, ctx->stream));
-            HIP_TRY(ctx, hipStreamWaitEvent(ctx->side, ctx->ev_fb_fork, 0));
-            StreamSwap sw(ctx, ctx->side);
-            ctx->wta_override = ctx->side;
-            ctx->fb_guard = gflag;
-            rc = dispatch(ctx, n, g, bs, DISPATCH_PATHS);
-            if (rc == SM_OK) rc = dispatch(ctx, n, g, bs, DISPATCH_WTA);
-            ctx->fb_guard = nullptr;
-            ctx->wta_override = nullptr;
-            if (rc != SM_OK) return rc;
-            HIP_TRY(ctx, hipEventRecord(ctx->ev_fb_join, ctx->side));
-        }
-        StageTimer th(ctx, ctx->stream, SM_STAGE_HORIZONTAL, G);
         smk::EwPatchArgs pa{};
         pa.cost = j.cost;
         pa.cost_pair = j.cost_pair;
@@ -1250,9 +1235,50 @@ int run_lines(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs, hipStream_t 
         pa.P2 = n.P2;
         pa.guard = gflag;
         pa.fixes = reinterpret_cast<unsigned long long*>((uint32_t*)ctx->sweep_err.p + ERR_EW_REPAIRS);
-        const hipError_t e = smk::ew_patch_launch(n.D, (int)et, pa, G, ctx->stream);
-        if (e == hipErrorInvalidValue) return fail(ctx, SM_E_UNSUPPORTED, "E/W patch: numDisparities %d not built", n.D);
-        HIP_TRY(ctx, e);
+        // u16 costs where no partial cell can saturate: atomic corrections, E and W side by side
+        // (sm_ew.hpp ATOM; sgbm5 8 pairs: patch 17.6 -> 15.2 us per pair; census8: 6.9 -> 7.5)
+        pa.atom = EW_PATCH_ATOM && et == 2 && 5 * path_max(n) < 65536 ? 1 : 0;
+        auto ew_patch = [&](hipStream_t st) -> int {
+            const hipError_t e = smk::ew_patch_launch(n.D, (int)et, pa, G, st);
+            if (e == hipErrorInvalidValue) return fail(ctx, SM_E_UNSUPPORTED, "E/W patch: numDisparities %d not built", n.D);
+            HIP_TRY(ctx, e);
+            return SM_OK;
+        };
+        // with row bands and atomic corrections the E/W patch runs on the side stream beside the
+        // band patch (both only add to the partial), ahead of the guarded fallback there
+        const bool ew_side = fb_side && pa.atom && j.nband > 1;
+        if (fb_side) {
+            // 5 paths: the group flag is final after the sweep, so the guarded per-direction
+            // fallback (two launches that exit at once unless a strip gave up) runs on the side
+            // stream beside the patch passes and the WTA row kernel, which writes nothing when
+            // the flag is set: the fallback's launch latency leaves the critical path
+            if (ctx->dbg_flags & DBG_FORCE_FALLBACK) HIP_TRY(ctx, hipMemsetAsync(gflag, 1, 1, ctx->stream));
+            if ((rc = ensure_event(ctx, ctx->ev_fb_fork)) != SM_OK) return rc;
+            if ((rc = ensure_event(ctx, ctx->ev_fb_join)) != SM_OK) return rc;
+            HIP_TRY(ctx, hipEventRecord(ctx->ev_fb_fork, ctx->stream));
+            HIP_TRY(ctx, hipStreamWaitEvent(ctx->side, ctx->ev_fb_fork, 0));
+            if (ew_side) {
+                if ((rc = ensure_event(ctx, ctx->ev_ew_done)) != SM_OK) return rc;
+                {
+                    StageTimer th(ctx, ctx->side, SM_STAGE_HORIZONTAL, G);
+                    if ((rc = ew_patch(ctx->side)) != SM_OK) return rc;
+                }
+                HIP_TRY(ctx, hipEventRecord(ctx->ev_ew_done, ctx->side));
+            }
+            StreamSwap sw(ctx, ctx->side);
+            ctx->wta_override = ctx->side;
+            ctx->fb_guard = gflag;
+            rc = dispatch(ctx, n, g, bs, DISPATCH_PATHS);
+            if (rc == SM_OK) rc = dispatch(ctx, n, g, bs, DISPATCH_WTA);
+            ctx->fb_guard = nullptr;
+            ctx->wta_override = nullptr;
+            if (rc != SM_OK) return rc;
+            HIP_TRY(ctx, hipEventRecord(ctx->ev_fb_join, ctx->side));
+        }
+        if (!ew_side) {
+            StageTimer th(ctx, ctx->stream, SM_STAGE_HORIZONTAL, G);
+            if ((rc = ew_patch(ctx->stream)) != SM_OK) return rc;
+        }
         if (j.nband > 1) {  // then the vertical chains at the band boundaries (after: both touch the partial)
             smk::BandPatchArgs ba{};
             ba.cost = j.cost;
@@ -1273,6 +1299,8 @@ int run_lines(sm_ctx* ctx, const Norm& n, const Geo& g, BufSet& bs, hipStream_t 
             const hipError_t eb = smk::band_patch_launch(n.D, (int)et, ba, G, ctx->stream);
             if (eb == hipErrorInvalidValue) return fail(ctx, SM_E_UNSUPPORTED, "band patch: numDisparities %d not built", n.D);
             HIP_TRY(ctx, eb);
+            // the WTA reads the partial both patches correct (the fallback's join comes after it)
+            if (ew_side) HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_ew_done, 0));
         }
     }
     if (ws != ctx->stream) {
@@ -2449,6 +2477,7 @@ void sm_destroy(sm_ctx* ctx)
     if (ctx->ev_stagger) (void)hipEventDestroy(ctx->ev_stagger);
     if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
     if (ctx->ev_fb_fork) (void)hipEventDestroy(ctx->ev_fb_fork);
+    if (ctx->ev_ew_done) (void)hipEventDestroy(ctx->ev_ew_done);
     if (ctx->ev_fb_join) (void)hipEventDestroy(ctx->ev_fb_join);
     if (ctx->side) (void)hipStreamDestroy(ctx->side);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);

@@ -71,8 +71,11 @@ namespace {
 template <int VL, int NP, typename CT>
 hipError_t run_patch(const EwPatchArgs& a, int npairs, hipStream_t stream)
 {
-    // one wave per image row, four rows per workgroup
-    hipLaunchKernelGGL((k_ew_patch<VL, NP, CT>), dim3((a.H + 3) / 4, npairs), dim3(256), 0, stream, a);
+    // one wave per image row (atomic corrections: per row and direction), four per workgroup
+    if (a.atom)
+        hipLaunchKernelGGL((k_ew_patch<VL, NP, CT, true>), dim3((2 * a.H + 3) / 4, npairs), dim3(256), 0, stream, a);
+    else
+        hipLaunchKernelGGL((k_ew_patch<VL, NP, CT, false>), dim3((a.H + 3) / 4, npairs), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
 

@@ -151,7 +151,11 @@ __global__ void __launch_bounds__(256) k_ew(EwArgs a)
 // u16 costs: the MODE 3 partial saturates at 0xFFFF; a cell below that holds the exact sum
 // (every term >= 0), one at 0xFFFF stays there (the true five-path sum is then still
 // >= 65535 - 2 * 16383 > 32767, so the WTA's 32767 clamp sees the same value).
-template <int VL, int NP, typename CT>
+// ATOM (the host's choice where 5 x path_max < 65536, so no partial cell saturates): the
+// corrections are u32 atomic adds of (true - applied) per u16 pair as one signed addend, exact
+// in any order while every half stays a valid sum (band patch argument), so the partial is never
+// read and E and W of a row run in two waves side by side (twice the waves, no E -> W order).
+template <int VL, int NP, typename CT, bool ATOM = false>
 __global__ void __launch_bounds__(256) k_ew_patch(EwPatchArgs a)
 {
     constexpr int LPW = 64 / VL, DPL = 2 * NP, D = VL * DPL;
@@ -167,13 +171,23 @@ __global__ void __launch_bounds__(256) k_ew_patch(EwPatchArgs a)
     if (a.guard && __hip_atomic_load(a.guard, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int g = lane % VL, kl = lane / VL;
-    const int y = (int)blockIdx.x * 4 + wave;  // one wave per image row (wave-uniform)
+    const int yw = (int)blockIdx.x * 4 + wave;  // one wave per image row (ATOM: per row and direction)
+    const int y = ATOM ? yw >> 1 : yw;           // (wave-uniform)
+    const int dir0 = ATOM ? (yw & 1) : 0, dir1 = ATOM ? dir0 + 1 : 2;
     const size_t pair = blockIdx.y;
     const int H = a.H, W1 = a.W1, nwg = a.nwg, CW = a.cw;
     if (y >= H) return;
     const uint64_t cells = (uint64_t)H * W1 * D;
     const rsrc_t rc = make_rsrc(a.cost + pair * a.cost_pair, cells * sizeof(CT));
     const rsrc_t rp = make_rsrc((const uint8_t*)a.part + pair * a.part_pair, cells * 2);
+    uint32_t* const pw = reinterpret_cast<uint32_t*>((uint8_t*)a.part + pair * a.part_pair);  // (ATOM)
+    // (second - first) per u16 half as one signed 32-bit addend, added atomically where nonzero
+    auto atom_add = [&](uint32_t word, uint32_t first, uint32_t second) {
+        const int lo = (int)(second & 0xFFFFu) - (int)(first & 0xFFFFu);
+        const int hi = (int)(second >> 16) - (int)(first >> 16);
+        const uint32_t add = (uint32_t)(hi * 65536 + lo);
+        if (add) __hip_atomic_fetch_add(pw + word, add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
     const rsrc_t rs = make_rsrc(a.st + pair * a.st_pair, a.st_pair);
     const uint32_t P1p = (uint32_t)a.P1 * 0x10001u, P2p = (uint32_t)a.P2 * 0x10001u;
     const uint32_t eL = g == 0 ? EDGE : 0u, eR = g == VL - 1 ? EDGE : 0u;
@@ -216,7 +230,7 @@ __global__ void __launch_bounds__(256) k_ew_patch(EwPatchArgs a)
         auto issue1 = [&](int u, int o) {  // slot u <- column o of the walk
             const int c = dir ? x0 + CW - 1 - o : x0 + o;
             cc[u].load(rc, o < ncol ? cell(c) * (uint32_t)sizeof(CT) : kOOB);
-            pb[u].load(rp, o < ncol ? cell(c) * 2u : kOOB);
+            if constexpr (!ATOM) pb[u].load(rp, o < ncol ? cell(c) * 2u : kOOB);
         };
         auto issue = [&](int o0) {
 #pragma unroll
@@ -246,7 +260,7 @@ __global__ void __launch_bounds__(256) k_ew_patch(EwPatchArgs a)
                 uint32_t C2[2][NP], Ln[2][NP], mn[2], pv_[NP];
                 unpack_ct_pk<CT, DPL>(cc[u], C2[0]);
 #pragma unroll
-                for (int q = 0; q < NP; q++) pv_[q] = pb[u].w[q];
+                for (int q = 0; q < NP; q++) pv_[q] = ATOM ? 0u : pb[u].w[q];
 #pragma unroll
                 for (int q = 0; q < NP; q++) C2[1][q] = C2[0][q];
                 sweep_step2n<VL, NP, H16, 2>(Lq, mq, C2, P1p, P2p, eL, eR, Ln, mn);
@@ -254,9 +268,13 @@ __global__ void __launch_bounds__(256) k_ew_patch(EwPatchArgs a)
                     met = true;
                     continue;
                 }
+                if constexpr (ATOM) {
+#pragma unroll
+                    for (int q = 0; q < NP; q++) atom_add(cell(c) / 2u + (uint32_t)q, Ln[0][q], Ln[1][q]);
+                }
                 uint32_t P[NP];
 #pragma unroll
-                for (int q = 0; q < NP; q++) {
+                for (int q = 0; q < NP && !ATOM; q++) {
                     if constexpr (SAT) {
                         // a half pv < 0xFFFF is the exact sum, pv >= sv: (pv - sv) + tv saturating;
                         // pv == 0xFFFF stays (sat: 0xFFFF exactly there, from pv + 1 wrapping to 0)
@@ -268,7 +286,7 @@ __global__ void __launch_bounds__(256) k_ew_patch(EwPatchArgs a)
                         P[q] = pk_add(pk_sub(pv_[q], Ln[0][q]), Ln[1][q]);
                     }
                 }
-                bstore_n<uint32_t, NP>(rp, cell(c) * 2u, P);
+                if constexpr (!ATOM) bstore_n<uint32_t, NP>(rp, cell(c) * 2u, P);
 #pragma unroll
                 for (int q = 0; q < NP; q++) {
                     Lq[0][q] = Ln[0][q];
@@ -322,7 +340,7 @@ __global__ void __launch_bounds__(256) k_ew_patch(EwPatchArgs a)
         auto issue1 = [&](int u, int o) {  // slot u <- column o of the walk
             const int c = dir ? x0 + CW - 1 - o : x0 + o;
             cc[u].load(rc, o < ncol ? cell64(c) * (uint32_t)sizeof(CT) : kOOB);
-            pb[u].load(rp, o < ncol ? cell64(c) * 2u : kOOB);
+            if constexpr (!ATOM) pb[u].load(rp, o < ncol ? cell64(c) * 2u : kOOB);
         };
         auto issue = [&](int o0) {
 #pragma unroll
@@ -352,7 +370,7 @@ __global__ void __launch_bounds__(256) k_ew_patch(EwPatchArgs a)
                 uint32_t C2[2][NPW], Ln[2][NPW], mn[2], pv_[NPW];
                 unpack_ct_pk<CT, DPLW>(cc[u], C2[0]);
 #pragma unroll
-                for (int q = 0; q < NPW; q++) pv_[q] = pb[u].w[q];
+                for (int q = 0; q < NPW; q++) pv_[q] = ATOM ? 0u : pb[u].w[q];
 #pragma unroll
                 for (int q = 0; q < NPW; q++) C2[1][q] = C2[0][q];
                 sweep_step2n<64, NPW, H16, 2>(Lq, mq, C2, P1p, P2p, 0u, 0u, Ln, mn);
@@ -360,9 +378,13 @@ __global__ void __launch_bounds__(256) k_ew_patch(EwPatchArgs a)
                     met = true;
                     continue;
                 }
+                if constexpr (ATOM) {
+#pragma unroll
+                    for (int q = 0; q < NPW; q++) atom_add(cell64(c) / 2u + (uint32_t)q, Ln[0][q], Ln[1][q]);
+                }
                 uint32_t P[NPW];
 #pragma unroll
-                for (int q = 0; q < NPW; q++) {
+                for (int q = 0; q < NPW && !ATOM; q++) {
                     if constexpr (SAT) {
                         // a half pv < 0xFFFF is the exact sum, pv >= sv: (pv - sv) + tv saturating;
                         // pv == 0xFFFF stays (sat: 0xFFFF exactly there, from pv + 1 wrapping to 0)
@@ -374,7 +396,7 @@ __global__ void __launch_bounds__(256) k_ew_patch(EwPatchArgs a)
                         P[q] = pk_add(pk_sub(pv_[q], Ln[0][q]), Ln[1][q]);
                     }
                 }
-                bstore_n<uint32_t, NPW>(rp, cell64(c) * 2u, P);
+                if constexpr (!ATOM) bstore_n<uint32_t, NPW>(rp, cell64(c) * 2u, P);
 #pragma unroll
                 for (int q = 0; q < NPW; q++) {
                     Lq[0][q] = Ln[0][q];
@@ -410,7 +432,7 @@ __global__ void __launch_bounds__(256) k_ew_patch(EwPatchArgs a)
     // phase A's open strips (walk never met), one bit per path position i >= 1
     __shared__ uint64_t openm[4][kPatchMaxChunks];
     uint32_t nfix = 0, nopen = 0;  // walks (per line), open strips (wave-uniform)
-    for (int dir = 0; dir < 2; dir++) {  // 0 = E (strips in x order), 1 = W (reverse)
+    for (int dir = dir0; dir < dir1; dir++) {  // 0 = E (strips in x order), 1 = W (reverse)
         auto strip_of = [&](int i) { return dir ? nwg - 1 - i : i; };  // path position -> strip
         int first_open = nwg;  // wave-uniform
         for (int i0 = 1, ch = 0; i0 < nwg; i0 += CHUNK, ch++) {
@@ -504,7 +526,7 @@ __global__ void __launch_bounds__(256) k_ew_patch(EwPatchArgs a)
                 }
             }
         }
-        if (dir == 0) order_partial();  // W touches the cells E wrote
+        if (!ATOM && dir == 0) order_partial();  // W touches the cells E wrote
     }
     if (a.fixes) {
         nfix = group_sum_u32_wave(g == 0 ? nfix : 0u);  // every line's walks

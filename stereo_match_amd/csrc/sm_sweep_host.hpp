@@ -179,6 +179,7 @@ struct EwPatchArgs {
     int H, W1, nwg, cw, P1, P2;
     const uint32_t* guard;  // the group's give-up flag: nothing to patch when set (the fallback recomputes)
     unsigned long long* fixes;  // [0] strip segments recomputed, [1] of them never met within the strip (u64 atomics)
+    int atom;  // 1: no partial cell can saturate (5 x path_max < 65536): atomic corrections, E and W side by side
 };
 // Vertical patch after a banded MODE 3 sweep (sm_ew.hpp k_band_patch): each
 // column's S / SE / SW state entering a band (speculative, from the band's warmup rows) is checked
