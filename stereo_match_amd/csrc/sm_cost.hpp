@@ -256,10 +256,21 @@ __global__ void __launch_bounds__(256) k_sgbm_prefilter(PrefilterArgs a)
     const int x0 = blockIdx.x * 256, y0 = blockIdx.y * PF_ROWS, im = view & 1, pair = view >> 1;
     const int W = a.W, H = a.H, ft = a.ftzero, tid = threadIdx.x;
     const uint8_t* img = a.img[im] + (size_t)pair * a.in_pair + ch;
+    // every byte load in flight before the first LDS write (a load -> wait -> write loop
+    // serialises a memory round trip per staged row)
+    uint32_t st0[PF_ROWS + 2], st1[PF_ROWS + 2];
+    const size_t cx0 = (size_t)min(max(x0 - 2 + tid, 0), W - 1) * cn;
+    const size_t cx1 = (size_t)min(max(x0 + 254 + tid, 0), W - 1) * cn;  // columns 256..259 (tid < 4)
 #pragma unroll
     for (int r = 0; r < PF_ROWS + 2; r++) {
         const uint8_t* row = img + (size_t)min(max(y0 - 1 + r, 0), H - 1) * a.stride;
-        for (int c = tid; c < 260; c += 256) rows[r][c] = row[(size_t)min(max(x0 - 2 + c, 0), W - 1) * cn];
+        st0[r] = row[cx0];
+        if (tid < 4) st1[r] = row[cx1];
+    }
+#pragma unroll
+    for (int r = 0; r < PF_ROWS + 2; r++) {
+        rows[r][tid] = (uint8_t)st0[r];
+        if (tid < 4) rows[r][256 + tid] = (uint8_t)st1[r];
     }
     __syncthreads();
 #pragma unroll
